@@ -1,0 +1,455 @@
+// Causal flash attention forward / backward for head_dim 64 on gfx950.
+//
+// Layout: the QKV GEMM output is consumed in place, qkv = [B, S, 3, H, 64]
+// (row stride 3·H·64 between positions); o = [B, S, H, 64]; lse = [B, H, S].
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 throughout (one wave = 32 rows).
+// Forward (FA2 structure, one workgroup = 4 waves = 128 queries of one (b,h)):
+//   S^T = K·Q^T with the query on the lane, so the online-softmax row
+//   statistics are lane-local (one cross-half exchange for the max), and the
+//   S^T accumulator is directly the B operand of O^T = V^T·P^T (no LDS round
+//   trip for P; k order permuted as in cdna_hip_programming.md §3).  V^T
+//   fragments come from ds_read_b64_tr_b16 transposed LDS reads.
+// Backward: two kernels without atomics.
+//   dK/dV: workgroup = 128 keys (32 per wave, key on the lane), S and dP are
+//     computed as [q × key] so P and dS are the B operands of dV^T = dO^T·P
+//     and dK^T = Q^T·dS; Q / dO tiles stream through LDS.
+//   dQ:   workgroup = 128 queries, S^T / dP^T with the query on the lane,
+//     dQ^T = K^T·dS^T; K / V tiles stream through LDS.
+// LDS tiles are [64 rows][64 bf16] with one XOR swizzle of the 16-B chunk
+// index, chosen so BOTH the row reads (ds_read_b128, 16 rows per lane group)
+// and the transposed reads (4 rows × 64 B per half-wave) are conflict-free.
+#include <math.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+constexpr int HD = 64;     // head dim
+constexpr int TROWS = 64;  // rows per LDS tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+// element offset of (row r, 16-B chunk ch) in a swizzled [64][64] bf16 tile
+__device__ __forceinline__ int toff(int r, int ch) { return r * HD + ((ch ^ swz(r)) << 3); }
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// row fragment: lane reads row (rbase + lane&31), chunk (2ks + lane>>5)
+__device__ __forceinline__ bf16x8 row_frag(const bf16* T, int rbase, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8*>(T + toff(rbase + (lane & 31), 2 * ks + (lane >> 5)));
+}
+
+// transposed fragment: A[row = cbase + lane&31][k permuted] = T[k0 + 8(j>>2) + 4hh + (j&3)][cbase + lane&31]
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* T, int k0, int cbase, int lane) {
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  const int col = cbase + 16 * (g & 1) + 4 * p;
+  const int r0 = k0 + 4 * (g >> 1) + q;
+  const int ch = col >> 3, in = col & 7;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(T + toff(r0, ch) + in));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(T + toff(r0 + 8, ch) + in));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// 8 accumulator registers [8s, 8s+8) → bf16 B-operand fragment
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
+  return r;
+}
+
+// ----- global → register → LDS staging of a [64 rows][64] tile (256 threads) -----
+struct Stage {
+  bf16x8 v[2];
+};
+
+__device__ __forceinline__ void stage_load(Stage& st, const bf16* base, size_t row_stride, int row0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    st.v[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(row0 + r) * row_stride + ch * 8);
+  }
+}
+
+__device__ __forceinline__ void stage_store(const Stage& st, bf16* T, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *reinterpret_cast<bf16x8*>(T + toff(r, ch)) = st.v[i];
+  }
+}
+
+// store a 32x32 f32 accumulator (lane col = row index `rowv`, regs = 32 columns
+// starting at c0) as bf16 into dst[rowv][c0 + ...] with scale
+__device__ __forceinline__ void store_acc_rows(bf16* dst_row, const f32x16& acc, int c0, int hh, float s) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bf16x4 v = {(bf16)(acc[4 * g] * s), (bf16)(acc[4 * g + 1] * s), (bf16)(acc[4 * g + 2] * s),
+                (bf16)(acc[4 * g + 3] * s)};
+    *reinterpret_cast<bf16x4*>(dst_row + c0 + 8 * g + 4 * hh) = v;
+  }
+}
+
+// ============================================================================
+// forward
+// ============================================================================
+__global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                    float* __restrict__ lse, int B, int S, int H, float c2) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int nqb = S / 128;
+  const int bh = blockIdx.x % (B * H);
+  const int qb = nqb - 1 - blockIdx.x / (B * H);  // heaviest query blocks first
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;  // row stride (elements) between positions
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+
+  const int q = qb * 128 + w * 32 + li;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
+
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = -INFINITY, l = 0.f;
+  const int ntiles = (qb * 128 + 128) / TROWS;
+  const int wave_qmax = qb * 128 + w * 32 + 31;
+
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store(sv, smem + TROWS * HD, tid);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
+    const bf16* Vt = Kt + TROWS * HD;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    }
+    const int key0 = t * TROWS;
+    if (key0 <= wave_qmax) {
+      f32x16 s0 = zero16(), s1 = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
+        s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
+      }
+      const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hh;
+        float a = s0[r] * c2, bb = s1[r] * c2;
+        if (diag) {
+          if (key0 + kr > q) a = -INFINITY;
+          if (key0 + 32 + kr > q) bb = -INFINITY;
+        }
+        s0[r] = a;
+        s1[r] = bb;
+        tmax = fmaxf(tmax, fmaxf(a, bb));
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mn);
+      m = mn;
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = exp2f(s0[r] - mn);
+        s1[r] = exp2f(s1[r] - mn);
+        ls += s0[r] + s1[r];
+      }
+      l = l * alpha + ls;
+      o0 *= alpha;
+      o1 *= alpha;
+#pragma unroll
+      for (int sst = 0; sst < 2; ++sst) {
+        const bf16x8 p0 = pack8(s0, sst), p1 = pack8(s1, sst);
+        o0 = mfma(tr_frag(Vt, 16 * sst, 0, lane), p0, o0);
+        o1 = mfma(tr_frag(Vt, 16 * sst, 32, lane), p0, o1);
+        o0 = mfma(tr_frag(Vt, 32 + 16 * sst, 0, lane), p1, o0);
+        o1 = mfma(tr_frag(Vt, 32 + 16 * sst, 32, lane), p1, o1);
+      }
+    }
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / lt;
+  bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
+  store_acc_rows(orow, o0, 0, hh, inv);
+  store_acc_rows(orow, o1, 32, hh, inv);
+  if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
+}
+
+// ============================================================================
+// backward: delta = rowsum(dO ∘ O)   (one thread per 8 elements, 8 lanes per row)
+// ============================================================================
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ o,
+                                                         float* __restrict__ delta, int B, int S, int H) {
+  const long long gid = blockIdx.x * 256LL + threadIdx.x;
+  const long long row = gid >> 3;  // (b, s, h) row
+  const int part = gid & 7;
+  const long long nrows = (long long)B * S * H;
+  float acc = 0.f;
+  if (row < nrows) {
+    f32x8 a = to_f32(reinterpret_cast<const bf16x8*>(dout + row * HD)[part]);
+    f32x8 c = to_f32(reinterpret_cast<const bf16x8*>(o + row * HD)[part]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (row < nrows && part == 0) {
+    const int h = row % H;
+    const long long bs = row / H;
+    const int s = bs % S, b = bs / S;
+    delta[((size_t)b * H + h) * S + s] = acc;
+  }
+}
+
+// ============================================================================
+// backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
+// ============================================================================
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                         const float* __restrict__ lse, const float* __restrict__ delta,
+                                                         bf16* __restrict__ dqkv, int B, int S, int H, float c2,
+                                                         float scale) {
+  // [buf][Q|dO][64][64] bf16 + [buf][lse2|delta][64] f32
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD + 2 * 2 * TROWS * 2];
+  float* sstat = reinterpret_cast<float*>(smem + 2 * 2 * TROWS * HD);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int nkb = S / 128;
+  const int bh = blockIdx.x % (B * H);
+  const int kb = blockIdx.x / (B * H);  // lowest key blocks have the most query tiles: issue first
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;
+  const size_t ors = (size_t)H * HD;
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+  const bf16* dobase = dout + (size_t)b * S * ors + (size_t)h * HD;
+  const float* lse_bh = lse + (size_t)bh * S;
+  const float* del_bh = delta + (size_t)bh * S;
+  (void)nkb;
+
+  const int key = kb * 128 + w * 32 + li;  // this lane's key (column of S / dP)
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)key * rs + 16 * ks + 8 * hh);
+    vf[ks] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)key * rs + 16 * ks + 8 * hh);
+  }
+  f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
+  const int qt0 = (kb * 128) / TROWS;
+  const int nqt = S / TROWS;
+  const int wave_kmin = kb * 128 + w * 32;
+
+  Stage sq, sd;
+  float st_l = 0.f, st_d = 0.f;
+  auto load_tile = [&](int qt) {
+    stage_load(sq, qbase, rs, qt * TROWS, tid);
+    stage_load(sd, dobase, ors, qt * TROWS, tid);
+    if (tid < 64) st_l = lse_bh[qt * TROWS + tid] * LOG2E;
+    else if (tid < 128) st_d = del_bh[qt * TROWS + tid - 64];
+  };
+  auto store_tile = [&](int buf) {
+    bf16* T = smem + buf * 2 * TROWS * HD;
+    stage_store(sq, T, tid);
+    stage_store(sd, T + TROWS * HD, tid);
+    float* ss = sstat + buf * 2 * TROWS;
+    if (tid < 64) ss[tid] = st_l;
+    else if (tid < 128) ss[tid] = st_d;
+  };
+  load_tile(qt0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int buf = (qt - qt0) & 1;
+    const bf16* Qt = smem + buf * 2 * TROWS * HD;
+    const bf16* Dt = Qt + TROWS * HD;
+    const float* L2 = sstat + buf * 2 * TROWS;
+    const float* DL = L2 + TROWS;
+    const bool more = qt + 1 < nqt;
+    if (more) load_tile(qt + 1);
+    const int q0 = qt * TROWS;
+    if (q0 + TROWS - 1 >= wave_kmin) {
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const int qb0 = q0 + 32 * qs;
+        if (qb0 + 31 < wave_kmin) continue;  // all queries before this wave's keys
+        f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
+          dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
+        }
+        const bool diag = qb0 < wave_kmin + 31;
+        // rows r: q = qb0 + (r&3) + 8(r>>2) + 4hh
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qr = 32 * qs + 8 * g + 4 * hh;
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(L2 + qr);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + qr);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            float p = exp2f(sacc[r] * c2 - l4[e]);
+            if (diag && (q0 + qr + e) < key) p = 0.f;
+            sacc[r] = p;
+            dpacc[r] = p * (dpacc[r] - d4[e]);
+          }
+        }
+#pragma unroll
+        for (int sst = 0; sst < 2; ++sst) {
+          const bf16x8 pb = pack8(sacc, sst);
+          const bf16x8 db = pack8(dpacc, sst);
+          dv0 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 0, lane), pb, dv0);
+          dv1 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 32, lane), pb, dv1);
+          dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
+          dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
+        }
+      }
+    }
+    if (more) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+  // dK = scale * dS^T Q ; dV = P^T dO.  dqkv row `key`, slot 1 (k) and 2 (v)
+  bf16* krow = dqkv + (size_t)(b * S + key) * rs + (size_t)H * HD + (size_t)h * HD;
+  bf16* vrow = krow + (size_t)H * HD;
+  store_acc_rows(krow, dk0, 0, hh, scale);
+  store_acc_rows(krow, dk1, 32, hh, scale);
+  store_acc_rows(vrow, dv0, 0, hh, 1.f);
+  store_acc_rows(vrow, dv1, 32, hh, 1.f);
+}
+
+// ============================================================================
+// backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
+// ============================================================================
+__global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                       const float* __restrict__ lse, const float* __restrict__ delta,
+                                                       bf16* __restrict__ dqkv, int B, int S, int H, float c2,
+                                                       float scale) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int nqb = S / 128;
+  const int bh = blockIdx.x % (B * H);
+  const int qb = nqb - 1 - blockIdx.x / (B * H);
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;
+  const size_t ors = (size_t)H * HD;
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+  const bf16* dobase = dout + (size_t)b * S * ors + (size_t)h * HD;
+
+  const int q = qb * 128 + w * 32 + li;
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
+    df[ks] = *reinterpret_cast<const bf16x8*>(dobase + (size_t)q * ors + 16 * ks + 8 * hh);
+  }
+  const float lq = lse[(size_t)bh * S + q] * LOG2E;
+  const float dq_delta = delta[(size_t)bh * S + q];
+  f32x16 a0 = zero16(), a1 = zero16();
+  const int ntiles = (qb * 128 + 128) / TROWS;
+  const int wave_qmax = qb * 128 + w * 32 + 31;
+
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store(sv, smem + TROWS * HD, tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
+    const bf16* Vt = Kt + TROWS * HD;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    }
+    const int key0 = t * TROWS;
+    if (key0 <= wave_qmax) {
+      const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
+#pragma unroll
+      for (int ksub = 0; ksub < 2; ++ksub) {
+        f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
+          dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          float p = exp2f(s[r] * c2 - lq);
+          if (diag && kr > q) p = 0.f;
+          s[r] = p * (dp[r] - dq_delta);  // dS^T
+        }
+#pragma unroll
+        for (int sst = 0; sst < 2; ++sst) {
+          const bf16x8 dsb = pack8(s, sst);
+          a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
+          a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
+        }
+      }
+    }
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
+  }
+  bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
+  store_acc_rows(qrow, a0, 0, hh, scale);
+  store_acc_rows(qrow, a1, 32, hh, scale);
+}
+
+int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
+  if (D != HD || S % 128 != 0) return -2;
+  const int grid = B * H * (S / 128);
+  attn_fwd_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E);
+  return 0;
+}
+
+int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse, float* delta, bf16* dqkv, int B,
+             int S, int H, int D, float scale, hipStream_t st) {
+  if (D != HD || S % 128 != 0) return -2;
+  const long long rows = (long long)B * S * H;
+  attn_delta_kernel<<<(unsigned)((rows * 8 + 255) / 256), 256, 0, st>>>(dout, o, delta, B, S, H);
+  const int grid = B * H * (S / 128);
+  attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
+  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
+  return 0;
+}
+
+}  // namespace pdo

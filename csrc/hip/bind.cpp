@@ -1,0 +1,263 @@
+// pybind11 / PyTorch binding of the paddle_operator_amd HIP kernels.
+// Compiled by hipcc for gfx950 (tools/build.py) — no hipify, no CUDA names.
+// Every entry point checks device, dtype, contiguity and shape before launch:
+// a kernel never sees a shape its grid does not assume.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <cmath>
+
+#include "kernels.h"
+
+namespace {
+
+using pdo::bf16;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_I64(t) TORCH_CHECK((t).scalar_type() == at::kLong, #t " must be int64")
+#define CHECK_IN(t) \
+  CHECK_DEV(t);     \
+  CHECK_CONTIG(t)
+#define CHECK_RC(rc, what) TORCH_CHECK((rc) == 0, what " rejected the shape (code ", rc, ")")
+
+inline bf16* bp(const at::Tensor& t) { return reinterpret_cast<bf16*>(t.data_ptr()); }
+inline float* fp(const at::Tensor& t) { return t.data_ptr<float>(); }
+
+// ---------------------------------------------------------------- layernorm
+std::vector<at::Tensor> layernorm_fwd(at::Tensor x, at::Tensor w, at::Tensor b, double eps) {
+  CHECK_IN(x); CHECK_IN(w); CHECK_IN(b); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b);
+  TORCH_CHECK(x.dim() == 2 && w.numel() == x.size(1) && b.numel() == x.size(1));
+  const int N = x.size(0), C = x.size(1);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({N}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
+  CHECK_RC(pdo::layernorm_fwd(bp(x), nullptr, bp(w), bp(b), nullptr, bp(y), fp(mean), fp(rstd), N, C, (float)eps,
+                              cur_stream()), "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+std::vector<at::Tensor> add_layernorm_fwd(at::Tensor x, at::Tensor r, at::Tensor w, at::Tensor b, double eps) {
+  CHECK_IN(x); CHECK_IN(r); CHECK_IN(w); CHECK_IN(b);
+  CHECK_BF16(x); CHECK_BF16(r); CHECK_BF16(w); CHECK_BF16(b);
+  TORCH_CHECK(x.dim() == 2 && x.sizes() == r.sizes() && w.numel() == x.size(1) && b.numel() == x.size(1));
+  const int N = x.size(0), C = x.size(1);
+  auto h = at::empty_like(x);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({N}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
+  CHECK_RC(pdo::layernorm_fwd(bp(x), bp(r), bp(w), bp(b), bp(h), bp(y), fp(mean), fp(rstd), N, C, (float)eps,
+                              cur_stream()), "add_layernorm_fwd");
+  return {h, y, mean, rstd};
+}
+
+std::vector<at::Tensor> ln_bwd_impl(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
+                                    c10::optional<at::Tensor> dres) {
+  CHECK_IN(dy); CHECK_IN(x); CHECK_IN(w); CHECK_IN(mean); CHECK_IN(rstd);
+  CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(w); CHECK_F32(mean); CHECK_F32(rstd);
+  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && w.numel() == x.size(1));
+  const int N = x.size(0), C = x.size(1);
+  TORCH_CHECK(mean.numel() == N && rstd.numel() == N);
+  const bf16* dr = nullptr;
+  if (dres.has_value()) {
+    CHECK_IN((*dres)); CHECK_BF16((*dres));
+    TORCH_CHECK(dres->sizes() == x.sizes());
+    dr = bp(*dres);
+  }
+  auto dx = at::empty_like(x);
+  const int G = pdo::layernorm_bwd_grid(N);
+  auto part = at::empty({G, 2 * C}, x.options().dtype(at::kFloat));
+  auto dw = at::empty_like(w);
+  auto db = at::empty_like(w);
+  CHECK_RC(pdo::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), dr, bp(dx), fp(part), bp(dw), bp(db), N, C,
+                              cur_stream()), "layernorm_bwd");
+  return {dx, dw, db};
+}
+
+std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd) {
+  return ln_bwd_impl(dy, x, w, mean, rstd, c10::nullopt);
+}
+
+std::vector<at::Tensor> layernorm_bwd_add(at::Tensor dy, at::Tensor h, at::Tensor w, at::Tensor mean,
+                                          at::Tensor rstd, at::Tensor dres) {
+  return ln_bwd_impl(dy, h, w, mean, rstd, dres);
+}
+
+// ---------------------------------------------------------------- bias + gelu
+at::Tensor bias_gelu_fwd(at::Tensor x, at::Tensor b) {
+  CHECK_IN(x); CHECK_IN(b); CHECK_BF16(x); CHECK_BF16(b);
+  TORCH_CHECK(x.dim() == 2 && b.numel() == x.size(1));
+  auto y = at::empty_like(x);
+  CHECK_RC(pdo::bias_gelu_fwd(bp(x), bp(b), bp(y), x.size(0), x.size(1), cur_stream()), "bias_gelu_fwd");
+  return y;
+}
+
+std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b) {
+  CHECK_IN(dy); CHECK_IN(x); CHECK_IN(b); CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(b);
+  TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && b.numel() == x.size(1));
+  const long long N = x.size(0);
+  const int F = x.size(1);
+  auto dx = at::empty_like(x);
+  const int G = pdo::bias_gelu_bwd_groups(N, F);
+  auto part = at::empty({G, F}, x.options().dtype(at::kFloat));
+  auto db = at::empty_like(b);
+  CHECK_RC(pdo::bias_gelu_bwd(bp(dy), bp(x), bp(b), bp(dx), fp(part), bp(db), N, F, cur_stream()), "bias_gelu_bwd");
+  return {dx, db};
+}
+
+// ---------------------------------------------------------------- cross entropy
+std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor tgt, int64_t V) {
+  CHECK_IN(logits); CHECK_IN(tgt); CHECK_BF16(logits); CHECK_I64(tgt);
+  TORCH_CHECK(logits.dim() == 2 && tgt.numel() == logits.size(0) && V <= logits.size(1));
+  const int N = logits.size(0), Vp = logits.size(1);
+  auto row_loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({N}, logits.options().dtype(at::kFloat));
+  auto stats = at::empty({2}, logits.options().dtype(at::kFloat));
+  CHECK_RC(pdo::xent_fwd(bp(logits), tgt.data_ptr<int64_t>(), fp(row_loss), fp(lse), fp(stats), N, Vp, (int)V,
+                         cur_stream()), "xent_fwd");
+  return {stats.select(0, 0), lse, stats};
+}
+
+at::Tensor xent_bwd(at::Tensor logits, at::Tensor tgt, at::Tensor lse, at::Tensor dloss, at::Tensor stats, int64_t V,
+                    bool inplace) {
+  CHECK_IN(logits); CHECK_IN(tgt); CHECK_IN(lse); CHECK_IN(dloss); CHECK_IN(stats);
+  CHECK_BF16(logits); CHECK_F32(lse); CHECK_F32(dloss); CHECK_F32(stats);
+  const int N = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(lse.numel() == N && tgt.numel() == N && dloss.numel() == 1 && stats.numel() == 2);
+  auto out = inplace ? logits : at::empty_like(logits);
+  CHECK_RC(pdo::xent_bwd(bp(logits), tgt.data_ptr<int64_t>(), fp(lse), fp(dloss), fp(stats), bp(out), N, Vp, (int)V,
+                         cur_stream()), "xent_bwd");
+  return out;
+}
+
+// ---------------------------------------------------------------- embedding
+at::Tensor embed_fwd(at::Tensor idx, at::Tensor wte, at::Tensor wpe) {
+  CHECK_IN(idx); CHECK_IN(wte); CHECK_IN(wpe); CHECK_I64(idx); CHECK_BF16(wte); CHECK_BF16(wpe);
+  TORCH_CHECK(idx.dim() == 2 && wte.dim() == 2 && wpe.dim() == 2 && wte.size(1) == wpe.size(1));
+  const int B = idx.size(0), S = idx.size(1), C = wte.size(1);
+  TORCH_CHECK(S <= wpe.size(0), "sequence longer than the position table");
+  auto y = at::empty({B, S, C}, wte.options());
+  CHECK_RC(pdo::embed_fwd(idx.data_ptr<int64_t>(), bp(wte), bp(wpe), bp(y), B, S, C, cur_stream()), "embed_fwd");
+  return y;
+}
+
+std::vector<at::Tensor> embed_bwd(at::Tensor dy, at::Tensor idx, int64_t Vp, int64_t P) {
+  CHECK_IN(dy); CHECK_IN(idx); CHECK_BF16(dy); CHECK_I64(idx);
+  TORCH_CHECK(dy.dim() == 3 && idx.dim() == 2 && dy.size(0) == idx.size(0) && dy.size(1) == idx.size(1));
+  const int B = dy.size(0), S = dy.size(1), C = dy.size(2);
+  TORCH_CHECK(S <= P);
+  auto acc = at::empty({Vp, C}, dy.options().dtype(at::kFloat));
+  auto dwte = at::empty({Vp, C}, dy.options());
+  auto dwpe = at::empty({P, C}, dy.options());
+  CHECK_RC(pdo::embed_bwd(bp(dy), idx.data_ptr<int64_t>(), fp(acc), bp(dwte), bp(dwpe), B, S, C, (int)Vp, (int)P,
+                          cur_stream()), "embed_bwd");
+  return {dwte, dwpe};
+}
+
+// ---------------------------------------------------------------- optimizer
+void sumsq(at::Tensor g, at::Tensor out, double scale) {
+  CHECK_IN(g); CHECK_IN(out); CHECK_BF16(g); CHECK_F32(out);
+  const int cap = 2048;
+  auto part = at::empty({cap}, g.options().dtype(at::kFloat));
+  CHECK_RC(pdo::sumsq(bp(g), g.numel(), fp(part), cap, (float)scale, fp(out), cur_stream()), "sumsq");
+}
+
+void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor master, at::Tensor m1, at::Tensor m2, at::Tensor decay,
+                at::Tensor normsq, double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
+                double grad_scale, double clip) {
+  CHECK_IN(p); CHECK_IN(g); CHECK_IN(master); CHECK_IN(m1); CHECK_IN(m2); CHECK_IN(decay); CHECK_IN(normsq);
+  CHECK_BF16(p); CHECK_BF16(g); CHECK_F32(master); CHECK_F32(m1); CHECK_F32(m2); CHECK_F32(decay);
+  const long long n = p.numel();
+  TORCH_CHECK(g.numel() == n && master.numel() == n && m1.numel() == n && m2.numel() == n);
+  TORCH_CHECK(n % 1024 == 0 && decay.numel() == n / 1024);
+  CHECK_RC(pdo::adamw_flat(bp(p), bp(g), fp(master), fp(m1), fp(m2), fp(decay), fp(normsq), n, (float)lr, (float)b1,
+                           (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, (float)grad_scale, (float)clip,
+                           cur_stream()), "adamw_flat");
+}
+
+// ---------------------------------------------------------------- attention
+std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t n_head) {
+  CHECK_IN(qkv); CHECK_BF16(qkv);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) % (3 * n_head) == 0);
+  const int B = qkv.size(0), S = qkv.size(1), C = qkv.size(2) / 3, H = n_head, D = C / H;
+  TORCH_CHECK(D == 64 && S % 128 == 0, "attn_fwd supports head_dim 64 and seq % 128 == 0");
+  auto o = at::empty({B, S, C}, qkv.options());
+  auto lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  CHECK_RC(pdo::attn_fwd(bp(qkv), bp(o), fp(lse), B, S, H, D, 1.f / std::sqrt((float)D), cur_stream()), "attn_fwd");
+  return {o, lse};
+}
+
+at::Tensor attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, at::Tensor lse, int64_t n_head) {
+  CHECK_IN(dout); CHECK_IN(qkv); CHECK_IN(o); CHECK_IN(lse);
+  CHECK_BF16(dout); CHECK_BF16(qkv); CHECK_BF16(o); CHECK_F32(lse);
+  const int B = qkv.size(0), S = qkv.size(1), C = qkv.size(2) / 3, H = n_head, D = C / H;
+  TORCH_CHECK(dout.sizes() == o.sizes() && o.size(2) == C && lse.numel() == (int64_t)B * H * S);
+  TORCH_CHECK(D == 64 && S % 128 == 0);
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  CHECK_RC(pdo::attn_bwd(bp(dout), bp(qkv), bp(o), fp(lse), fp(delta), bp(dqkv), B, S, H, D,
+                         1.f / std::sqrt((float)D), cur_stream()), "attn_bwd");
+  return dqkv;
+}
+
+// ---------------------------------------------------------------- bucket helpers
+void scale_(at::Tensor x, double s) {
+  CHECK_IN(x); CHECK_BF16(x);
+  CHECK_RC(pdo::scale_bf16(bp(x), x.numel(), (float)s, cur_stream()), "scale_bf16");
+}
+
+// flat[off_i : off_i + n_i] = scale * t_i for every tensor (one launch)
+void flatten_scale(std::vector<at::Tensor> ts, at::Tensor flat, std::vector<int64_t> offsets, double scale,
+                   bool reverse) {
+  CHECK_IN(flat); CHECK_BF16(flat);
+  TORCH_CHECK(ts.size() == offsets.size());
+  const int n = ts.size();
+  if (n == 0) return;
+  auto meta = at::empty({n, 3}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  int64_t* mp = meta.data_ptr<int64_t>();
+  std::vector<long long> sizes(n), offs(n);
+  int64_t prev = -1;
+  for (int i = 0; i < n; ++i) {
+    CHECK_IN(ts[i]); CHECK_BF16(ts[i]);
+    TORCH_CHECK(offsets[i] > prev, "offsets must be increasing");
+    TORCH_CHECK(offsets[i] + ts[i].numel() <= flat.numel(), "tensor overruns the flat buffer");
+    prev = offsets[i];
+    mp[3 * i] = reinterpret_cast<int64_t>(ts[i].data_ptr());
+    mp[3 * i + 1] = ts[i].numel();
+    mp[3 * i + 2] = offsets[i];
+    sizes[i] = ts[i].numel();
+    offs[i] = offsets[i];
+  }
+  auto dmeta = meta.to(flat.device(), /*non_blocking=*/true);
+  int rc = reverse ? pdo::unflatten(bp(flat), nullptr, sizes.data(), offs.data(), n, dmeta.data_ptr(), cur_stream())
+                   : pdo::flatten_scale(nullptr, sizes.data(), offs.data(), n, bp(flat), (float)scale,
+                                        dmeta.data_ptr(), cur_stream());
+  CHECK_RC(rc, "flatten/unflatten");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_pdo_hip, m) {
+  m.doc() = "paddle_operator_amd HIP/CDNA4 kernels (gfx950)";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("add_layernorm_fwd", &add_layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd_add", &layernorm_bwd_add);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("sumsq", &sumsq);
+  m.def("adamw_flat", &adamw_flat);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("scale_", &scale_);
+  m.def("flatten_scale", &flatten_scale);
+  m.attr("arch") = "gfx950";
+}

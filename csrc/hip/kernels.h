@@ -1,0 +1,56 @@
+// Host-side launch API of the paddle_operator_amd HIP kernels (gfx950).
+// Raw pointers + hipStream_t only: no torch headers here, so each kernel TU
+// compiles in seconds; `bind.cpp` adapts torch tensors to these calls.
+// Return value: 0 ok, <0 unsupported shape (caller raises).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pdo {
+typedef __bf16 bf16;
+
+// layernorm.hip
+int layernorm_fwd(const bf16* x, const bf16* r, const bf16* w, const bf16* b, bf16* h, bf16* y, float* mean,
+                  float* rstd, int N, int C, float eps, hipStream_t st);
+int layernorm_bwd_grid(int N);
+int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
+                  const bf16* dres, bf16* dx, float* part, bf16* dw, bf16* db, int N, int C, hipStream_t st);
+void colsum(const float* part, int G, int C, int stride, bf16* out_bf16, float* out_f32, hipStream_t st);
+
+// gelu.hip
+int bias_gelu_fwd(const bf16* x, const bf16* b, bf16* y, long long N, int F, hipStream_t st);
+int bias_gelu_bwd_groups(long long N, int F);
+int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, bf16* db, long long N, int F,
+                  hipStream_t st);
+
+// xent.hip
+int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,
+             hipStream_t st);
+int xent_bwd(const bf16* logits, const int64_t* tgt, const float* lse, const float* dloss, const float* stats,
+             bf16* dlogits, int N, int Vp, int V, hipStream_t st);
+
+// embed.hip
+int embed_fwd(const int64_t* idx, const bf16* wte, const bf16* wpe, bf16* y, int B, int S, int C, hipStream_t st);
+int embed_bwd(const bf16* dy, const int64_t* idx, float* acc, bf16* dwte, bf16* dwpe, int B, int S, int C, int Vp,
+              int P, hipStream_t st);
+int cast_f32_bf16(const float* in, bf16* out, long long n, hipStream_t st);
+
+// optim.hip
+int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, float* out, hipStream_t st);
+int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, const float* decay_chunks,
+               const float* normsq, long long n, float lr, float b1, float b2, float eps, float wd, float bc1,
+               float bc2, float grad_scale, float clip, hipStream_t st);
+
+// attention.hip  (qkv: [B, S, 3, H, D] bf16; o: [B, S, H, D]; lse: [B, H, S] f32)
+int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st);
+int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse, float* delta, bf16* dqkv, int B,
+             int S, int H, int D, float scale, hipStream_t st);
+
+// bucket.hip (DDP helpers: multi-tensor flatten with fused scale / unflatten)
+int flatten_scale(const void* const* srcs, const long long* sizes, const long long* offsets, int n, bf16* dst,
+                  float scale, void* dev_meta, hipStream_t st);
+int unflatten(const bf16* src, void* const* dsts, const long long* sizes, const long long* offsets, int n,
+              void* dev_meta, hipStream_t st);
+int scale_bf16(bf16* x, long long n, float s, hipStream_t st);
+
+}  // namespace pdo

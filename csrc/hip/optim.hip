@@ -1,0 +1,89 @@
+// Fused AdamW over the flat parameter arena + gradient global-norm (gfx950).
+// One pass: bf16 grad → ×(grad_scale · clip_coef) → fp32 moments/master →
+// bf16 compute copy.  The clip coefficient is read from device memory
+// (written by `sumsq`), so clipping costs no host synchronisation.
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+__global__ __launch_bounds__(256) void sumsq_part_kernel(const bf16* __restrict__ g, long long nvec,
+                                                         float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    f32x8 v = to_f32(reinterpret_cast<const bf16x8*>(g)[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(1024) void sumsq_final_kernel(const float* __restrict__ part, int G, float scale2,
+                                                           float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < G; i += 1024) s += part[i];
+  s = block_sum<16>(s, red);
+  if (threadIdx.x == 0) out[0] = s * scale2;
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
+                                                    float* __restrict__ master, float* __restrict__ m1,
+                                                    float* __restrict__ m2, const float* __restrict__ decay_chunks,
+                                                    const float* __restrict__ normsq, long long nvec, float lr,
+                                                    float b1, float b2, float eps, float wd, float inv_bc1,
+                                                    float inv_sqrt_bc2, float grad_scale, float clip) {
+  float coef = grad_scale;
+  if (clip > 0.f) {
+    const float norm = sqrtf(normsq[0]);
+    coef *= fminf(1.f, clip / (norm + 1e-6f));
+  }
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    const float dec = decay_chunks[i >> 7];  // 1024 elements per chunk = 128 vectors
+    f32x8 gr = to_f32(reinterpret_cast<const bf16x8*>(g)[i]) * coef;
+    f32x4* mp = reinterpret_cast<f32x4*>(master) + 2 * i;
+    f32x4* ap = reinterpret_cast<f32x4*>(m1) + 2 * i;
+    f32x4* vp = reinterpret_cast<f32x4*>(m2) + 2 * i;
+    f32x4 w0 = mp[0], w1 = mp[1], a0 = ap[0], a1 = ap[1], v0 = vp[0], v1 = vp[1];
+    f32x8 w = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+    f32x8 a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    f32x8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    a = b1 * a + (1.f - b1) * gr;
+    v = b2 * v + (1.f - b2) * gr * gr;
+    const float shrink = 1.f - lr * wd * dec;
+    f32x8 upd;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) upd[j] = (a[j] * inv_bc1) / (sqrtf(v[j]) * inv_sqrt_bc2 + eps);
+    w = w * shrink - lr * upd;
+    mp[0] = f32x4{w[0], w[1], w[2], w[3]};
+    mp[1] = f32x4{w[4], w[5], w[6], w[7]};
+    ap[0] = f32x4{a[0], a[1], a[2], a[3]};
+    ap[1] = f32x4{a[4], a[5], a[6], a[7]};
+    vp[0] = f32x4{v[0], v[1], v[2], v[3]};
+    vp[1] = f32x4{v[4], v[5], v[6], v[7]};
+    reinterpret_cast<bf16x8*>(p)[i] = to_bf16(w);
+  }
+}
+
+int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, float* out, hipStream_t st) {
+  if (n % 8) return -2;
+  int G = stream_grid(n / 8, 256);
+  if (G > part_cap) G = part_cap;
+  sumsq_part_kernel<<<G, 256, 0, st>>>(g, n / 8, part);
+  sumsq_final_kernel<<<1, 1024, 0, st>>>(part, G, scale * scale, out);
+  return 0;
+}
+
+int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, const float* decay_chunks,
+               const float* normsq, long long n, float lr, float b1, float b2, float eps, float wd, float bc1,
+               float bc2, float grad_scale, float clip, hipStream_t st) {
+  if (n % 1024) return -2;
+  const long long nvec = n / 8;
+  adamw_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr, b1, b2,
+                                                        eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
+  return 0;
+}
+
+}  // namespace pdo

@@ -1,0 +1,123 @@
+// Softmax cross-entropy over a padded vocabulary (gfx950).
+// Forward: one 256-thread block per row, single pass with an online
+// (max, sum-exp) pair per thread over 16-B vectors, block combine → lse and the
+// row loss; padded columns (>= V) are masked.  The mean over valid targets is
+// reduced deterministically by a one-block kernel that also stores the count
+// for backward.  Backward writes dlogits = (softmax - onehot) * dloss / count
+// in place over the logits buffer (one read + one write of [N, Vp]).
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                       float* __restrict__ row_loss, float* __restrict__ lse_out,
+                                                       int Vp, int V) {
+  __shared__ float red_m[4], red_s[4];
+  const int row = blockIdx.x;
+  const bf16x8* lv = reinterpret_cast<const bf16x8*>(logits + (size_t)row * Vp);
+  const int nv = Vp >> 3;
+  float m = -INFINITY, s = 0.f;
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    f32x8 v = to_f32(lv[i]);
+    const int c0 = i * 8;
+    float vm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c0 + j >= V) v[j] = -INFINITY;
+      vm = fmaxf(vm, v[j]);
+    }
+    if (vm > m) {
+      s *= __expf(m - vm);
+      m = vm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(v[j] - m);
+  }
+  // wave combine of (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red_m[w] = m;
+    red_s[w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = red_m[0];
+    for (int i = 1; i < 4; ++i) M = fmaxf(M, red_m[i]);
+    float S = 0.f;
+    for (int i = 0; i < 4; ++i) S += red_m[i] == -INFINITY ? 0.f : red_s[i] * __expf(red_m[i] - M);
+    const float lse = M + __logf(S);
+    lse_out[row] = lse;
+    const int64_t t = tgt[row];
+    row_loss[row] = (t >= 0 && t < V) ? lse - (float)logits[(size_t)row * Vp + t] : 0.f;
+  }
+}
+
+// loss = sum(row_loss) / count(valid targets); stats[0]=loss, stats[1]=count
+__global__ __launch_bounds__(1024) void xent_mean_kernel(const float* __restrict__ row_loss,
+                                                         const int64_t* __restrict__ tgt, int N, int V,
+                                                         float* __restrict__ stats) {
+  __shared__ float red[16];
+  float s = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < N; i += 1024) {
+    s += row_loss[i];
+    c += (tgt[i] >= 0 && tgt[i] < V) ? 1.f : 0.f;
+  }
+  s = block_sum<16>(s, red);
+  c = block_sum<16>(c, red);
+  if (threadIdx.x == 0) {
+    stats[1] = c;
+    stats[0] = c > 0.f ? s / c : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                       const float* __restrict__ lse, const float* __restrict__ dloss,
+                                                       const float* __restrict__ stats, bf16* __restrict__ dlogits,
+                                                       int Vp, int V) {
+  const int row = blockIdx.x;
+  const float L = lse[row];
+  const int64_t t = tgt[row];
+  const float cnt = stats[1];
+  const float scale = (t >= 0 && t < V && cnt > 0.f) ? dloss[0] / cnt : 0.f;
+  const bf16x8* lv = reinterpret_cast<const bf16x8*>(logits + (size_t)row * Vp);
+  bf16x8* dv = reinterpret_cast<bf16x8*>(dlogits + (size_t)row * Vp);
+  const int nv = Vp >> 3;
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    f32x8 v = to_f32(lv[i]);
+    const int c0 = i * 8;
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      float p = c < V ? __expf(v[j] - L) : 0.f;
+      if (c == t) p -= 1.f;
+      o[j] = p * scale;
+    }
+    dv[i] = to_bf16(o);
+  }
+}
+
+int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,
+             hipStream_t st) {
+  if (Vp % 8) return -2;
+  xent_fwd_kernel<<<N, 256, 0, st>>>(logits, tgt, row_loss, lse, Vp, V);
+  xent_mean_kernel<<<1, 1024, 0, st>>>(row_loss, tgt, N, V, stats);
+  return 0;
+}
+
+int xent_bwd(const bf16* logits, const int64_t* tgt, const float* lse, const float* dloss, const float* stats,
+             bf16* dlogits, int N, int Vp, int V, hipStream_t st) {
+  if (Vp % 8) return -2;
+  xent_bwd_kernel<<<N, 256, 0, st>>>(logits, tgt, lse, dloss, stats, dlogits, Vp, V);
+  return 0;
+}
+
+}  // namespace pdo

@@ -1,0 +1,153 @@
+"""GPT-2 family (BASELINE config 4: GPT-2-medium, collective mode, 8×MI355X).
+
+Architecture follows the public GPT-2 definition (pre-LN transformer, learned
+positions, tanh-GELU MLP, tied input/output embedding).  Layout decisions are
+MI355X-first rather than a transcription of any reference implementation:
+
+* the vocabulary is padded 50257 → 50304 (a multiple of 128) so the LM-head
+  GEMM tiles evenly on the 256-CU grid; padded logits are masked inside the
+  fused cross-entropy kernel, so the loss is exactly the 50257-way loss;
+* QKV stays packed ([B, S, 3, H, D]) and the flash-attention kernel reads it in
+  place — no transpose/contiguous copies around attention;
+* residual add + LayerNorm are one kernel, bias + GELU is one kernel (with the
+  bias gradient reduced inside the backward kernel), embedding gather + position
+  add is one kernel;
+* all dense projections are plain hipBLASLt GEMMs (``torch.mm``) on bf16.
+
+The reference operator has no model code at all; this workload
+is what a PaddleJob launches (``deploy/examples/resnet.yaml:14-19`` pattern).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 1024
+    n_layer: int = 24
+    n_head: int = 16
+    ln_eps: float = 1e-5
+    pad_vocab_to: int = 128
+
+    @property
+    def padded_vocab(self) -> int:
+        m = self.pad_vocab_to
+        return (self.vocab_size + m - 1) // m * m
+
+    @staticmethod
+    def named(name: str) -> "GPT2Config":
+        table = {
+            "gpt2": dict(n_embd=768, n_layer=12, n_head=12),
+            "gpt2-medium": dict(n_embd=1024, n_layer=24, n_head=16),
+            "gpt2-large": dict(n_embd=1280, n_layer=36, n_head=20),
+            "gpt2-xl": dict(n_embd=1600, n_layer=48, n_head=25),
+            # tiny config for CPU tests / smoke
+            "gpt2-tiny": dict(n_embd=128, n_layer=2, n_head=2, n_positions=256, vocab_size=1000),
+        }
+        return GPT2Config(**table[name])
+
+    def n_params(self) -> int:
+        C, L = self.n_embd, self.n_layer
+        per_layer = 12 * C * C + 13 * C
+        return self.padded_vocab * C + self.n_positions * C + L * per_layer + 2 * C
+
+    def flops_per_token(self, seq: int) -> float:
+        """Training FLOPs/token (fwd+bwd = 3× fwd), dense + attention."""
+        C, L = self.n_embd, self.n_layer
+        dense = 6 * (L * 12 * C * C + self.padded_vocab * C)
+        attn = 6 * L * seq * C  # causal: QK^T and PV over on average S/2 keys (×2 matmuls)
+        return float(dense + attn)
+
+
+class Linear(nn.Module):
+    """y = x @ W^T (+ b). Weight stored [out, in] like nn.Linear."""
+
+    def __init__(self, fin, fout, bias=True):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.bias = nn.Parameter(torch.zeros(fout)) if bias else None
+
+    def forward(self, x):
+        return torch.nn.functional.linear(x, self.weight, self.bias)
+
+    def forward_nobias(self, x):
+        return torch.nn.functional.linear(x, self.weight)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        C = cfg.n_embd
+        self.cfg = cfg
+        self.ln1_w = nn.Parameter(torch.ones(C))
+        self.ln1_b = nn.Parameter(torch.zeros(C))
+        self.qkv = Linear(C, 3 * C)
+        self.proj = Linear(C, C)
+        self.ln2_w = nn.Parameter(torch.ones(C))
+        self.ln2_b = nn.Parameter(torch.zeros(C))
+        self.fc = Linear(C, 4 * C)
+        self.fc_proj = Linear(4 * C, C)
+
+    def forward(self, x, h):
+        """x: residual stream, h: LN1(x) already computed by the caller.
+
+        Returns (x_out, ln1_of_next_input_not_applied) — the next block's LN1 is
+        fused with this block's final residual add by the caller.
+        """
+        cfg = self.cfg
+        a = ops.attention(self.qkv(h), cfg.n_head)
+        a = self.proj(a)
+        x, h2 = ops.add_layer_norm(x, a, self.ln2_w, self.ln2_b, cfg.ln_eps)
+        m = ops.bias_gelu(self.fc.forward_nobias(h2), self.fc.bias)
+        m = self.fc_proj(m)
+        return x, m
+
+
+class GPT2(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.cfg = cfg
+        C = cfg.n_embd
+        self.wte = nn.Parameter(torch.empty(cfg.padded_vocab, C))
+        self.wpe = nn.Parameter(torch.empty(cfg.n_positions, C))
+        self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.lnf_w = nn.Parameter(torch.ones(C))
+        self.lnf_b = nn.Parameter(torch.zeros(C))
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self, seed: int = 1234):
+        g = torch.Generator().manual_seed(seed)
+        std = 0.02
+        proj_std = 0.02 / math.sqrt(2 * self.cfg.n_layer)
+        for name, p in self.named_parameters():
+            if p.dim() == 2:
+                s = proj_std if (name.endswith("proj.weight") and "blocks" in name) else std
+                p.copy_(torch.randn(p.shape, generator=g) * s)
+        self.wte[self.cfg.vocab_size:].zero_()
+
+    def forward(self, idx, targets=None):
+        cfg = self.cfg
+        x = ops.embedding(idx, self.wte, self.wpe)
+        blk0 = self.blocks[0]
+        h = ops.layer_norm(x, blk0.ln1_w, blk0.ln1_b, cfg.ln_eps)
+        for i, blk in enumerate(self.blocks):
+            x, m = blk(x, h)
+            if i + 1 < len(self.blocks):
+                nb = self.blocks[i + 1]
+                x, h = ops.add_layer_norm(x, m, nb.ln1_w, nb.ln1_b, cfg.ln_eps)
+            else:
+                x, h = ops.add_layer_norm(x, m, self.lnf_w, self.lnf_b, cfg.ln_eps)
+        logits = torch.nn.functional.linear(h, self.wte)
+        if targets is None:
+            return logits[..., :cfg.vocab_size]
+        return ops.cross_entropy(logits, targets, cfg.vocab_size)

@@ -1,0 +1,264 @@
+"""Fused ops for the flagship workloads.
+
+Every op has two implementations:
+
+* the HIP/CDNA4 kernel in ``csrc/hip`` (used for every CUDA/HIP tensor), and
+* a plain PyTorch fp32 reference (``ref_*``), used on CPU and as the oracle in
+  the numerics tests (``tests/test_ops_gpu.py``).
+
+Dispatch is by device, never by try/except: a GPU tensor with the extension
+missing raises (see ``paddle_operator_amd._native.require_hip``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+
+__all__ = [
+    "layer_norm", "add_layer_norm", "bias_gelu", "attention", "cross_entropy",
+    "embedding", "ref_layer_norm", "ref_bias_gelu", "ref_attention",
+    "ref_cross_entropy", "use_hip",
+]
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    if not t.is_cuda:
+        return False
+    if _native.ops_mode() == "torch":
+        return False
+    _native.require_hip()
+    return True
+
+
+# ----------------------------------------------------------------------------
+# reference implementations (fp32 math, cast back to input dtype)
+# ----------------------------------------------------------------------------
+
+def ref_layer_norm(x, w, b, eps=1e-5):
+    y = F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+    return y.to(x.dtype)
+
+
+def _gelu_tanh(x):
+    return 0.5 * x * (1.0 + torch.tanh(0.7978845608028654 * (x + 0.044715 * x * x * x)))
+
+
+def ref_bias_gelu(x, b):
+    return _gelu_tanh(x.float() + b.float()).to(x.dtype)
+
+
+def ref_attention(q, k, v, causal=True):
+    """q,k,v: [B, H, S, D] → [B, H, S, D] (fp32 math)."""
+    qf, kf, vf = q.float(), k.float(), v.float()
+    s = qf @ kf.transpose(-1, -2) / math.sqrt(q.shape[-1])
+    if causal:
+        S = q.shape[-2]
+        mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return (p @ vf).to(q.dtype)
+
+
+def ref_cross_entropy(logits, target, vocab: int | None = None):
+    """Mean token cross entropy; columns >= ``vocab`` (padding) are masked."""
+    lf = logits.float()
+    if vocab is not None and vocab < lf.shape[-1]:
+        lf = lf[..., :vocab]
+    return F.cross_entropy(lf.reshape(-1, lf.shape[-1]), target.reshape(-1))
+
+
+# ----------------------------------------------------------------------------
+# LayerNorm (optionally fused with the residual add)
+# ----------------------------------------------------------------------------
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        m = _native.require_hip()
+        x2 = x.reshape(-1, x.shape[-1])
+        y, mean, rstd = m.layernorm_fwd(x2, w, b, eps)
+        ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x2, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = m.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, w, mean, rstd)
+        return dx.view(ctx.shape), dw, db, None
+
+
+def layer_norm(x, w, b, eps=1e-5):
+    if use_hip(x):
+        return _LayerNormFn.apply(x.contiguous(), w, b, eps)
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+class _AddLayerNormFn(torch.autograd.Function):
+    """h = x + r ; y = LN(h).  Returns (h, y).  One read of x and r, one write
+    of h and y: the residual stream never makes a separate HBM round trip."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, b, eps):
+        m = _native.require_hip()
+        x2 = x.reshape(-1, x.shape[-1])
+        r2 = r.reshape(-1, r.shape[-1])
+        h, y, mean, rstd = m.add_layernorm_fwd(x2, r2, w, b, eps)
+        ctx.save_for_backward(h, w, mean, rstd)
+        ctx.shape = x.shape
+        return h.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        m = _native.require_hip()
+        h, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = m.layernorm_bwd_add(dy.reshape(h.shape).contiguous(), h, w, mean, rstd,
+                                         dh.reshape(h.shape).contiguous())
+        dx = dx.view(ctx.shape)
+        return dx, dx, dw, db, None
+
+
+def add_layer_norm(x, r, w, b, eps=1e-5):
+    if use_hip(x):
+        return _AddLayerNormFn.apply(x.contiguous(), r.contiguous(), w, b, eps)
+    h = x + r
+    return h, F.layer_norm(h, (h.shape[-1],), w, b, eps)
+
+
+# ----------------------------------------------------------------------------
+# bias + GELU(tanh)
+# ----------------------------------------------------------------------------
+
+class _BiasGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b):
+        m = _native.require_hip()
+        x2 = x.reshape(-1, x.shape[-1])
+        y = m.bias_gelu_fwd(x2, b)
+        ctx.save_for_backward(x2, b)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x2, b = ctx.saved_tensors
+        dx, db = m.bias_gelu_bwd(dy.reshape(x2.shape).contiguous(), x2, b)
+        return dx.view(ctx.shape), db
+
+
+def bias_gelu(x, b):
+    if use_hip(x):
+        return _BiasGeluFn.apply(x.contiguous(), b)
+    return F.gelu(x + b, approximate="tanh")
+
+
+# ----------------------------------------------------------------------------
+# causal attention, q/k/v packed as produced by the QKV projection
+# ----------------------------------------------------------------------------
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, n_head):
+        # qkv: [B, S, 3, H, D] (the natural output layout of x @ W_qkv)
+        m = _native.require_hip()
+        o, lse = m.attn_fwd(qkv, n_head)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.n_head = n_head
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        m = _native.require_hip()
+        qkv, o, lse = ctx.saved_tensors
+        dqkv = m.attn_bwd(do.contiguous(), qkv, o, lse, ctx.n_head)
+        return dqkv, None
+
+
+def attention(qkv: torch.Tensor, n_head: int) -> torch.Tensor:
+    """Causal self-attention.
+
+    ``qkv``: [B, S, 3*C] straight out of the QKV GEMM; returns [B, S, C].
+    HIP path: MFMA flash attention reading q/k/v in place (no transposes).
+    """
+    B, S, C3 = qkv.shape
+    C = C3 // 3
+    D = C // n_head
+    if use_hip(qkv) and D == 64 and S % 128 == 0:
+        return _FlashAttnFn.apply(qkv.contiguous(), n_head)
+    # shapes outside the hand-written kernel's contract (head_dim != 64 or
+    # seq % 128 != 0) use the framework SDPA on GPU / the fp32 reference on CPU
+    q, k, v = qkv.view(B, S, 3, n_head, D).permute(2, 0, 3, 1, 4).unbind(0)
+    if qkv.is_cuda:
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    else:
+        o = ref_attention(q, k, v, causal=True)
+    return o.transpose(1, 2).reshape(B, S, C)
+
+
+# ----------------------------------------------------------------------------
+# softmax cross entropy over a (padded) vocabulary
+# ----------------------------------------------------------------------------
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, vocab):
+        m = _native.require_hip()
+        l2 = logits.reshape(-1, logits.shape[-1])
+        t = target.reshape(-1)
+        loss, lse, stats = m.xent_fwd(l2, t, vocab)
+        ctx.save_for_backward(l2, t, lse, stats)
+        ctx.vocab = vocab
+        ctx.shape = logits.shape
+        return loss.clone()
+
+    @staticmethod
+    def backward(ctx, dloss):
+        m = _native.require_hip()
+        l2, t, lse, stats = ctx.saved_tensors
+        # the logits buffer is dead after this point: write dlogits in place
+        dl = m.xent_bwd(l2, t, lse, dloss.reshape(1).float().contiguous(), stats, ctx.vocab, True)
+        return dl.view(ctx.shape), None, None
+
+
+def cross_entropy(logits, target, vocab: int | None = None):
+    V = vocab if vocab is not None else logits.shape[-1]
+    if use_hip(logits):
+        return _XentFn.apply(logits.contiguous(), target.contiguous(), V)
+    return ref_cross_entropy(logits, target, V)
+
+
+# ----------------------------------------------------------------------------
+# token + position embedding
+# ----------------------------------------------------------------------------
+
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe):
+        m = _native.require_hip()
+        y = m.embed_fwd(idx, wte, wpe)
+        ctx.save_for_backward(idx)
+        ctx.wte_shape = wte.shape
+        ctx.wpe_shape = wpe.shape
+        ctx.dtype = wte.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        (idx,) = ctx.saved_tensors
+        dwte, dwpe = m.embed_bwd(dy.contiguous(), idx, ctx.wte_shape[0], ctx.wpe_shape[0])
+        return None, dwte.to(ctx.dtype), dwpe.to(ctx.dtype)
+
+
+def embedding(idx, wte, wpe):
+    """y[b, s] = wte[idx[b, s]] + wpe[s]."""
+    if use_hip(wte):
+        return _EmbedFn.apply(idx.contiguous(), wte, wpe)
+    S = idx.shape[1]
+    return F.embedding(idx, wte) + wpe[:S].unsqueeze(0)

@@ -1,0 +1,91 @@
+"""Fused AdamW over a :class:`~paddle_operator_amd.parallel.flat.FlatParams` arena.
+
+One HIP kernel per step (``adamw_flat`` in ``csrc/hip/optim.hip``) reads the
+bf16 gradient, applies ``grad_scale`` (= 1/world for a summed all-reduce) and
+the global-norm clip coefficient (computed on device by ``sumsq`` — no host
+sync), updates the fp32 master weights and both moments, and writes the bf16
+compute copy.  Traffic per element: 2 B grad + 12 B state read, 12 B state +
+2 B param written = 28 B, HBM-bound at ~6 TB/s → ~1.7 ms for GPT-2-medium.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from . import use_hip
+
+
+class FlatAdamW:
+    def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
+                 max_grad_norm: float | None = 1.0):
+        self.flat = flat
+        self.lr = lr
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.wd = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.step_count = 0
+        self.master = flat.params.detach().float().clone()
+        self.m = torch.zeros_like(self.master)
+        self.v = torch.zeros_like(self.master)
+        self._norm_buf = torch.zeros(2, dtype=torch.float32, device=flat.device)
+
+    def grad_norm_sq(self, grad_scale=1.0):
+        """Device scalar of ||grad_scale * g||^2 (no sync)."""
+        g = self.flat.grads
+        if use_hip(g):
+            m = _native.require_hip()
+            m.sumsq(g, self._norm_buf, grad_scale)
+            return self._norm_buf[0]
+        gs = g.float() * grad_scale
+        self._norm_buf[0] = (gs * gs).sum()
+        return self._norm_buf[0]
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0, lr: float | None = None):
+        self.step_count += 1
+        lr = self.lr if lr is None else lr
+        t = self.step_count
+        bc1 = 1.0 - self.b1 ** t
+        bc2 = 1.0 - self.b2 ** t
+        clip = self.max_grad_norm if self.max_grad_norm is not None else -1.0
+        if clip > 0:
+            self.grad_norm_sq(grad_scale)
+        f = self.flat
+        if use_hip(f.grads):
+            m = _native.require_hip()
+            m.adamw_flat(f.params, f.grads, self.master, self.m, self.v, f.decay_chunks,
+                         self._norm_buf, lr, self.b1, self.b2, self.eps, self.wd,
+                         bc1, bc2, grad_scale, clip)
+            return
+        # reference path (fp32 math, identical formula to the kernel)
+        g = f.grads.float() * grad_scale
+        if clip > 0:
+            norm = torch.sqrt(self._norm_buf[0])
+            g = g * torch.clamp(clip / (norm + 1e-6), max=1.0)
+        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        decay = f.decay_chunks.repeat_interleave(f.numel // f.decay_chunks.numel())
+        self.master.mul_(1 - lr * self.wd * decay)
+        denom = (self.v / bc2).sqrt_().add_(self.eps)
+        self.master.addcdiv_(self.m, denom, value=-lr / bc1)
+        f.params.copy_(self.master)
+
+    def state_dict(self):
+        return {"master": self.master, "m": self.m, "v": self.v, "step": self.step_count}
+
+    def load_state_dict(self, sd):
+        self.master.copy_(sd["master"])
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.step_count = int(sd["step"])
+        self.flat.params.copy_(self.master)
+
+
+def cosine_lr(step, base_lr, warmup=100, total=10000, min_ratio=0.1):
+    if step < warmup:
+        return base_lr * (step + 1) / warmup
+    p = min(1.0, (step - warmup) / max(1, total - warmup))
+    return base_lr * (min_ratio + (1 - min_ratio) * 0.5 * (1 + math.cos(math.pi * p)))

@@ -1,0 +1,102 @@
+"""Training step engine shared by ``bench.py``, ``pdo-launch`` workloads and tests.
+
+One step = zero grads (memset of the flat arena) → forward → backward with
+bucketed RCCL all-reduce overlapped → fused AdamW.  Synthetic batches are
+generated on device every step (``torch.randint`` on the GPU; no H2D copy),
+matching BASELINE's "synthetic data / random-init weights" rule.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from .models.gpt2 import GPT2, GPT2Config
+from .ops.optim import FlatAdamW
+from .parallel.ddp import BucketedDDP
+from .parallel.flat import FlatParams
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+
+def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
+    """Initialise torch.distributed from the torchrun / pdo-launch env contract.
+
+    On ROCm the ``nccl`` backend IS RCCL.  ``hipSetDevice(local_rank)`` happens
+    before any other HIP call so the communicator binds the right GPU.
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    info = DistInfo(rank, world, local)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        import datetime
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return info
+
+
+class GPT2Trainer:
+    def __init__(self, cfg: GPT2Config, micro_batch: int, seq_len: int, device,
+                 dtype=torch.bfloat16, lr=3e-4, bucket_mb: int = 64, seed: int = 0):
+        self.cfg = cfg
+        self.B = micro_batch
+        self.S = seq_len
+        self.device = torch.device(device)
+        torch.manual_seed(seed)
+        model = GPT2(cfg)
+        model.to(device=self.device, dtype=dtype)
+        self.model = model
+        self.flat = FlatParams(model, dtype=dtype, device=self.device,
+                               bucket_bytes=bucket_mb << 20, late=("wte",))
+        self.ddp = BucketedDDP(self.flat)
+        self.opt = FlatAdamW(self.flat, lr=lr)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed + (dist.get_rank() if dist.is_initialized() else 0))
+
+    def sync_initial_weights(self):
+        self.ddp.broadcast_params(0)
+        self.opt.master.copy_(self.flat.params.float())
+
+    def batch(self):
+        V = self.cfg.vocab_size
+        idx = torch.randint(0, V, (self.B, self.S + 1), device=self.device, generator=self.gen)
+        return idx[:, :-1], idx[:, 1:]
+
+    def step(self, idx=None, tgt=None):
+        if idx is None:
+            idx, tgt = self.batch()
+        self.flat.zero_grad()
+        self.ddp.prepare()
+        loss = self.model(idx, tgt)
+        loss.backward()
+        self.ddp.finish()
+        self.opt.step(grad_scale=self.ddp.grad_scale)
+        return loss
+
+    def tokens_per_step(self):
+        return self.B * self.S
+
+
+def now():
+    return time.perf_counter()

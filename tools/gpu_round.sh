@@ -1,0 +1,15 @@
+#!/bin/bash
+# one GPU session: numerics tests → bench (hip ops) → kernel-trace profile
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+MB=${MB:-16}
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+for mb in $MB; do
+  timeout -k 10 300 python bench.py --micro-batch $mb --steps 10 --warmup 3 >> gpurun_out/bench_hip.jsonl 2>> gpurun_out/bench_hip.err || { tail -20 gpurun_out/bench_hip.err; exit 1; }
+done
+cat gpurun_out/bench_hip.jsonl
+if [ -n "$PROF" ]; then
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_hip -o run -- python3 $GRAFT_REPO_ROOT/bench.py --micro-batch 16 --steps 3 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/prof_hip.log 2>&1 || exit 1
+fi

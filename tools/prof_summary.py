@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 ``--kernel-trace`` database (ROCm 7.2 rocpd sqlite).
+
+usage: python tools/prof_summary.py gpurun_out/prof/run_results.db [--steps K] [--top N]
+
+Groups dispatches by kernel name (long Tensile names shortened), prints total
+ms, calls, mean µs and share; with ``--steps`` also per-step ms.  Output is
+plain markdown so it can be committed under ``profiles/``.
+"""
+import argparse
+import re
+import sqlite3
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    if name.startswith("Cijk_"):
+        m = re.search(r"MT(\d+x\d+x\d+)", name)
+        kind = name.split("_")[1] + "_" + name.split("_")[2]
+        return f"hipBLASLt GEMM {kind} MT{m.group(1) if m else '?'}"
+    if name.startswith("void "):
+        name = name[5:]
+    # drop the trailing argument list only (templates may contain parentheses)
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            name = name[:i]
+            break
+    return name[:120].replace("|", "/")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--steps", type=int, default=0)
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    rows = c.execute("select name, duration, start, end from kernels").fetchall()
+    agg = defaultdict(lambda: [0, 0.0])
+    t0 = min(r[2] for r in rows)
+    t1 = max(r[3] for r in rows)
+    for name, dur, _, _ in rows:
+        k = short(name)
+        agg[k][0] += 1
+        agg[k][1] += dur
+    total = sum(v[1] for v in agg.values())
+    print(f"# rocprofv3 kernel summary {a.title}\n")
+    print(f"dispatches: {len(rows)}  kernel time: {total/1e6:.2f} ms  span: {(t1-t0)/1e6:.2f} ms\n")
+    hdr = "| kernel | calls | total ms | mean us | % |"
+    if a.steps:
+        hdr = hdr[:-1] + " ms/step |"
+    print(hdr)
+    print("|" + "---|" * (hdr.count("|") - 1))
+    for k, (n, d) in sorted(agg.items(), key=lambda x: -x[1][1])[:a.top]:
+        line = f"| {k} | {n} | {d/1e6:.3f} | {d/n/1e3:.1f} | {100*d/total:.1f} |"
+        if a.steps:
+            line += f" {d/1e6/a.steps:.3f} |"
+        print(line)
+
+
+if __name__ == "__main__":
+    main()
