@@ -36,27 +36,34 @@ std::vector<at::Tensor> layernorm_fwd(at::Tensor x, at::Tensor w, at::Tensor b, 
   auto y = at::empty_like(x);
   auto mean = at::empty({N}, x.options().dtype(at::kFloat));
   auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
-  CHECK_RC(pdo::layernorm_fwd(bp(x), nullptr, bp(w), bp(b), nullptr, bp(y), fp(mean), fp(rstd), N, C, (float)eps,
-                              cur_stream()), "layernorm_fwd");
+  CHECK_RC(pdo::layernorm_fwd(bp(x), nullptr, nullptr, bp(w), bp(b), nullptr, bp(y), fp(mean), fp(rstd), N, C,
+                              (float)eps, cur_stream()), "layernorm_fwd");
   return {y, mean, rstd};
 }
 
-std::vector<at::Tensor> add_layernorm_fwd(at::Tensor x, at::Tensor r, at::Tensor w, at::Tensor b, double eps) {
+std::vector<at::Tensor> add_layernorm_fwd(at::Tensor x, at::Tensor r, at::Tensor w, at::Tensor b, double eps,
+                                          c10::optional<at::Tensor> rbias) {
   CHECK_IN(x); CHECK_IN(r); CHECK_IN(w); CHECK_IN(b);
   CHECK_BF16(x); CHECK_BF16(r); CHECK_BF16(w); CHECK_BF16(b);
   TORCH_CHECK(x.dim() == 2 && x.sizes() == r.sizes() && w.numel() == x.size(1) && b.numel() == x.size(1));
+  const bf16* rb = nullptr;
+  if (rbias.has_value()) {
+    CHECK_IN((*rbias)); CHECK_BF16((*rbias));
+    TORCH_CHECK(rbias->numel() == x.size(1));
+    rb = bp(*rbias);
+  }
   const int N = x.size(0), C = x.size(1);
   auto h = at::empty_like(x);
   auto y = at::empty_like(x);
   auto mean = at::empty({N}, x.options().dtype(at::kFloat));
   auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
-  CHECK_RC(pdo::layernorm_fwd(bp(x), bp(r), bp(w), bp(b), bp(h), bp(y), fp(mean), fp(rstd), N, C, (float)eps,
+  CHECK_RC(pdo::layernorm_fwd(bp(x), bp(r), rb, bp(w), bp(b), bp(h), bp(y), fp(mean), fp(rstd), N, C, (float)eps,
                               cur_stream()), "add_layernorm_fwd");
   return {h, y, mean, rstd};
 }
 
 std::vector<at::Tensor> ln_bwd_impl(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
-                                    c10::optional<at::Tensor> dres) {
+                                    c10::optional<at::Tensor> dres, bool rbias) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(w); CHECK_IN(mean); CHECK_IN(rstd);
   CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(w); CHECK_F32(mean); CHECK_F32(rstd);
   TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && w.numel() == x.size(1));
@@ -70,21 +77,22 @@ std::vector<at::Tensor> ln_bwd_impl(at::Tensor dy, at::Tensor x, at::Tensor w, a
   }
   auto dx = at::empty_like(x);
   const int G = pdo::layernorm_bwd_grid(N);
-  auto part = at::empty({G, 2 * C}, x.options().dtype(at::kFloat));
-  auto dw = at::empty_like(w);
-  auto db = at::empty_like(w);
-  CHECK_RC(pdo::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), dr, bp(dx), fp(part), bp(dw), bp(db), N, C,
-                              cur_stream()), "layernorm_bwd");
-  return {dx, dw, db};
+  const int NA = rbias ? 3 : 2;
+  auto part = at::empty({G * NA * C + pdo::colsum_scratch_floats(G, NA * C)}, x.options().dtype(at::kFloat));
+  auto out = at::empty({NA, C}, w.options());
+  CHECK_RC(pdo::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), dr, bp(dx), fp(part),
+                              fp(part) + (size_t)G * NA * C, bp(out), rbias, N, C, cur_stream()), "layernorm_bwd");
+  if (rbias) return {dx, out[0], out[1], out[2]};
+  return {dx, out[0], out[1]};
 }
 
 std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd) {
-  return ln_bwd_impl(dy, x, w, mean, rstd, c10::nullopt);
+  return ln_bwd_impl(dy, x, w, mean, rstd, c10::nullopt, false);
 }
 
 std::vector<at::Tensor> layernorm_bwd_add(at::Tensor dy, at::Tensor h, at::Tensor w, at::Tensor mean,
-                                          at::Tensor rstd, at::Tensor dres) {
-  return ln_bwd_impl(dy, h, w, mean, rstd, dres);
+                                          at::Tensor rstd, at::Tensor dres, bool rbias) {
+  return ln_bwd_impl(dy, h, w, mean, rstd, dres, rbias);
 }
 
 // ---------------------------------------------------------------- bias + gelu
@@ -103,10 +111,23 @@ std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b)
   const int F = x.size(1);
   auto dx = at::empty_like(x);
   const int G = pdo::bias_gelu_bwd_groups(N, F);
-  auto part = at::empty({G, F}, x.options().dtype(at::kFloat));
+  auto part = at::empty({(int64_t)G * F + pdo::colsum_scratch_floats(G, F)}, x.options().dtype(at::kFloat));
   auto db = at::empty_like(b);
-  CHECK_RC(pdo::bias_gelu_bwd(bp(dy), bp(x), bp(b), bp(dx), fp(part), bp(db), N, F, cur_stream()), "bias_gelu_bwd");
+  CHECK_RC(pdo::bias_gelu_bwd(bp(dy), bp(x), bp(b), bp(dx), fp(part), fp(part) + (size_t)G * F, bp(db), N, F,
+                              cur_stream()), "bias_gelu_bwd");
   return {dx, db};
+}
+
+// db = colsum(dy) for a [N, F] bf16 gradient
+at::Tensor bias_grad(at::Tensor dy) {
+  CHECK_IN(dy); CHECK_BF16(dy);
+  TORCH_CHECK(dy.dim() == 2);
+  const long long N = dy.size(0);
+  const int F = dy.size(1);
+  auto scratch = at::empty({pdo::bias_grad_scratch_floats(N, F)}, dy.options().dtype(at::kFloat));
+  auto db = at::empty({F}, dy.options());
+  CHECK_RC(pdo::bias_grad(bp(dy), N, F, bp(db), fp(scratch), cur_stream()), "bias_grad");
+  return db;
 }
 
 // ---------------------------------------------------------------- cross entropy
@@ -244,11 +265,13 @@ void flatten_scale(std::vector<at::Tensor> ts, at::Tensor flat, std::vector<int6
 PYBIND11_MODULE(_pdo_hip, m) {
   m.doc() = "paddle_operator_amd HIP/CDNA4 kernels (gfx950)";
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("add_layernorm_fwd", &add_layernorm_fwd);
+  m.def("add_layernorm_fwd", &add_layernorm_fwd, py::arg("x"), py::arg("r"), py::arg("w"), py::arg("b"),
+        py::arg("eps"), py::arg("rbias") = py::none());
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("layernorm_bwd_add", &layernorm_bwd_add);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_grad", &bias_grad);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("embed_fwd", &embed_fwd);

@@ -52,6 +52,7 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16* __restri
   f32x8 acc = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c8 < F8) {
     const f32x8 bb = to_f32(reinterpret_cast<const bf16x8*>(b)[c8]);
+#pragma unroll 4
     for (int r = r0; r < r1; ++r) {
       const size_t idx = (size_t)r * F8 + c8;
       f32x8 d = to_f32(reinterpret_cast<const bf16x8*>(dy)[idx]);
@@ -83,13 +84,13 @@ int bias_gelu_bwd_groups(long long N, int F) {
   return (int)gy;
 }
 
-int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, bf16* db, long long N, int F,
-                  hipStream_t st) {
+int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, float* scratch, bf16* db,
+                  long long N, int F, hipStream_t st) {
   if (F % 8) return -2;
   const int gx = (F / 8 + 255) / 256;
   const int gy = bias_gelu_bwd_groups(N, F);
   bias_gelu_bwd_kernel<<<dim3(gx, gy), 256, 0, st>>>(dy, x, b, dx, part, (int)N, F);
-  colsum(part, gy, F, F, db, nullptr, st);
+  colsum(part, gy, F, F, db, scratch, st);
   return 0;
 }
 

@@ -10,18 +10,24 @@ namespace pdo {
 typedef __bf16 bf16;
 
 // layernorm.hip
-int layernorm_fwd(const bf16* x, const bf16* r, const bf16* w, const bf16* b, bf16* h, bf16* y, float* mean,
-                  float* rstd, int N, int C, float eps, hipStream_t st);
+int layernorm_fwd(const bf16* x, const bf16* r, const bf16* rb, const bf16* w, const bf16* b, bf16* h, bf16* y,
+                  float* mean, float* rstd, int N, int C, float eps, hipStream_t st);
 int layernorm_bwd_grid(int N);
 int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
-                  const bf16* dres, bf16* dx, float* part, bf16* dw, bf16* db, int N, int C, hipStream_t st);
-void colsum(const float* part, int G, int C, int stride, bf16* out_bf16, float* out_f32, hipStream_t st);
+                  const bf16* dres, bf16* dx, float* part, float* scratch, bf16* out, bool rbias, int N, int C,
+                  hipStream_t st);
+
+// reduce.hip
+int colsum_scratch_floats(int G, int C);
+void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st);
+int bias_grad_scratch_floats(long long N, int F);
+int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st);
 
 // gelu.hip
 int bias_gelu_fwd(const bf16* x, const bf16* b, bf16* y, long long N, int F, hipStream_t st);
 int bias_gelu_bwd_groups(long long N, int F);
-int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, bf16* db, long long N, int F,
-                  hipStream_t st);
+int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, float* scratch, bf16* db,
+                  long long N, int F, hipStream_t st);
 
 // xent.hip
 int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,

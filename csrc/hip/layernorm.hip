@@ -4,7 +4,7 @@
 // mean, then centred variance), reductions are 64-lane shuffles.  Backward
 // computes dx per row and accumulates dgamma/dbeta per lane in registers over
 // a grid-stride row loop; the 4 waves of a block combine through LDS and the
-// per-block partials are summed by `colsum_kernel` (deterministic, no atomics).
+// per-block partials are summed by the two-level `colsum` (reduce.hip).
 #include "common.h"
 #include "kernels.h"
 
@@ -12,6 +12,7 @@ namespace pdo {
 
 template <int VPL, bool ADD>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ r,
+                                                     const bf16* __restrict__ rb,
                                                      const bf16* __restrict__ w, const bf16* __restrict__ b,
                                                      bf16* __restrict__ h, bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -30,7 +31,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ x,
     const int c8 = lane + i * 64;
     if (c8 < C8) {
       v[i] = to_f32(xr[c8]);
-      if (ADD) v[i] += to_f32(rr[c8]);
+      if (ADD) {
+        v[i] += to_f32(rr[c8]);
+        if (rb) v[i] += to_f32(reinterpret_cast<const bf16x8*>(rb)[c8]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
     } else {
@@ -70,22 +74,26 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ x,
   }
 }
 
-template <int VPL, bool ADD>
+// NA = 2: partials (dgamma, dbeta); NA = 3: + colsum(dx) — the gradient of a
+// bias folded into the residual branch (h = x + r + rbias).
+template <int VPL, bool ADD, int NA>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                      const bf16* __restrict__ w, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const bf16* __restrict__ dres,
                                                      bf16* __restrict__ dx, float* __restrict__ part, int N, int C) {
-  __shared__ float red[4 * 2 * 64 * 8 * VPL];  // per wave: dw,db partial of its columns
+  constexpr int COLS = 64 * 8 * VPL;
+  __shared__ float red[NA * COLS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int C8 = C >> 3;
   const float inv_c = 1.f / (float)C;
-  f32x8 wv[VPL], adw[VPL], adb[VPL];
+  f32x8 wv[VPL], adw[VPL], adb[VPL], adx[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c8 = lane + i * 64;
     wv[i] = c8 < C8 ? to_f32(reinterpret_cast<const bf16x8*>(w)[c8]) : f32x8{0, 0, 0, 0, 0, 0, 0, 0};
     adw[i] = f32x8{0, 0, 0, 0, 0, 0, 0, 0};
-    adb[i] = f32x8{0, 0, 0, 0, 0, 0, 0, 0};
+    adb[i] = adw[i];
+    adx[i] = adw[i];
   }
   const int nw = gridDim.x * 4;
   for (int row = blockIdx.x * 4 + wid; row < N; row += nw) {
@@ -118,55 +126,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
       if (c8 < C8) {
         f32x8 o = (g[i] - s1 - xh[i] * s2) * rs;
         if (ADD) o += to_f32(reinterpret_cast<const bf16x8*>(dres + base)[c8]);
+        if (NA == 3) adx[i] += o;
         reinterpret_cast<bf16x8*>(dx + base)[c8] = to_bf16(o);
       }
     }
   }
-  // combine the 4 waves: wave 0..3 stores, then each thread sums a slice
-  float* my = red + wid * (2 * 64 * 8 * VPL);
+  // combine the 4 waves sequentially through one [NA][COLS] LDS image
+  for (int k = 0; k < 4; ++k) {
+    if (wid == k) {
 #pragma unroll
-  for (int i = 0; i < VPL; ++i)
+      for (int i = 0; i < VPL; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      my[(i * 64 + lane) * 8 + j] = adw[i][j];
-      my[64 * 8 * VPL + (i * 64 + lane) * 8 + j] = adb[i][j];
+        for (int j = 0; j < 8; ++j) {
+          const int c = (i * 64 + lane) * 8 + j;
+          const float a0 = adw[i][j], a1 = adb[i][j], a2 = adx[i][j];
+          if (k == 0) {
+            red[c] = a0;
+            red[COLS + c] = a1;
+            if (NA == 3) red[2 * COLS + c] = a2;
+          } else {
+            red[c] += a0;
+            red[COLS + c] += a1;
+            if (NA == 3) red[2 * COLS + c] += a2;
+          }
+        }
     }
-  __syncthreads();
-  const int per = 2 * 64 * 8 * VPL;
-  for (int k = threadIdx.x; k < per; k += 256) {
-    float t = red[k] + red[per + k] + red[2 * per + k] + red[3 * per + k];
-    // k < 64*8*VPL: dw column k ; else db column k - 64*8*VPL
-    const int half = 64 * 8 * VPL;
-    const int col = k < half ? k : k - half;
-    if (col < C) part[(size_t)blockIdx.x * 2 * C + (k < half ? 0 : C) + col] = t;
+    __syncthreads();
   }
-}
-
-// out[c] = sum_g part[g*stride + c] ; 16 waves per 64 columns
-__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int G, int C, int stride,
-                                                      bf16* __restrict__ out_bf16, float* __restrict__ out_f32) {
-  __shared__ float red[16][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (col < C) {
-    for (int g = wid; g < G; g += 16) s += part[(size_t)g * stride + col];
+  float* pp = part + (size_t)blockIdx.x * NA * C;
+  for (int k = threadIdx.x; k < NA * C; k += 256) {
+    const int a = k / C, c = k - a * C;
+    pp[k] = red[a * COLS + c];
   }
-  red[wid][lane] = s;
-  __syncthreads();
-  if (wid == 0) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][lane];
-    if (col < C) {
-      if (out_bf16) out_bf16[col] = (bf16)t;
-      if (out_f32) out_f32[col] = t;
-    }
-  }
-}
-
-void colsum(const float* part, int G, int C, int stride, bf16* out_bf16, float* out_f32, hipStream_t st) {
-  colsum_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, G, C, stride, out_bf16, out_f32);
 }
 
 #define LN_DISPATCH(VPL_, ...)                  \
@@ -187,15 +178,16 @@ static int vpl_for(int C) {
   return v;
 }
 
-int layernorm_fwd(const bf16* x, const bf16* r, const bf16* w, const bf16* b, bf16* h, bf16* y, float* mean,
-                  float* rstd, int N, int C, float eps, hipStream_t st) {
+int layernorm_fwd(const bf16* x, const bf16* r, const bf16* rb, const bf16* w, const bf16* b, bf16* h, bf16* y,
+                  float* mean, float* rstd, int N, int C, float eps, hipStream_t st) {
   if (C % 8 != 0 || C > 4096) return -2;
+  if (rb && !r) return -4;
   const int grid = (N + 3) / 4;
   const int vpl = vpl_for(C);
   if (r) {
-    LN_DISPATCH(vpl, ln_fwd_kernel<V, true><<<grid, 256, 0, st>>>(x, r, w, b, h, y, mean, rstd, N, C, eps))
+    LN_DISPATCH(vpl, ln_fwd_kernel<V, true><<<grid, 256, 0, st>>>(x, r, rb, w, b, h, y, mean, rstd, N, C, eps))
   } else {
-    LN_DISPATCH(vpl, ln_fwd_kernel<V, false><<<grid, 256, 0, st>>>(x, r, w, b, h, y, mean, rstd, N, C, eps))
+    LN_DISPATCH(vpl, ln_fwd_kernel<V, false><<<grid, 256, 0, st>>>(x, r, rb, w, b, h, y, mean, rstd, N, C, eps))
   }
   return 0;
 }
@@ -207,19 +199,25 @@ int layernorm_bwd_grid(int N) {
   return g;
 }
 
+// out: bf16 [NA*C] = dgamma | dbeta | (drbias); part: [grid][NA*C] f32;
+// scratch: colsum_scratch_floats(grid, NA*C)
 int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
-                  const bf16* dres, bf16* dx, float* part, bf16* dw, bf16* db, int N, int C, hipStream_t st) {
+                  const bf16* dres, bf16* dx, float* part, float* scratch, bf16* out, bool rbias, int N, int C,
+                  hipStream_t st) {
   if (C % 8 != 0 || C > 4096) return -2;
+  if (rbias && !dres) return -4;
   const int grid = layernorm_bwd_grid(N);
   const int vpl = vpl_for(C);
-  if (vpl > 4) return -3;  // LDS budget of the in-block combine
-  if (dres) {
-    LN_DISPATCH(vpl, ln_bwd_kernel<V, true><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
+  if (vpl > 4) return -3;  // register/LDS budget of the in-block combine
+  const int NA = rbias ? 3 : 2;
+  if (rbias) {
+    LN_DISPATCH(vpl, ln_bwd_kernel<V, true, 3><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
+  } else if (dres) {
+    LN_DISPATCH(vpl, ln_bwd_kernel<V, true, 2><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
   } else {
-    LN_DISPATCH(vpl, ln_bwd_kernel<V, false><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
+    LN_DISPATCH(vpl, ln_bwd_kernel<V, false, 2><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
   }
-  colsum(part, grid, C, 2 * C, dw, nullptr, st);
-  colsum(part + C, grid, C, 2 * C, db, nullptr, st);
+  colsum(part, grid, NA * C, NA * C, out, scratch, st);
   return 0;
 }
 

@@ -1,0 +1,97 @@
+// Column reductions (bias / norm-weight gradients) for gfx950.
+//
+// out[c] = Σ_r in[r][c] as a deterministic two-level tree: level 1 gives each
+// workgroup a 256-column (f32) / 512-column (bf16) stripe × a slice of rows,
+// 8 waves stride the slice, the waves combine in LDS and the block writes one
+// partial row; level 2 folds the ≤ a few dozen partial rows and writes bf16.
+// Enough workgroups to keep HBM busy (the single-level version with one
+// block per 64 columns was latency-bound at ~20 µs per call).
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+constexpr int RPB = 64;  // rows per level-1 workgroup
+
+__global__ __launch_bounds__(512) void colsum_f32_pass(const float* __restrict__ in, int G, int C, int ld, int rpb,
+                                                       float* __restrict__ out_part, bf16* __restrict__ out_bf16) {
+  __shared__ f32x4 red[8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = (blockIdx.x * 64 + lane) * 4;
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(G, r0 + rpb);
+  f32x4 s = {0, 0, 0, 0};
+  if (col < C) {
+#pragma unroll 4
+    for (int r = r0 + w; r < r1; r += 8) s += *reinterpret_cast<const f32x4*>(in + (size_t)r * ld + col);
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < C) {
+    f32x4 t = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) t += red[i][lane];
+    if (out_bf16) {
+      bf16x4 o = {(bf16)t[0], (bf16)t[1], (bf16)t[2], (bf16)t[3]};
+      *reinterpret_cast<bf16x4*>(out_bf16 + col) = o;
+    } else {
+      *reinterpret_cast<f32x4*>(out_part + (size_t)blockIdx.y * C + col) = t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void colsum_bf16_pass(const bf16* __restrict__ in, int N, int F, int rpb,
+                                                        float* __restrict__ out_part) {
+  __shared__ f32x8 red[8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c8 = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * rpb;
+  const int r1 = min(N, r0 + rpb);
+  f32x8 s = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c8 * 8 < F) {
+#pragma unroll 4
+    for (int r = r0 + w; r < r1; r += 8) s += to_f32(reinterpret_cast<const bf16x8*>(in + (size_t)r * F)[c8]);
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c8 * 8 < F) {
+    f32x8 t = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) t += red[i][lane];
+    float* o = out_part + (size_t)blockIdx.y * F + c8 * 8;
+    reinterpret_cast<f32x4*>(o)[0] = f32x4{t[0], t[1], t[2], t[3]};
+    reinterpret_cast<f32x4*>(o)[1] = f32x4{t[4], t[5], t[6], t[7]};
+  }
+}
+
+int colsum_scratch_floats(int G, int C) { return ((G + RPB - 1) / RPB) * C; }
+
+// part: [G][ld] f32 (first C columns used).  scratch: colsum_scratch_floats(G, C)
+void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st) {
+  const int gx = (C / 4 + 63) / 64;
+  if (G <= RPB) {
+    colsum_f32_pass<<<dim3(gx, 1), 512, 0, st>>>(part, G, C, ld, RPB, nullptr, out);
+    return;
+  }
+  const int gs = (G + RPB - 1) / RPB;
+  colsum_f32_pass<<<dim3(gx, gs), 512, 0, st>>>(part, G, C, ld, RPB, scratch, nullptr);
+  colsum_f32_pass<<<dim3(gx, 1), 512, 0, st>>>(scratch, gs, C, C, gs, nullptr, out);
+}
+
+int bias_grad_scratch_floats(long long N, int F) {
+  const int gs = (int)((N + 255) / 256);
+  return gs * F;
+}
+
+// db[f] = Σ_n dy[n][f]  (bf16 in, bf16 out); scratch: bias_grad_scratch_floats
+int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st) {
+  if (F % 8) return -2;
+  const int gx = (F / 8 + 63) / 64;
+  const int gs = (int)((N + 255) / 256);
+  colsum_bf16_pass<<<dim3(gx, gs), 512, 0, st>>>(dy, (int)N, F, 256, scratch);
+  const int gx2 = (F / 4 + 63) / 64;
+  colsum_f32_pass<<<dim3(gx2, 1), 512, 0, st>>>(scratch, gs, F, F, gs, nullptr, db);
+  return 0;
+}
+
+}  // namespace pdo

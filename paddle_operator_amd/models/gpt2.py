@@ -77,10 +77,11 @@ class Linear(nn.Module):
         self.bias = nn.Parameter(torch.zeros(fout)) if bias else None
 
     def forward(self, x):
-        return torch.nn.functional.linear(x, self.weight, self.bias)
+        return ops.linear(x, self.weight, self.bias)
 
     def forward_nobias(self, x):
-        return torch.nn.functional.linear(x, self.weight)
+        """Bias is applied by the consumer (fused into GELU / residual+LN)."""
+        return ops.linear(x, self.weight)
 
 
 class Block(nn.Module):
@@ -100,16 +101,16 @@ class Block(nn.Module):
     def forward(self, x, h):
         """x: residual stream, h: LN1(x) already computed by the caller.
 
-        Returns (x_out, ln1_of_next_input_not_applied) — the next block's LN1 is
-        fused with this block's final residual add by the caller.
+        Returns (x_mid, m, fc_proj_bias): the MLP branch output ``m`` WITHOUT
+        its bias — the caller fuses ``x_mid + m + bias`` with the next LayerNorm.
         """
         cfg = self.cfg
         a = ops.attention(self.qkv(h), cfg.n_head)
-        a = self.proj(a)
-        x, h2 = ops.add_layer_norm(x, a, self.ln2_w, self.ln2_b, cfg.ln_eps)
+        a = self.proj.forward_nobias(a)
+        x, h2 = ops.add_layer_norm(x, a, self.ln2_w, self.ln2_b, cfg.ln_eps, rbias=self.proj.bias)
         m = ops.bias_gelu(self.fc.forward_nobias(h2), self.fc.bias)
-        m = self.fc_proj(m)
-        return x, m
+        m = self.fc_proj.forward_nobias(m)
+        return x, m, self.fc_proj.bias
 
 
 class GPT2(nn.Module):
@@ -141,13 +142,13 @@ class GPT2(nn.Module):
         blk0 = self.blocks[0]
         h = ops.layer_norm(x, blk0.ln1_w, blk0.ln1_b, cfg.ln_eps)
         for i, blk in enumerate(self.blocks):
-            x, m = blk(x, h)
+            x, m, mb = blk(x, h)
             if i + 1 < len(self.blocks):
                 nb = self.blocks[i + 1]
-                x, h = ops.add_layer_norm(x, m, nb.ln1_w, nb.ln1_b, cfg.ln_eps)
+                x, h = ops.add_layer_norm(x, m, nb.ln1_w, nb.ln1_b, cfg.ln_eps, rbias=mb)
             else:
-                x, h = ops.add_layer_norm(x, m, self.lnf_w, self.lnf_b, cfg.ln_eps)
-        logits = torch.nn.functional.linear(h, self.wte)
+                x, h = ops.add_layer_norm(x, m, self.lnf_w, self.lnf_b, cfg.ln_eps, rbias=mb)
+        logits = ops.linear(h, self.wte)
         if targets is None:
             return logits[..., :cfg.vocab_size]
         return ops.cross_entropy(logits, targets, cfg.vocab_size)

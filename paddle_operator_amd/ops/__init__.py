@@ -100,34 +100,94 @@ def layer_norm(x, w, b, eps=1e-5):
 
 
 class _AddLayerNormFn(torch.autograd.Function):
-    """h = x + r ; y = LN(h).  Returns (h, y).  One read of x and r, one write
-    of h and y: the residual stream never makes a separate HBM round trip."""
+    """h = x + r (+ rbias) ; y = LN(h).  Returns (h, y).
+
+    One read of x and r, one write of h and y: the residual stream never makes
+    a separate HBM round trip.  ``rbias`` is the bias of the GEMM that produced
+    ``r`` (attention / MLP output projection) folded in; its gradient is the
+    column sum of dh, reduced inside the LayerNorm backward kernel."""
 
     @staticmethod
-    def forward(ctx, x, r, w, b, eps):
+    def forward(ctx, x, r, w, b, rbias, eps):
         m = _native.require_hip()
         x2 = x.reshape(-1, x.shape[-1])
         r2 = r.reshape(-1, r.shape[-1])
-        h, y, mean, rstd = m.add_layernorm_fwd(x2, r2, w, b, eps)
+        h, y, mean, rstd = m.add_layernorm_fwd(x2, r2, w, b, eps, rbias)
         ctx.save_for_backward(h, w, mean, rstd)
         ctx.shape = x.shape
+        ctx.has_rbias = rbias is not None
         return h.view(x.shape), y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dh, dy):
         m = _native.require_hip()
         h, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = m.layernorm_bwd_add(dy.reshape(h.shape).contiguous(), h, w, mean, rstd,
-                                         dh.reshape(h.shape).contiguous())
-        dx = dx.view(ctx.shape)
-        return dx, dx, dw, db, None
+        outs = m.layernorm_bwd_add(dy.reshape(h.shape).contiguous(), h, w, mean, rstd,
+                                   dh.reshape(h.shape).contiguous(), ctx.has_rbias)
+        dx = outs[0].view(ctx.shape)
+        drb = outs[3] if ctx.has_rbias else None
+        return dx, dx, outs[1], outs[2], drb, None
 
 
-def add_layer_norm(x, r, w, b, eps=1e-5):
+def add_layer_norm(x, r, w, b, eps=1e-5, rbias=None):
     if use_hip(x):
-        return _AddLayerNormFn.apply(x.contiguous(), r.contiguous(), w, b, eps)
-    h = x + r
+        return _AddLayerNormFn.apply(x.contiguous(), r.contiguous(), w, b, rbias, eps)
+    h = x + r if rbias is None else x + r + rbias
     return h, F.layer_norm(h, (h.shape[-1],), w, b, eps)
+
+
+# ----------------------------------------------------------------------------
+# linear with direct-to-arena weight gradient
+# ----------------------------------------------------------------------------
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T (+ b) on hipBLASLt (bias fused in the GEMM epilogue).
+
+    Backward writes dW straight into the parameter's slice of the flat
+    gradient arena (``addmm_`` with beta=1 — no separate gradient tensor, no
+    AccumulateGrad add kernel) and then signals the bucketed all-reduce that
+    the parameter is ready.  The bias gradient is a HIP column reduction."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        ctx.b = b
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        K = x.shape[-1]
+        Fo = dy.shape[-1]
+        dy2 = dy.reshape(-1, Fo)
+        x2 = x.reshape(-1, K)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ w).view(x.shape)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if _direct_ok(w):
+                w.grad.view(Fo, K).addmm_(dy2.t(), x2)
+                w._pdo_ready(w)
+            else:
+                dw = dy2.t() @ x2
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = _native.require_hip().bias_grad(dy2.contiguous()) if use_hip(dy2) else dy2.float().sum(0).to(dy.dtype)
+        return dx, dw, db
+
+
+def _direct_ok(p) -> bool:
+    g = p.grad
+    return (getattr(p, "_pdo_direct", False) and g is not None and g.is_contiguous()
+            and torch.is_grad_enabled() is False)
+
+
+def linear(x, w, b=None):
+    if use_hip(x):
+        return _LinearFn.apply(x, w, b)
+    return F.linear(x, w, b)
 
 
 # ----------------------------------------------------------------------------

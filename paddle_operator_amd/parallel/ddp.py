@@ -41,6 +41,8 @@ class BucketedDDP:
         if self.enabled:
             for s in flat.slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._hook))
+                # ops that write gradients straight into the arena signal here
+                s.param._pdo_ready = self._hook
 
     # -- API --------------------------------------------------------------
     def broadcast_params(self, src: int = 0):

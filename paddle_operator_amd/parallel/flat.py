@@ -53,6 +53,10 @@ def _round_up(x, m):
     return (x + m - 1) // m * m
 
 
+def _noop_ready(p):
+    return None
+
+
 def default_no_decay(name: str, p: torch.Tensor) -> bool:
     """Biases, norm weights and 1-D params are not decayed."""
     return p.dim() < 2
@@ -88,6 +92,10 @@ class FlatParams:
         for s in self.slots:
             s.param.data = self.params[s.offset:s.offset + s.numel].view(s.shape)
             s.param.grad = self.grads[s.offset:s.offset + s.numel].view(s.shape)
+            # ops.linear may write dW straight into the arena; parameters used
+            # in several places (tied embeddings) keep autograd accumulation
+            s.param._pdo_direct = s.name not in late_set
+            s.param._pdo_ready = _noop_ready
         # one weight-decay flag per ALIGN-element chunk
         wd = torch.zeros(off // ALIGN, dtype=torch.float32)
         for s in self.slots:

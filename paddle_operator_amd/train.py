@@ -63,6 +63,9 @@ class GPT2Trainer:
         self.B = micro_batch
         self.S = seq_len
         self.device = torch.device(device)
+        if self.device.type == "cuda":
+            from .utils.tuning import enable_tuned_gemms
+            enable_tuned_gemms()
         torch.manual_seed(seed)
         model = GPT2(cfg)
         model.to(device=self.device, dtype=dtype)

@@ -54,19 +54,21 @@ def test_layernorm(cuda, N, C):
     assert rel_err(b.grad, bf.grad) < 2e-2
 
 
-def test_add_layernorm(cuda):
+@pytest.mark.parametrize("N,C,with_rb", [(1024, 1024, False), (16384, 1024, True), (333, 768, True)])
+def test_add_layernorm(cuda, N, C, with_rb):
     ops = _ops()
-    N, C = 1024, 1024
     g = torch.Generator(device=cuda).manual_seed(1)
     x = torch.randn(N, C, device=cuda, generator=g).bfloat16().requires_grad_()
     r = torch.randn(N, C, device=cuda, generator=g).bfloat16().requires_grad_()
     w = (1 + 0.1 * torch.randn(C, device=cuda, generator=g)).bfloat16().requires_grad_()
     b = (0.1 * torch.randn(C, device=cuda, generator=g)).bfloat16().requires_grad_()
-    h, y = ops.add_layer_norm(x, r, w, b)
+    rb = (0.1 * torch.randn(C, device=cuda, generator=g)).bfloat16().requires_grad_() if with_rb else None
+    h, y = ops.add_layer_norm(x, r, w, b, rbias=rb)
     dh, dy = torch.randn_like(h), torch.randn_like(y)
     torch.autograd.backward([h, y], [dh, dy])
     xf, rf, wf, bf = (t.detach().float().requires_grad_() for t in (x, r, w, b))
-    hf = xf + rf
+    rbf = rb.detach().float().requires_grad_() if with_rb else None
+    hf = xf + rf + (rbf if with_rb else 0)
     yf = torch.nn.functional.layer_norm(hf, (C,), wf, bf, 1e-5)
     torch.autograd.backward([hf, yf], [dh.float(), dy.float()])
     assert rel_err(h, hf) < 1e-2
@@ -75,6 +77,55 @@ def test_add_layernorm(cuda):
     assert rel_err(r.grad, rf.grad) < 2e-2
     assert rel_err(w.grad, wf.grad) < 2e-2
     assert rel_err(b.grad, bf.grad) < 2e-2
+    if with_rb:
+        assert rel_err(rb.grad, rbf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,F", [(16384, 3072), (100, 1024)])
+def test_bias_grad_and_linear(cuda, N, F):
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(11)
+    K = 512
+    x = torch.randn(N, K, device=cuda, generator=g).bfloat16().requires_grad_()
+    w = (0.05 * torch.randn(F, K, device=cuda, generator=g)).bfloat16().requires_grad_()
+    b = torch.randn(F, device=cuda, generator=g).bfloat16().requires_grad_()
+    y = ops.linear(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yf = torch.nn.functional.linear(xf, wf, bf)
+    yf.backward(dy.float())
+    assert rel_err(y, yf) < 2e-2
+    assert rel_err(x.grad, xf.grad) < 2e-2
+    assert rel_err(w.grad, wf.grad) < 2e-2
+    assert rel_err(b.grad, bf.grad) < 2e-2
+
+
+def test_linear_direct_arena_grad(cuda):
+    """dW lands in the flat arena via addmm_ and the ready-callback fires once."""
+    from paddle_operator_amd.parallel.flat import FlatParams
+    from paddle_operator_amd import ops
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.randn(256, 128) * 0.05)
+            self.b = torch.nn.Parameter(torch.zeros(256))
+
+        def forward(self, x):
+            return ops.linear(x, self.w, self.b)
+
+    m = M().to(cuda).bfloat16()
+    fp_ = FlatParams(m, device=cuda)
+    seen = []
+    m.w._pdo_ready = lambda p: seen.append(p)
+    x = torch.randn(64, 128, device=cuda).bfloat16()
+    for _ in range(2):  # two micro-batches accumulate
+        m(x).float().sum().backward()
+    assert len(seen) == 2
+    ref = 2 * (torch.ones(64, 256, device=cuda).t() @ x.float())
+    assert rel_err(m.w.grad, ref) < 2e-2
+    assert m.w.grad.data_ptr() == fp_.grads[fp_.slots[[s.name for s in fp_.slots].index("w")].offset:].data_ptr()
 
 
 @pytest.mark.parametrize("N,F", [(1024, 4096), (77, 3072)])
