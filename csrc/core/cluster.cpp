@@ -26,7 +26,7 @@ Cluster::Cluster(ClusterOptions opt) : opt_(std::move(opt)) {
   }
   store_.reset(new store::Store(clock_));
   kv_.reset(new kv::KVStore(clock_));
-  kvc_.reset(new kv::LocalClient(kv_.get(), "127.0.0.1:2379"));
+  kvc_.reset(new kv::LocalClient(kv_.get(), opt_.kv_endpoint));
   ports_.reset(opt_.port_start, opt_.port_end);
   api_.reset(new StoreApi(store_.get()));
   sched_.reset(new Scheduler(store_.get(), opt_.nodes));

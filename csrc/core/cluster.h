@@ -36,6 +36,7 @@ struct ClusterOptions {
   double kubelet_config_retry_s = -1;  // <0: mode default (compat 1 s, fast event-driven)
   int port_start = 35000, port_end = 65000;
   std::string namespace_;
+  std::string kv_endpoint = "127.0.0.1:2379";  // advertised to elastic pods (PADDLE_ELASTIC_SERVER)
 };
 
 class Cluster {

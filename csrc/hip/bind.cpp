@@ -260,6 +260,74 @@ void flatten_scale(std::vector<at::Tensor> ts, at::Tensor flat, std::vector<int6
   CHECK_RC(rc, "flatten/unflatten");
 }
 
+// ---------------------------------------------------------------- device / IPC bootstrap
+// (launcher: hipSetDevice before any other HIP call, intra-node hipIpc handle
+// exchange to probe/warm the xGMI peer links before the RCCL communicator)
+#define HIP_OK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    TORCH_CHECK(e_ == hipSuccess, #x " failed: ", hipGetErrorString(e_));            \
+  } while (0)
+
+py::dict device_info(int dev) {
+  hipDeviceProp_t p;
+  HIP_OK(hipGetDeviceProperties(&p, dev));
+  char bus[64] = {0};
+  HIP_OK(hipDeviceGetPCIBusId(bus, sizeof bus, dev));
+  py::dict d;
+  d["name"] = std::string(p.name);
+  d["gcn_arch"] = std::string(p.gcnArchName);
+  d["pci_bus_id"] = std::string(bus);
+  d["compute_units"] = p.multiProcessorCount;
+  d["total_mem"] = (int64_t)p.totalGlobalMem;
+  d["lds_per_block"] = (int64_t)p.sharedMemPerBlock;
+  d["clock_khz"] = p.clockRate;
+  d["l2_bytes"] = p.l2CacheSize;
+  d["warp_size"] = p.warpSize;
+  return d;
+}
+
+int set_device(int dev) {
+  HIP_OK(hipSetDevice(dev));
+  int cur = -1;
+  HIP_OK(hipGetDevice(&cur));
+  return cur;
+}
+
+py::bytes ipc_get_handle(at::Tensor t) {
+  CHECK_DEV(t);
+  hipIpcMemHandle_t h;
+  HIP_OK(hipIpcGetMemHandle(&h, t.data_ptr()));
+  return py::bytes(reinterpret_cast<const char*>(&h), sizeof h);
+}
+
+// map a peer's exported buffer into this process as a uint8 tensor
+at::Tensor ipc_open_handle(py::bytes handle, int64_t nbytes, int64_t device) {
+  std::string hs = handle;
+  TORCH_CHECK(hs.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
+  hipIpcMemHandle_t h;
+  memcpy(&h, hs.data(), sizeof h);
+  void* p = nullptr;
+  HIP_OK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  auto opts = at::TensorOptions().dtype(at::kByte).device(at::Device(at::kCUDA, (c10::DeviceIndex)device));
+  return at::from_blob(p, {nbytes}, [](void* ptr) { (void)hipIpcCloseMemHandle(ptr); }, opts);
+}
+
+bool can_access_peer(int dev, int peer) {
+  int ok = 0;
+  HIP_OK(hipDeviceCanAccessPeer(&ok, dev, peer));
+  return ok != 0;
+}
+
+bool enable_peer_access(int peer) {
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return true;
+  }
+  return e == hipSuccess;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_pdo_hip, m) {
@@ -282,5 +350,11 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("scale_", &scale_);
   m.def("flatten_scale", &flatten_scale);
+  m.def("device_info", &device_info);
+  m.def("set_device", &set_device);
+  m.def("ipc_get_handle", &ipc_get_handle);
+  m.def("ipc_open_handle", &ipc_open_handle);
+  m.def("can_access_peer", &can_access_peer);
+  m.def("enable_peer_access", &enable_peer_access);
   m.attr("arch") = "gfx950";
 }

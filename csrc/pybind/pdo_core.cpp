@@ -122,6 +122,7 @@ static pdo::ClusterOptions cluster_opts(const py::kwargs& kw) {
       o.port_start = pr.first;
       o.port_end = pr.second;
     } else if (k == "namespace") o.namespace_ = v.cast<std::string>();
+    else if (k == "kv_endpoint") o.kv_endpoint = v.cast<std::string>();
     else if (k == "nodes") {
       for (auto n : v.cast<py::list>()) {
         auto d = n.cast<py::dict>();

@@ -1,0 +1,140 @@
+"""Rank bootstrap on MI355X: device affinity → RCCL communicator → readiness.
+
+Order matters on ROCm (BASELINE north star: "RCCL-init / HIP device-affinity
+path"):
+
+1. ``pin``: CPU affinity to the GPU's NUMA-local cores (sysfs, no HIP).
+2. ``hipSetDevice(local_rank)`` (``torch.cuda.set_device``) BEFORE any other
+   HIP call, so the RCCL communicator and every allocation bind the right GPU.
+3. ``init_process_group("nccl")`` — on ROCm the nccl backend IS RCCL; the
+   unique id travels through rank 0's TCPStore (or pdo-kv for elastic jobs);
+   ``device_id`` makes the communicator eager (created now, not lazily at the
+   first collective), so "ready" really means the xGMI rings are up.
+4. Optional intra-node IPC probe: every rank exports a staging buffer with
+   ``hipIpcGetMemHandle``; peers on the same node open it
+   (``hipIpcOpenMemHandle``) and copy over xGMI — validates peer access and
+   measures per-pair bandwidth before training (bucket sizing input).
+5. Warm-up all-reduce, then a readiness record in pdo-kv
+   (``/pdo/<job>/ready/<rank>``) and a ``PDO_READY`` log line.
+"""
+from __future__ import annotations
+
+import datetime
+import json
+import os
+import socket
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..utils import topology
+
+
+@dataclass
+class Bootstrapped:
+    rank: int
+    world: int
+    local_rank: int
+    device: torch.device
+    backend: str
+    t_start: float
+    t_pg: float = 0.0
+    t_ready: float = 0.0
+    ipc_gbps: Optional[dict] = None
+
+
+def _env_int(k, d):
+    return int(os.environ.get(k, str(d)))
+
+
+def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ipc_probe: bool = False,
+         store=None) -> Bootstrapped:
+    rank = _env_int("RANK", 0)
+    world = _env_int("WORLD_SIZE", 1)
+    local = _env_int("LOCAL_RANK", 0)
+    gpu = torch.cuda.is_available()
+    if backend is None:
+        backend = "nccl" if gpu else "gloo"
+    topology.pin_to_gpu(local)  # before HIP init: uses sysfs only
+    if gpu:
+        torch.cuda.set_device(local)  # hipSetDevice
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    b = Bootstrapped(rank, world, local, dev, backend, t_start)
+    if world > 1 and not dist.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = dev
+        if store is not None:
+            kw["store"] = store
+        else:
+            kw["init_method"] = f"tcp://{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        if ipc_probe and gpu:
+            b.ipc_gbps = ipc_probe_run(dev)
+        # warm-up: forces the communicator + first ring setup before "ready"
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        if gpu:
+            torch.cuda.synchronize(dev)
+    b.t_pg = time.time()
+    return b
+
+
+def ipc_probe_run(dev: torch.device, nbytes: int = 64 << 20) -> dict:
+    """Exchange hipIpc handles with same-node peers and time a 64 MiB copy per pair."""
+    m = _native.require_hip()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    node = os.environ.get("PDO_NODE_NAME") or socket.gethostname()
+    buf = torch.full((nbytes,), rank % 251, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    rec = {"node": node, "pid": os.getpid(), "handle": m.ipc_get_handle(buf).hex(),
+           "device": torch.cuda.current_device(), "bdf": m.device_info(torch.cuda.current_device())["pci_bus_id"]}
+    allrec = [None] * world
+    dist.all_gather_object(allrec, rec)
+    out = {}
+    peers = [r for r, x in enumerate(allrec) if x["node"] == node and r != rank]
+    local_dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    for r in peers:
+        try:
+            peer = m.ipc_open_handle(bytes.fromhex(allrec[r]["handle"]), nbytes, dev.index)
+        except RuntimeError as e:  # same GPU / no peer access
+            out[r] = f"unavailable: {e}"
+            continue
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(4):
+            local_dst.copy_(peer, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / 4
+        ok = bool((local_dst[:4096] == (r % 251)).all().item())
+        out[r] = round(nbytes / dt / 1e9, 1) if ok else "mismatch"
+        del peer
+    dist.barrier()  # keep every exported buffer alive until all peers are done
+    del buf
+    return out
+
+
+def report_ready(b: Bootstrapped, job_key: str, kv_endpoints: str = "", extra: Optional[dict] = None):
+    b.t_ready = time.time()
+    rec = {"rank": b.rank, "world": b.world, "t_start": b.t_start, "t_pg": b.t_pg, "t_ready": b.t_ready,
+           "host": socket.gethostname(), "pid": os.getpid(), "backend": b.backend}
+    if b.ipc_gbps is not None:
+        rec["ipc_gbps"] = b.ipc_gbps
+    if extra:
+        rec.update(extra)
+    line = "PDO_READY " + json.dumps(rec)
+    print(line, flush=True)
+    if kv_endpoints:
+        from ..kv.client import KVClient
+        try:
+            KVClient(kv_endpoints).put(f"/pdo/{job_key}/ready/{b.rank}", json.dumps(rec))
+        except Exception as e:  # readiness reporting must never kill a rank
+            print(f"[pdo-launch] ready report to kv failed: {e}", flush=True)
+    return rec

@@ -1,0 +1,220 @@
+"""Elastic agent: KV membership → rendezvous → supervised RCCL worker.
+
+The reference operator only keeps ``/paddle/<ns>-<name>/np`` in etcd in sync
+with ``spec.worker.replicas`` (controllers/paddlejob_elastic.go:27-55) and
+gives elastic pods OnFailure restarts plus the PADDLE_ELASTIC_* env
+(controllers/paddlejob_helper.go:333-348); re-rendezvous is left to the Paddle
+image.  An RCCL communicator cannot be resized, so pdo's agent owns the
+worker process and rebuilds the world on every membership/np change:
+
+KV layout under ``/paddle/<job-id>/`` (pdo-kv, etcd-v3 JSON gateway):
+
+* ``np``                — desired world size; the agent creates it from
+  PADDLE_ELASTIC_NP if absent (the controller never creates it, only updates).
+* ``nodes/<id>``        — membership, value ``{"id","host","port"}``, bound to a
+  lease of ``ttl`` seconds kept alive by the agent: a killed pod drops out
+  after ``ttl`` without anyone deleting it.
+* ``rdzv/<gen>/<id>``   — per-generation arrival barrier.  ``gen`` is a digest
+  of (np, the first np member ids), so every agent that sees the same
+  membership computes the same generation, the same rank order and the same
+  TCPStore port (``PADDLE_PORT + 2 + gen % 16`` on rank 0's host; each pod owns
+  20 ports, paddlejob_helper.go:215-279).
+* ``done/<id>``         — written when a worker finished all steps.
+
+Loop: register → wait for ≥ np live members (``PADDLE_ELASTIC_TIMEOUT``) →
+barrier on ``rdzv/<gen>`` → spawn ``pdo-launch --worker`` with RANK/WORLD_SIZE/
+MASTER_* → watch np + membership every ``poll`` s; on change SIGTERM the
+worker (rank 0 checkpoints in its SIGTERM handler) and rendezvous again; on
+worker failure with unchanged membership restart it (``max_restarts``).
+Workers resume from the newest checkpoint, whose flat-arena layout does not
+depend on the world size.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional, Tuple
+
+from ..kv.client import KVClient
+
+STORE_BASE_OFFSET = 2
+STORE_PORTS = 16
+
+
+def _log(msg):
+    print(f"[pdo-elastic {time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+class ElasticAgent:
+    def __init__(self, kv: KVClient, job_id: str, member_id: int, host: str, port: int, np_default: int,
+                 timeout: float = 60.0, ttl: int = 6, poll: float = 0.25, max_restarts: int = 3):
+        self.kv = kv
+        self.job = job_id
+        self.id = int(member_id)
+        self.host, self.port = host, int(port)
+        self.np_default = int(np_default)
+        self.timeout = timeout
+        self.ttl = ttl
+        self.poll = poll
+        self.max_restarts = max_restarts
+        self.prefix = f"/paddle/{job_id}/"
+        self.lease = 0
+        self._ka = None
+        self.proc: Optional[subprocess.Popen] = None
+        self.history: List[dict] = []
+
+    # ------------------------------------------------------------ membership
+    def register(self):
+        self.kv.put_if_absent(self.prefix + "np", str(self.np_default))
+        self.lease = self.kv.lease_grant(self.ttl)
+        self.kv.put(self.prefix + f"nodes/{self.id:06d}",
+                    json.dumps({"id": self.id, "host": self.host, "port": self.port}), lease=self.lease)
+        self._ka = self.kv.keepalive_thread(self.lease, self.ttl)
+
+    def deregister(self):
+        if self._ka is not None:
+            self._ka.set()
+        try:
+            if self.lease:
+                self.kv.lease_revoke(self.lease)
+        except Exception:
+            pass
+
+    def np(self) -> int:
+        v = self.kv.get(self.prefix + "np")
+        try:
+            return int(v) if v is not None else self.np_default
+        except ValueError:
+            return self.np_default
+
+    def members(self) -> List[dict]:
+        kvs = self.kv.get_prefix(self.prefix + "nodes/")
+        out = [json.loads(v) for _, v in sorted(kvs.items())]
+        return sorted(out, key=lambda m: m["id"])
+
+    @staticmethod
+    def plan(np_: int, members: List[dict]) -> Tuple[int, List[dict]]:
+        """Deterministic generation id + rank order for (np, membership)."""
+        chosen = members[:np_]
+        h = hashlib.sha1(json.dumps([np_, [m["id"] for m in chosen]]).encode()).hexdigest()
+        return int(h[:8], 16), chosen
+
+    # ------------------------------------------------------------ rendezvous
+    def rendezvous(self) -> Optional[dict]:
+        """Block until a generation forms that includes this member.
+
+        Returns the world description, or None on timeout."""
+        deadline = time.time() + self.timeout
+        while time.time() < deadline:
+            np_ = self.np()
+            mem = self.members()
+            if len(mem) < np_:
+                time.sleep(self.poll)
+                continue
+            gen, chosen = self.plan(np_, mem)
+            ids = [m["id"] for m in chosen]
+            if self.id not in ids:  # surplus member: stand by until np grows / someone leaves
+                time.sleep(self.poll)
+                deadline = time.time() + self.timeout
+                continue
+            key = self.prefix + f"rdzv/{gen:08x}/"
+            self.kv.put(key + f"{self.id:06d}", "1", lease=self.lease)
+            # every chosen member must arrive while the plan stays valid
+            t_bar = time.time() + min(10.0, max(1.0, deadline - time.time()))
+            while time.time() < t_bar:
+                if len(self.kv.get_prefix(key)) >= np_:
+                    master = chosen[0]
+                    return {"gen": gen, "np": np_, "rank": ids.index(self.id), "ids": ids,
+                            "master_addr": master["host"],
+                            "master_port": master["port"] + STORE_BASE_OFFSET + gen % STORE_PORTS}
+                if self.plan(self.np(), self.members())[0] != gen:
+                    break
+                time.sleep(self.poll / 2)
+        return None
+
+    def changed(self, world: dict) -> bool:
+        np_ = self.np()
+        mem = self.members()
+        return len(mem) < np_ or self.plan(np_, mem)[0] != world["gen"]
+
+    # ------------------------------------------------------------ supervision
+    def spawn(self, world: dict, worker_argv: List[str]) -> subprocess.Popen:
+        env = dict(os.environ)
+        env.update({"RANK": str(world["rank"]), "WORLD_SIZE": str(world["np"]), "LOCAL_RANK": "0",
+                    "LOCAL_WORLD_SIZE": "1", "MASTER_ADDR": world["master_addr"],
+                    "MASTER_PORT": str(world["master_port"]), "PDO_ELASTIC_GEN": f"{world['gen']:08x}"})
+        cmd = [sys.executable, "-m", "paddle_operator_amd.launch", "--worker"] + worker_argv
+        return subprocess.Popen(cmd, env=env, start_new_session=True)
+
+    def stop_worker(self, grace: float = 20.0):
+        p = self.proc
+        if p is None or p.poll() is not None:
+            return
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            return
+        try:
+            p.wait(grace)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+
+    def run(self, worker_argv: List[str]) -> int:
+        self.register()
+        restarts = 0
+        try:
+            while True:
+                t0 = time.time()
+                world = self.rendezvous()
+                if world is None:
+                    _log(f"rendezvous timed out after {self.timeout}s")
+                    return 3
+                _log(f"gen {world['gen']:08x}: rank {world['rank']}/{world['np']} master "
+                     f"{world['master_addr']}:{world['master_port']} (rdzv {time.time() - t0:.2f}s)")
+                self.history.append(world)
+                self.proc = self.spawn(world, worker_argv)
+                while True:
+                    rc = self.proc.poll()
+                    if rc is not None:
+                        break
+                    if self.changed(world):
+                        _log("membership/np changed → stopping worker for re-rendezvous")
+                        self.stop_worker()
+                        rc = None
+                        break
+                    time.sleep(self.poll)
+                if rc is None:
+                    continue
+                if rc == 0:
+                    self.kv.put(self.prefix + f"done/{self.id:06d}", json.dumps({"gen": world["gen"]}))
+                    return 0
+                if self.changed(world):
+                    continue  # a peer left: not this worker's fault
+                restarts += 1
+                _log(f"worker exited rc={rc}; restart {restarts}/{self.max_restarts}")
+                if restarts > self.max_restarts:
+                    return rc
+        finally:
+            self.stop_worker(5.0)
+            self.deregister()
+
+
+def _strip(argv: List[str]) -> List[str]:
+    return [a for a in argv if a not in ("--elastic", "--worker")]
+
+
+def run_agent(args, jenv, argv: List[str]) -> int:
+    eps = jenv.kv_endpoints()
+    if not eps:
+        raise SystemExit("elastic mode needs PADDLE_ELASTIC_SERVER (or PDO_KV)")
+    agent = ElasticAgent(KVClient(eps), jenv.elastic_job_id or jenv.job_key(), jenv.trainer_id, jenv.pod_ip,
+                         jenv.port, jenv.elastic_np or jenv.trainers_num, timeout=float(jenv.elastic_timeout),
+                         ttl=int(os.environ.get("PDO_ELASTIC_TTL", "6")))
+    signal.signal(signal.SIGTERM, lambda *a: sys.exit(143))
+    return agent.run(_strip(argv))

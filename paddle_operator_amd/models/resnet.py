@@ -1,0 +1,86 @@
+"""ResNet-50 (BASELINE configs 2, 3, 5: collective ResNet-50 on 1 / 8 MI355X,
+elastic ResNet-50) — written out here because torchvision is not part of the
+image.  Standard v1.5 bottleneck architecture (stride on the 3×3 conv).
+
+MI355X choices: channels_last activations + bf16 autocast so MIOpen picks
+its NHWC implicit-GEMM convolutions on the matrix cores; BatchNorm in fp32
+(autocast keeps it there); parameters live in a flat fp32 arena
+(parallel.flat) so the gradient all-reduce buckets are slices.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, downsample=None):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x
+        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        out = F.relu(self.bn2(self.conv2(out)), inplace=True)
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            idt = self.downsample(x)
+        return F.relu(out + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, width=64):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        cin = width
+        stages = []
+        for i, n in enumerate(layers):
+            w = width * (2 ** i)
+            stride = 1 if i == 0 else 2
+            blocks = []
+            for j in range(n):
+                ds = None
+                if j == 0 and (stride != 1 or cin != w * Bottleneck.expansion):
+                    ds = nn.Sequential(nn.Conv2d(cin, w * Bottleneck.expansion, 1, stride=stride, bias=False),
+                                       nn.BatchNorm2d(w * Bottleneck.expansion))
+                blocks.append(Bottleneck(cin, w, stride if j == 0 else 1, ds))
+                cin = w * Bottleneck.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        for m in self.modules():  # zero-init last BN of each block (standard large-batch recipe)
+            if isinstance(m, Bottleneck):
+                nn.init.zeros_(m.bn3.weight)
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        x = F.max_pool2d(x, 3, 2, 1)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000):
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def resnet18_like_tiny(num_classes=10):
+    """Tiny variant for CPU tests."""
+    return ResNet((1, 1, 1, 1), num_classes, width=8)

@@ -86,12 +86,19 @@ class FlatParams:
         self.numel = off
         self.params = torch.zeros(off, dtype=dtype, device=device)
         self.grads = torch.zeros(off, dtype=dtype, device=device)
+        # keep each parameter's memory format (e.g. channels_last conv weights
+        # for MIOpen NHWC kernels): the arena slice is viewed with its strides
+        self._strides = {}
+        for s in self.slots:
+            p = s.param
+            dense = p.is_contiguous() or (p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last))
+            self._strides[s.name] = tuple(p.stride()) if dense else None
         with torch.no_grad():
             for s in self.slots:
-                self.params[s.offset:s.offset + s.numel].copy_(s.param.detach().reshape(-1))
+                self._view(self.params, s).copy_(s.param.detach())
         for s in self.slots:
-            s.param.data = self.params[s.offset:s.offset + s.numel].view(s.shape)
-            s.param.grad = self.grads[s.offset:s.offset + s.numel].view(s.shape)
+            s.param.data = self._view(self.params, s)
+            s.param.grad = self._view(self.grads, s)
             # ops.linear may write dW straight into the arena; parameters used
             # in several places (tied embeddings) keep autograd accumulation
             s.param._pdo_direct = s.name not in late_set
@@ -105,6 +112,11 @@ class FlatParams:
                 wd[c0:c1] = 1.0
         self.decay_chunks = wd.to(device)
         self.buckets = self._make_buckets(bucket_bytes)
+
+    def _view(self, buf, s):
+        seg = buf[s.offset:s.offset + s.numel]
+        st = self._strides.get(s.name)
+        return seg.as_strided(s.shape, st) if st is not None else seg.view(s.shape)
 
     def _make_buckets(self, bucket_bytes):
         esz = torch.empty((), dtype=self.dtype).element_size()
@@ -136,7 +148,7 @@ class FlatParams:
         """Re-point .grad at the arena (after anything replaced it)."""
         for s in self.slots:
             g = s.param.grad
-            view = self.grads[s.offset:s.offset + s.numel].view(s.shape)
+            view = self._view(self.grads, s)
             if g is None or g.data_ptr() != view.data_ptr():
                 if g is not None:
                     view.copy_(g)

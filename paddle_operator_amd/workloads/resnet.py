@@ -1,0 +1,92 @@
+"""ResNet-50 data-parallel training step (collective mode)."""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from ..models.resnet import resnet18_like_tiny, resnet50
+from ..parallel.ddp import BucketedDDP
+from ..parallel.flat import FlatParams
+
+
+class FlatSGD:
+    """Momentum SGD over the flat fp32 arena (3 bulk ops per step)."""
+
+    def __init__(self, flat: FlatParams, lr=0.1, momentum=0.9, weight_decay=5e-5):
+        self.flat, self.lr, self.mom, self.wd = flat, lr, momentum, weight_decay
+        self.buf = torch.zeros_like(flat.params)
+        self.decay = flat.decay_chunks.repeat_interleave(flat.numel // flat.decay_chunks.numel())
+        self.step_count = 0
+
+    @torch.no_grad()
+    def step(self, grad_scale=1.0):
+        g = self.flat.grads
+        if grad_scale != 1.0:
+            g.mul_(grad_scale)
+        g.addcmul_(self.decay, self.flat.params, value=self.wd)
+        self.buf.mul_(self.mom).add_(g)
+        self.flat.params.add_(self.buf, alpha=-self.lr)
+        self.step_count += 1
+
+    def state_dict(self):
+        return {"buf": self.buf, "step": self.step_count}
+
+    def load_state_dict(self, sd):
+        self.buf.copy_(sd["buf"])
+        self.step_count = int(sd["step"])
+
+
+class ResNetTrainer:
+    def __init__(self, batch: int, device, tiny: bool = False, bucket_mb: int = 25, channels_last: bool = True):
+        self.device = torch.device(device)
+        self.B = batch
+        self.tiny = tiny
+        model = (resnet18_like_tiny() if tiny else resnet50()).to(self.device)
+        self.cl = channels_last and self.device.type == "cuda"
+        if self.cl:
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
+        self.flat = FlatParams(model, dtype=torch.float32, device=self.device, bucket_bytes=bucket_mb << 20)
+        self.ddp = BucketedDDP(self.flat)
+        self.opt = FlatSGD(self.flat)
+        self.res = 32 if tiny else 224
+        self.classes = 10 if tiny else 1000
+        self.gen = torch.Generator(device=self.device).manual_seed(dist.get_rank() if dist.is_initialized() else 0)
+
+    def sync_initial_weights(self):
+        self.ddp.broadcast_params(0)
+        if self.ddp.world > 1:
+            for b in self.model.buffers():
+                dist.broadcast(b, 0)
+
+    def batch(self):
+        x = torch.randn(self.B, 3, self.res, self.res, device=self.device, generator=self.gen)
+        if self.cl:
+            x = x.to(memory_format=torch.channels_last)
+        y = torch.randint(0, self.classes, (self.B,), device=self.device, generator=self.gen)
+        return x, y
+
+    def step(self):
+        x, y = self.batch()
+        self.flat.zero_grad()
+        self.ddp.prepare()
+        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == "cuda"):
+            out = self.model(x)
+        loss = F.cross_entropy(out.float(), y)
+        loss.backward()
+        self.ddp.finish()
+        self.opt.step(self.ddp.grad_scale)
+        return loss
+
+    def state_dict(self):
+        return {"params": self.flat.params, "opt_buf": self.opt.buf, "buffers": {k: v for k, v in
+                                                                                  self.model.named_buffers()}}
+
+    def load_state_dict(self, sd):
+        self.flat.params.copy_(sd["params"].to(self.flat.params.device))
+        self.opt.buf.copy_(sd["opt_buf"].to(self.opt.buf.device))
+        bufs = dict(self.model.named_buffers())
+        for k, v in sd.get("buffers", {}).items():
+            if k in bufs:
+                bufs[k].copy_(v.to(bufs[k].device))
