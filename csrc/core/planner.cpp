@@ -159,6 +159,16 @@ Plan reconcile(const Observed& obs, const Options& opt, HostPorts* ports, double
         return p;
       }
     }
+    // fast mode: the reference leaves the Service of a scaled-in pod behind
+    // until the job is cleaned up (paddlejob_controller.go:161-191); drop it
+    if (!compat) {
+      for (auto& s : obs.services) {
+        auto ri = build::extract_name_index(obj_name(s));
+        const api::ResourceSpec* rs = job.spec.role(ri.first);
+        if (rs && ri.second >= rs->replicas && !terminating(s))
+          p.actions.push_back(act(Op::DeleteService, obj_name(s)));
+      }
+    }
   }
 
   // ---------------------------------------------------------- 8. host ports
@@ -246,6 +256,8 @@ Plan reconcile(const Observed& obs, const Options& opt, HostPorts* ports, double
     std::set<std::string> existing;
     for (auto& pod : obs.pods) existing.insert(obj_name(pod));
     bool created = false;
+    build::Options bopt = opt.build;
+    bopt.volcano = opt.volcano;  // --scheduling=volcano also stamps schedulerName + group annotations
     for (auto& role : api::role_order()) {
       const api::ResourceSpec* rs = job.spec.role(role);
       const api::ResourceStatus* st = job.status.role(role);
@@ -254,7 +266,7 @@ Plan reconcile(const Observed& obs, const Options& opt, HostPorts* ports, double
       for (int i = 0; i < rs->replicas; ++i) {
         const std::string name = build::res_name(job.name(), role, i);
         if (existing.count(name)) continue;
-        Action a = act(Op::CreatePod, name, build::construct_pod(job, role, i, opt.build));
+        Action a = act(Op::CreatePod, name, build::construct_pod(job, role, i, bopt));
         a.role = role;
         p.actions.push_back(a);
         created = true;

@@ -409,8 +409,11 @@ PYBIND11_MODULE(_pdo_core, m) {
       .def("free_gpus", [](PyCluster& c) { return c.c->scheduler().free_gpus(); })
       .def("queue_len", [](PyCluster& c) { return c.c->controller().queue().len(); })
       .def("reconcile", [](PyCluster& c, const std::string& ns, const std::string& name) {
-        py::gil_scoped_release g;
-        auto r = c.c->controller().reconcile(ns, name);
+        decltype(c.c->controller().reconcile(ns, name)) r;
+        {
+          py::gil_scoped_release g;
+          r = c.c->controller().reconcile(ns, name);
+        }
         return py::make_tuple(r.step, r.requeue, r.requeue_after, r.error, r.actions);
       })
       .def("serve", [](PyCluster& c, const std::string& addr) {

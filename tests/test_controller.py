@@ -1,0 +1,384 @@
+"""Control plane (native ``_pdo_core``) on CPU.
+
+Mirrors the reference's only behavioural test — the envtest spec
+controllers/paddlejob_controller_test.go:32-113 (wide-and-deep, Service
+mode, PS 3 / worker 2 → status refs 3/2, mode PS; update to PS 1 / worker 4
+→ refs 1/4) — and then covers what envtest never exercised
+(controllers/suite_test.go:73-77 runs without Volcano, etcd, init image or
+exec): builders' env contract, ConfigMap endpoint table, Host mode ports,
+Volcano gang, clean-pod policies, finalizer, failure, elastic ``np`` sync,
+compat-mode sequencing, the REST apiserver and the exec agent running real
+pdo-launch ranks.
+"""
+import json
+import os
+import socket
+import sys
+import time
+import urllib.request
+
+import pytest
+
+from paddle_operator_amd.api import types as T
+
+core_mod = pytest.importorskip("paddle_operator_amd._pdo_core")
+from paddle_operator_amd.controller import LocalCluster  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+POD = {"spec": {"containers": [{"name": "paddle", "image": "demo:v1"}]}}
+POD_NEVER = {"spec": {"restartPolicy": "Never", "containers": [{"name": "paddle", "image": "demo:v1"}]}}
+
+
+def refs(cl, name, role):
+    st = (cl.job(name) or {}).get("status") or {}
+    return len((st.get(role) or {}).get("refs") or [])
+
+
+def env_of(pod):
+    out = {}
+    for e in pod["spec"]["containers"][0].get("env", []):
+        out[e["name"]] = e.get("value", e.get("valueFrom"))
+    return out
+
+
+@pytest.fixture(params=["fast", "compat"])
+def sim(request):
+    cl = LocalCluster(mode=request.param, agent="sim", virtual_clock=True)
+    yield cl
+    cl.stop()
+
+
+# ----------------------------------------------------------------------------- reference envtest spec
+def test_reference_envtest_wide_and_deep_service(sim):
+    job = T.paddlejob("wide-and-deep-service", clean_pod_policy="Never", intranet="Service",
+                      ps={"replicas": 3, "template": POD_NEVER}, worker={"replicas": 2, "template": POD_NEVER})
+    sim.create(job)
+    assert sim.wait(lambda: refs(sim, "wide-and-deep-service", "ps") == 3 and
+                    refs(sim, "wide-and-deep-service", "worker") == 2, timeout=10)
+    j = sim.job("wide-and-deep-service")
+    assert j["status"]["mode"] == T.Mode.PS
+    j["spec"]["ps"]["replicas"] = 1
+    j["spec"]["worker"]["replicas"] = 4
+    sim.update(j)
+    assert sim.wait(lambda: refs(sim, "wide-and-deep-service", "ps") == 1 and
+                    refs(sim, "wide-and-deep-service", "worker") == 4, timeout=10)
+    names = sorted(p["metadata"]["name"] for p in sim.pods("wide-and-deep-service"))
+    assert names == ["wide-and-deep-service-ps-0"] + [f"wide-and-deep-service-worker-{i}" for i in range(4)]
+    # one Service per pod, named like the pod; Service-mode endpoints use pod names
+    assert sim.get("Service", "wide-and-deep-service-worker-3") is not None
+    w0 = sim.get("Pod", "wide-and-deep-service-worker-0")
+    assert env_of(w0)["POD_IP"] == "wide-and-deep-service-worker-0"
+    assert w0["spec"]["containers"][0]["ports"] == [{"containerPort": 2379}]
+    svcs = {s["metadata"]["name"] for s in sim.list("Service", "default")}
+    if sim.opts["mode"] == "fast":  # fast mode also drops Services of scaled-in pods
+        assert "wide-and-deep-service-ps-2" not in svcs
+    else:  # reference behaviour: they stay until cleanup
+        assert "wide-and-deep-service-ps-2" in svcs
+
+
+# ----------------------------------------------------------------------------- builders
+def test_pod_builder_env_contract():
+    c = core_mod
+    job = T.paddlejob("pj", ps={"replicas": 2, "template": POD}, worker={"replicas": 3, "template": POD})
+    pod = c.construct_pod(job, "worker", 1)
+    md = pod["metadata"]
+    assert md["name"] == "pj-worker-1"
+    assert md["labels"][T.LABEL_RESOURCE_NAME] == "pj-worker-1" and md["labels"][T.LABEL_RESOURCE_TYPE] == "worker"
+    assert md["annotations"][T.ANNOTATION_RESOURCE] == "worker"
+    assert pod["spec"]["hostname"] == "pj-worker-1" and pod["spec"]["subdomain"] == "pj-worker-1"
+    env = env_of(pod)
+    assert env["POD_IP"] == {"fieldRef": {"fieldPath": "status.podIP"}}
+    assert env["PADDLE_TRAINER_ID"] == "1"
+    assert env["TRAINING_ROLE"] == env["PADDLE_TRAINING_ROLE"] == "TRAINER"
+    assert pod["spec"]["containers"][0]["envFrom"] == [{"configMapRef": {"name": "pj"}}]
+    assert pod["spec"]["restartPolicy"] == "Never"
+    assert env_of(c.construct_pod(job, "ps", 0))["TRAINING_ROLE"] == "PSERVER"
+    # name/index parsing (paddlejob_helper.go:206-213)
+    assert c.extract_name_index("pj-worker-12") == ("worker", 12)
+    assert c.res_name("pj", "ps", 3) == "pj-ps-3"
+
+
+def test_configmap_endpoint_table():
+    c = core_mod
+    job = T.paddlejob("pj", ps={"replicas": 2, "template": POD}, worker={"replicas": 2, "template": POD},
+                      with_gloo=1)
+    pods = []
+    for role, n in (("ps", 2), ("worker", 2)):
+        for i in range(n):
+            p = c.construct_pod(job, role, i)
+            p["status"] = {"podIP": f"10.0.{0 if role == 'ps' else 1}.{i + 1}"}
+            pods.append(p)
+    cm = c.construct_configmap(job, pods)
+    d = cm["data"]
+    assert d["TRAINER_PORTS_NUM"] == "20" and d["PADDLE_PORT"] == "2379"
+    assert d["PADDLE_PSERVERS_IP_PORT_LIST"] == "10.0.0.1:2379,10.0.0.2:2379"
+    assert d["PADDLE_TRAINER_ENDPOINTS"] == "10.0.1.1:2379,10.0.1.2:2379"
+    assert d["PADDLE_TRAINERS"] == "10.0.1.1,10.0.1.2" and d["PADDLE_TRAINERS_NUM"] == "2"
+    assert d["PADDLE_WITH_GLOO"] == "1" and d["PADDLE_GLOO_RENDEZVOUS"] == "3"
+    assert d["PADDLE_GLOO_HTTP_ENDPOINT"] == "10.0.0.1:2397"
+    # not all pods have an IPv4 yet → no ConfigMap (D-16)
+    pods[-1]["status"] = {}
+    assert c.construct_configmap(job, pods) is None
+
+
+def test_elastic_pod_env_and_restart_policy():
+    job = T.paddlejob("el", worker={"replicas": 4, "template": POD}, elastic=1)
+    pod = core_mod.construct_pod(job, "worker", 0, {"etcd_endpoints": ["10.1.1.1:2379"]})
+    env = env_of(pod)
+    assert env["PADDLE_ELASTIC_JOB_ID"] == "default-el" and env["PADDLE_ELASTIC_NP"] == "4"
+    assert env["PADDLE_ELASTIC_TIMEOUT"] == "60"
+    assert pod["spec"]["restartPolicy"] == "OnFailure"
+    assert "envFrom" not in pod["spec"]["containers"][0]
+
+
+def test_podgroup_min_resources():
+    # requests win over limits per container (paddlejob_helper.go:538-545)
+    res = {"limits": {T.AMD_GPU: 8, "cpu": "4"}, "requests": {"cpu": "4", "memory": "8Gi", T.AMD_GPU: 8}}
+    tmpl = {"spec": {"containers": [{"name": "c", "image": "x", "resources": res}]}}
+    job = T.paddlejob("g", worker={"replicas": 2, "template": tmpl}, ps={"replicas": 1, "template": POD},
+                      scheduling_policy={"minAvailable": 3, "queue": "q1", "priorityClass": "high"})
+    pg = core_mod.construct_podgroup(job)
+    assert pg["spec"]["minMember"] == 3 and pg["spec"]["queue"] == "q1"
+    assert pg["spec"]["priorityClassName"] == "high"
+    mr = pg["spec"]["minResources"]
+    assert mr[T.AMD_GPU] in (16, "16") and mr["cpu"] in ("8", 8) and mr["memory"] == "16Gi"
+
+
+def test_quantity_sum():
+    assert core_mod.quantity_sum(["500m", "1", "1.5"]) == "3"
+    assert core_mod.quantity_sum(["1Gi", "512Mi"]) == "1536Mi"
+
+
+def test_phase_fsm_fixed_order():
+    """D-1 fix: fixed ps→worker→heter order, Failed > Starting > Pending priority."""
+    job = T.paddlejob("p", ps={"replicas": 1, "template": POD}, worker={"replicas": 2, "template": POD})
+    job["status"] = {"ps": {"running": 1}, "worker": {"failed": 1, "pending": 1}}
+    assert core_mod.derive_phase(job) == T.Phase.Failed
+    job["status"] = {"ps": {"pending": 1}, "worker": {"running": 2}}
+    assert core_mod.derive_phase(job) == T.Phase.Pending
+    job["status"] = {"ps": {"running": 1}, "worker": {"running": 2}}
+    assert core_mod.derive_phase(job) == T.Phase.Running
+    # mixed running/succeeded keeps the previous phase (paddlejob_helper.go:120-131)
+    job["status"] = {"phase": "Running", "ps": {"running": 1}, "worker": {"succeeded": 2}}
+    assert core_mod.derive_phase(job) == T.Phase.Running
+    job["status"] = {"phase": "Running", "ps": {"succeeded": 1}, "worker": {"succeeded": 2}}
+    assert core_mod.derive_phase(job) == T.Phase.Completed
+    job["status"]["phase"] = "Failed"  # terminal phases are sticky
+    assert core_mod.derive_phase(job) == T.Phase.Failed
+    assert core_mod.derive_mode(job) == T.Mode.PS
+
+
+# ----------------------------------------------------------------------------- lifecycle
+def test_collective_hostnetwork_volcano_lifecycle():
+    cl = LocalCluster(mode="fast", agent="sim", virtual_clock=True, volcano=True, port_range=(40000, 40100),
+                      nodes=[{"name": "n0", "gpus": 8}])
+    job = T.paddlejob("coll", worker={"replicas": 2, "template": POD}, intranet="Host",
+                      scheduling_policy={"minAvailable": 2, "queue": "default"})
+    cl.create(job)
+    assert cl.wait_phase("coll", T.Phase.Running, timeout=10)
+    j = cl.job("coll")
+    assert T.FINALIZER in j["metadata"]["finalizers"]
+    port = int(j["metadata"]["annotations"][T.ANNOTATION_HOST_PORT])
+    assert 40000 <= port < 40100
+    cm = cl.get("ConfigMap", "coll")["data"]
+    assert cm["PADDLE_PORT"] == str(port)
+    p = cl.get("Pod", "coll-worker-1")
+    assert p["spec"]["hostNetwork"] is True and p["spec"]["schedulerName"] == "volcano"
+    pg = cl.get("PodGroup", "coll")
+    assert pg["spec"]["minMember"] == 2 and pg["status"]["phase"] in ("Inqueue", "Running")
+    for n in ("coll-worker-0", "coll-worker-1"):
+        cl.sim_exit(n, 0)
+    assert cl.wait_phase("coll", T.Phase.Completed, timeout=10)
+    # default clean policy cleans pods on completion; PodGroup removed on terminal phase
+    assert cl.wait(lambda: not cl.pods("coll") and cl.get("PodGroup", "coll") is None, timeout=10)
+    st = cl.job("coll")["status"]
+    assert st["completionTime"] and st["startTime"]
+    cl.delete(T.KIND, "coll")
+    assert cl.wait(lambda: cl.job("coll") is None, timeout=10)  # finalizer released the port and let go
+    assert cl._c.host_ports() == 0
+    cl.stop()
+
+
+@pytest.mark.parametrize("policy,expect_pods", [("OnFailure", 0), ("Never", 2), ("OnCompletion", 2),
+                                                ("Always", 0)])
+def test_failure_and_clean_policy(policy, expect_pods):
+    cl = LocalCluster(mode="fast", agent="sim", virtual_clock=True)
+    cl.create(T.paddlejob("f", worker={"replicas": 2, "template": POD}, clean_pod_policy=policy))
+    assert cl.wait_phase("f", T.Phase.Running, timeout=10)
+    cl.sim_exit("f-worker-1", 3)
+    assert cl.wait_phase("f", T.Phase.Failed, timeout=10)
+    cl.run_for(1.0)
+    assert len(cl.pods("f")) == expect_pods
+    st = cl.job("f")["status"]
+    assert st["phase"] == T.Phase.Failed  # sticky even after the pods are gone
+    if expect_pods:
+        assert st["worker"]["failed"] == 1
+    cl.stop()
+
+
+def test_delete_job_with_finalizer_removes_children(sim):
+    sim.create(T.paddlejob("d", ps={"replicas": 1, "template": POD}, worker={"replicas": 2, "template": POD}))
+    assert sim.wait_phase("d", T.Phase.Running, timeout=10)
+    sim.delete(T.KIND, "d")
+    assert sim.wait(lambda: sim.job("d") is None, timeout=10)
+    assert sim.wait(lambda: not sim.pods("d") and sim.get("ConfigMap", "d") is None, timeout=10)
+
+
+def test_deleted_pod_is_recreated(sim):
+    sim.create(T.paddlejob("r", worker={"replicas": 2, "template": POD}))
+    assert sim.wait_phase("r", T.Phase.Running, timeout=10)
+    uid = sim.get("Pod", "r-worker-1")["metadata"]["uid"]
+    sim.delete("Pod", "r-worker-1")
+    assert sim.wait(lambda: (sim.get("Pod", "r-worker-1") or {}).get("metadata", {}).get("uid") not in (None, uid),
+                    timeout=10)
+
+
+def test_elastic_np_sync():
+    """controllers/paddlejob_elastic.go:27-55: never creates np; updates it on scale + Event Scaled."""
+    cl = LocalCluster(mode="fast", agent="sim", virtual_clock=True, elastic_kv=True)
+    cl.create(T.paddlejob("el", worker={"replicas": 2, "template": POD}, elastic=1))
+    assert cl.wait_phase("el", T.Phase.Running, timeout=10)
+    assert cl.get("ConfigMap", "el") is None  # elastic jobs get no endpoint table
+    assert cl.kv_get("/paddle/default-el/np") is None
+    cl.scale("el", "worker", 3)
+    cl.run_for(1.0)
+    assert cl.kv_get("/paddle/default-el/np") is None
+    cl.kv_put("/paddle/default-el/np", "3")  # the launcher's agent owns creation
+    cl.scale("el", "worker", 4)
+    assert cl.wait(lambda: cl.kv_get("/paddle/default-el/np") == "4", timeout=10)
+    assert any(e["reason"] == "Scaled" for e in cl.events())
+    assert cl.wait(lambda: len(cl.pods("el")) == 4, timeout=10)
+    assert env_of(cl.get("Pod", "el-worker-3"))["PADDLE_ELASTIC_NP"] == "4"
+    cl.stop()
+
+
+def test_compat_mode_is_one_mutation_per_pass():
+    """compat reproduces the reference's one-object-per-reconcile creation (D-3)."""
+    job = T.paddlejob("c", worker={"replicas": 4, "template": POD})
+    out = {}
+    for mode in ("compat", "fast"):
+        cl = LocalCluster(mode=mode, agent="sim", virtual_clock=True, workers=1)
+        cl.create(job)
+        n_pass = 0
+        while len(cl.pods("c")) < 4 and n_pass < 50:
+            cl.reconcile("c")
+            n_pass += 1
+        out[mode] = n_pass
+        cl.stop()
+    assert out["fast"] == 1 or out["fast"] < out["compat"]
+    assert out["compat"] >= 4
+
+
+def test_gpu_gang_and_device_assignment():
+    cl = LocalCluster(mode="fast", agent="sim", virtual_clock=True, nodes=[{"name": "n0", "gpus": 8}])
+    tmpl = {"spec": {"containers": [{"name": "c", "image": "x", "resources": {"limits": {T.AMD_GPU: 2}}}]}}
+    cl.create(T.paddlejob("g", worker={"replicas": 3, "template": tmpl}))
+    assert cl.wait_phase("g", T.Phase.Running, timeout=10)
+    assert cl.free_gpus() == {"n0": 2}
+    cl.create(T.paddlejob("h", worker={"replicas": 2, "template": tmpl}))  # needs 4, only 2 free
+    cl.run_for(1.0)
+    assert cl.job("h")["status"].get("phase") in (None, T.Phase.Pending, "")
+    cl.delete(T.KIND, "g")
+    assert cl.wait_phase("h", T.Phase.Running, timeout=10)
+    cl.stop()
+
+
+# ----------------------------------------------------------------------------- REST apiserver
+def _http(method, url, body=None):
+    data = json.dumps(body).encode() if body is not None else None
+    req = urllib.request.Request(url, data=data, method=method, headers={"Content-Type": "application/json"})
+    try:
+        with urllib.request.urlopen(req, timeout=5) as r:
+            return r.status, json.loads(r.read() or b"{}")
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read() or b"{}")
+
+
+def test_rest_apiserver_crud():
+    cl = LocalCluster(mode="fast", agent="sim")
+    url = cl.serve("127.0.0.1:0")
+    cl.start()
+    try:
+        base = f"{url}/apis/{T.GROUP}/{T.VERSION}/namespaces/default/paddlejobs"
+        st, obj = _http("POST", base, T.paddlejob("rest", worker={"replicas": 2, "template": POD}))
+        assert st == 201, obj
+        st, _ = _http("POST", base, T.paddlejob("rest", worker={"replicas": 2, "template": POD}))
+        assert st == 409
+        t_end = time.time() + 10
+        while time.time() < t_end:
+            st, obj = _http("GET", f"{base}/rest")
+            if (obj.get("status") or {}).get("phase") == "Running":
+                break
+            time.sleep(0.05)
+        assert obj["status"]["phase"] == "Running"
+        st, lst = _http("GET", f"{url}/api/v1/namespaces/default/pods?labelSelector={T.LABEL_RESOURCE_TYPE}%3Dworker")
+        assert st == 200 and len(lst["items"]) == 2
+        st, _ = _http("DELETE", f"{base}/rest")
+        assert st == 200
+        t_end = time.time() + 10
+        while time.time() < t_end and _http("GET", f"{base}/rest")[0] != 404:
+            time.sleep(0.05)
+        assert _http("GET", f"{base}/rest")[0] == 404
+        with urllib.request.urlopen(f"{url}/metrics", timeout=5) as r:
+            assert b"pdo_reconcile" in r.read()
+    finally:
+        cl.stop()
+
+
+# ----------------------------------------------------------------------------- exec agent e2e
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launcher_container(args):
+    return {"name": "paddle", "image": "pdo/launcher:rocm",
+            "command": [sys.executable, "-m", "paddle_operator_amd.launch"] + args,
+            "env": [{"name": "PYTHONPATH", "value": REPO}, {"name": "OMP_NUM_THREADS", "value": "2"},
+                    {"name": "PDO_OPS", "value": "torch"}]}
+
+
+def test_exec_agent_collective_job_completes(tmp_path):
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path))
+    tmpl = {"spec": {"containers": [_launcher_container(["--workload", "resnet50", "--tiny", "--steps", "3"])]}}
+    cl.create(T.paddlejob("e2e", worker={"replicas": 2, "template": tmpl}, clean_pod_policy="Never"))
+    try:
+        ok = cl.wait_phase("e2e", T.Phase.Completed, timeout=180)
+        logs = {i: open(os.path.join(cl.sandbox(f"e2e-worker-{i}"), "paddle.log")).read()
+                for i in range(2) if cl.sandbox(f"e2e-worker-{i}")}
+        assert ok, (cl.job("e2e")["status"], logs)
+        assert len(logs) == 2
+        for i, text in logs.items():
+            ready = [json.loads(l[10:]) for l in text.splitlines() if l.startswith("PDO_READY ")]
+            assert ready and ready[0]["rank"] == i and ready[0]["world"] == 2
+    finally:
+        cl.stop()
+
+
+def test_exec_agent_elastic_scale_out(tmp_path):
+    """Config 5 shape (elastic 2 → 3) end to end: controller np sync → agents re-rendezvous."""
+    port = _free_port()
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), elastic_kv=True,
+                      kv_endpoint=f"127.0.0.1:{port}")
+    cl.serve(f"127.0.0.1:{port}")
+    args = ["--workload", "resnet50", "--tiny", "--steps", "40", "--throttle-ms", "80",
+            "--ckpt-dir", str(tmp_path / "ckpt"), "--ckpt-every", "5"]
+    cont = _launcher_container(args)
+    cont["env"].append({"name": "PDO_ELASTIC_TTL", "value": "3"})
+    cl.create(T.paddlejob("ej", worker={"replicas": 2, "template": {"spec": {"containers": [cont]}}}, elastic=1,
+                          clean_pod_policy="Never"))
+    try:
+        assert cl.wait(lambda: cl.kv_get("/pdo/default-ej/ready/1") is not None, timeout=120)
+        cl.scale("ej", "worker", 3)
+        ok = cl.wait_phase("ej", T.Phase.Completed, timeout=180)
+        logs = [open(os.path.join(cl.sandbox(f"ej-worker-{i}"), "paddle.log")).read() for i in range(3)
+                if cl.sandbox(f"ej-worker-{i}")]
+        assert ok, (cl.job("ej")["status"], [l[-2000:] for l in logs])
+        assert cl.kv_get("/paddle/default-ej/np") == "3"
+        worlds = {json.loads(l[10:])["world"] for t in logs for l in t.splitlines() if l.startswith("PDO_READY ")}
+        assert worlds == {2, 3}
+    finally:
+        cl.stop()

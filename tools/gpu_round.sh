@@ -20,3 +20,7 @@ if [ -n "$TUNE" ]; then
   timeout -k 10 300 python bench.py --micro-batch $TUNE --steps 10 --warmup 3 >> gpurun_out/bench_tune.jsonl 2>> gpurun_out/bench_tune.err || exit 1
   cat gpurun_out/bench_tune.jsonl
 fi
+if [ -n "$RESNET" ]; then
+  timeout -k 10 400 python -m paddle_operator_amd.launch --workload resnet50 --batch $RESNET --steps 30 --log-every 10 > gpurun_out/resnet50.log 2>&1 || { tail -30 gpurun_out/resnet50.log; exit 1; }
+  grep -E "PDO_READY|PDO_DONE|step" gpurun_out/resnet50.log
+fi
