@@ -57,9 +57,69 @@ Agent::Agent(store::Store* s, AgentOptions o, api::Clock clock, ObjectApi* write
     : s_(s), writer_(writer), opt_(std::move(o)), clock_(std::move(clock)) {
   for (int i = 0; i < opt_.node.gpus; ++i) free_gpus_.insert(i);
   mkdirs(opt_.sandbox_root);
+  if (opt_.mode == AgentOptions::Exec && !opt_.zygote_cmd.empty()) start_zygote();
 }
 
-Agent::~Agent() { shutdown(); }
+Agent::~Agent() {
+  shutdown();
+  stop_zygote();
+}
+
+void Agent::start_zygote() {
+  zygote_sock_ = opt_.sandbox_root + "/zygote.sock";
+  ::unlink(zygote_sock_.c_str());
+  std::vector<std::string> argv = opt_.zygote_cmd;
+  argv.push_back("--socket");
+  argv.push_back(zygote_sock_);
+  std::vector<char*> av;
+  for (auto& a : argv) av.push_back(const_cast<char*>(a.c_str()));
+  av.push_back(nullptr);
+  const std::string logp = opt_.sandbox_root + "/zygote.log";
+  pid_t pid = fork();
+  if (pid == 0) {
+    setpgid(0, 0);
+    int fd = open(logp.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+    if (fd >= 0) {
+      dup2(fd, 1);
+      dup2(fd, 2);
+      close(fd);
+    }
+    execvp(av[0], av.data());
+    _exit(127);
+  }
+  if (pid > 0) {
+    setpgid(pid, pid);
+    zygote_pid_ = pid;
+  } else {
+    zygote_sock_.clear();
+  }
+}
+
+void Agent::stop_zygote() {
+  if (zygote_pid_ <= 0) return;
+  ::kill(zygote_pid_, SIGTERM);
+  for (int i = 0; i < 200; ++i) {
+    int st;
+    if (waitpid(zygote_pid_, &st, WNOHANG) == zygote_pid_) {
+      zygote_pid_ = -1;
+      break;
+    }
+    usleep(10000);
+  }
+  if (zygote_pid_ > 0) {
+    ::kill(-zygote_pid_, SIGKILL);
+    int st;
+    waitpid(zygote_pid_, &st, 0);
+    zygote_pid_ = -1;
+  }
+  ::unlink(zygote_sock_.c_str());
+}
+
+bool Agent::zygote_ready() const {
+  if (zygote_sock_.empty()) return false;
+  struct stat sb;
+  return ::stat(zygote_sock_.c_str(), &sb) == 0;
+}
 
 size_t Agent::pods() const {
   std::lock_guard<std::mutex> g(mu_);
@@ -162,13 +222,35 @@ bool Agent::build_env(const Rt& rt, const Value& pod, const Value& c, std::vecto
   }
   // device + sandbox env (the device plugin's job on a real node)
   if (!rt.gpus.empty()) {
+    // indices are into the agent's own visible set: if the agent itself was
+    // restricted (HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES), map through it;
+    // ROCR_VISIBLE_DEVICES is inherited untouched (applied below HIP's list)
+    std::vector<std::string> parent;
+    const char* pv = getenv("HIP_VISIBLE_DEVICES");
+    if (!pv || !*pv) pv = getenv("CUDA_VISIBLE_DEVICES");
+    if (pv && *pv) {
+      std::string cur;
+      for (const char* q = pv;; ++q) {
+        if (*q == ',' || *q == 0) {
+          if (!cur.empty()) parent.push_back(cur);
+          cur.clear();
+          if (!*q) break;
+        } else {
+          cur += *q;
+        }
+      }
+    }
     std::string ids;
-    for (size_t i = 0; i < rt.gpus.size(); ++i) ids += (i ? "," : "") + std::to_string(rt.gpus[i]);
+    for (size_t i = 0; i < rt.gpus.size(); ++i) {
+      const int g = rt.gpus[i];
+      ids += (i ? "," : "") + (g < (int)parent.size() ? parent[g] : std::to_string(g));
+    }
     set("HIP_VISIBLE_DEVICES", ids);
   }
   set("PDO_POD_IP", rt.ip);
   set("PDO_NODE_NAME", opt_.node.name);
   set("PDO_SANDBOX", rt.sandbox);
+  if (!zygote_sock_.empty() && !m.count("PDO_ZYGOTE")) set("PDO_ZYGOTE", zygote_sock_);
   // inherited agent environment first, pod env overrides
   std::map<std::string, std::string> full;
   for (char** e = environ; e && *e; ++e) {
@@ -176,7 +258,7 @@ bool Agent::build_env(const Rt& rt, const Value& pod, const Value& c, std::vecto
     size_t eq = kv.find('=');
     if (eq == std::string::npos) continue;
     std::string k = kv.substr(0, eq);
-    if (k == "HIP_VISIBLE_DEVICES" || k == "ROCR_VISIBLE_DEVICES" || k == "CUDA_VISIBLE_DEVICES") continue;
+    if (k == "HIP_VISIBLE_DEVICES" || k == "CUDA_VISIBLE_DEVICES") continue;
     full[k] = kv.substr(eq + 1);
   }
   for (auto& k : order) full[k] = m[k];

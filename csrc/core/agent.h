@@ -42,6 +42,9 @@ struct AgentOptions {
   double sim_ip_delay = 0.0;
   double sim_start_delay = 0.0;
   double sim_run_s = -1;  // <0: run until told otherwise
+  // warm launcher: argv of a per-node zygote (launch/zygote.py) started with
+  // the agent; its socket is exported to pods as PDO_ZYGOTE (Exec mode)
+  std::vector<std::string> zygote_cmd;
 };
 
 class Agent {
@@ -66,6 +69,9 @@ class Agent {
   size_t pods() const;
   const AgentOptions& options() const { return opt_; }
   std::string sandbox_of(const std::string& ns, const std::string& pod) const;
+  // zygote socket path ("" if none) and whether it is accepting
+  const std::string& zygote_socket() const { return zygote_sock_; }
+  bool zygote_ready() const;
 
  private:
   struct Proc {
@@ -109,6 +115,10 @@ class Agent {
   std::map<std::string, Rt> rts_;  // ns/name
   std::set<int> free_gpus_;
   int ip_seq_ = 0;
+  pid_t zygote_pid_ = -1;
+  std::string zygote_sock_;
+  void start_zygote();
+  void stop_zygote();
 };
 
 }  // namespace pdo

@@ -42,6 +42,7 @@ Cluster::Cluster(ClusterOptions opt) : opt_(std::move(opt)) {
     ao.sim_ip_delay = opt_.sim_ip_delay;
     ao.sim_start_delay = opt_.sim_start_delay;
     ao.sim_run_s = opt_.sim_run_s;
+    ao.zygote_cmd = opt_.zygote_cmd;
     ao.config_retry_s = opt_.kubelet_config_retry_s >= 0 ? opt_.kubelet_config_retry_s : (compat ? 1.0 : 0.0);
     agents_.emplace_back(new Agent(store_.get(), ao, clock_));
   }
@@ -65,6 +66,12 @@ Cluster::~Cluster() {
 }
 
 double Cluster::now() const { return clock_(); }
+
+bool Cluster::zygotes_ready() const {
+  for (auto& a : agents_)
+    if (!a->zygote_socket().empty() && !a->zygote_ready()) return false;
+  return true;
+}
 
 void Cluster::advance(double dt) {
   if (!opt_.virtual_clock) return;

@@ -37,6 +37,7 @@ struct ClusterOptions {
   int port_start = 35000, port_end = 65000;
   std::string namespace_;
   std::string kv_endpoint = "127.0.0.1:2379";  // advertised to elastic pods (PADDLE_ELASTIC_SERVER)
+  std::vector<std::string> zygote_cmd;          // per-node warm launcher (exec agents)
 };
 
 class Cluster {
@@ -54,6 +55,7 @@ class Cluster {
   // tick for `s` seconds (virtual or real) regardless of quiescence
   int run_for(double s, double step = 0.01);
   void start();  // background loop (real clock)
+  bool zygotes_ready() const;
   void stop();
 
   store::Store& store() { return *store_; }

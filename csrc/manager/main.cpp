@@ -75,6 +75,14 @@ static int detect_gpus() {
       }
   }
   closedir(d);
+  // a restricted manager (container / scheduler slice) only owns what it sees
+  for (const char* var : {"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"}) {
+    const char* v = getenv(var);
+    if (!v || !*v) continue;
+    int cnt = 1;
+    for (const char* q = v; *q; ++q) cnt += *q == ',';
+    n = std::min(n, cnt);
+  }
   return n;
 }
 

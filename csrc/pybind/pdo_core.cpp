@@ -123,6 +123,7 @@ static pdo::ClusterOptions cluster_opts(const py::kwargs& kw) {
       o.port_end = pr.second;
     } else if (k == "namespace") o.namespace_ = v.cast<std::string>();
     else if (k == "kv_endpoint") o.kv_endpoint = v.cast<std::string>();
+    else if (k == "zygote_cmd") o.zygote_cmd = v.cast<std::vector<std::string>>();
     else if (k == "nodes") {
       for (auto n : v.cast<py::list>()) {
         auto d = n.cast<py::dict>();
@@ -442,6 +443,7 @@ PYBIND11_MODULE(_pdo_core, m) {
         return port;
       }, py::arg("addr") = "127.0.0.1:0")
       .def("start", [](PyCluster& c) { c.c->start(); })
+      .def("zygotes_ready", [](PyCluster& c) { return c.c->zygotes_ready(); })
       .def("stop", [](PyCluster& c) {
         py::gil_scoped_release g;
         c.c->stop();

@@ -31,6 +31,16 @@ class LocalCluster:
     """
 
     def __init__(self, **opts):
+        if opts.pop("zygote", False):
+            # per-node warm launcher: pods whose entry point is bin/pdo-launch fork
+            # from a pre-imported interpreter (launch/zygote.py)
+            import os
+            import sys
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            pp = os.environ.get("PYTHONPATH", "")
+            if root not in pp.split(os.pathsep):
+                os.environ["PYTHONPATH"] = root + (os.pathsep + pp if pp else "")
+            opts["zygote_cmd"] = [sys.executable, "-m", "paddle_operator_amd.launch.zygote"]
         self._c = core().Cluster(**opts)
         self.opts = opts
         self.url: Optional[str] = None
@@ -151,6 +161,9 @@ class LocalCluster:
 
     def start(self):
         self._c.start()
+
+    def zygotes_ready(self) -> bool:
+        return self._c.zygotes_ready()
 
     def stop(self):
         self._c.stop()

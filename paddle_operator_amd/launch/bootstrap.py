@@ -47,6 +47,17 @@ class Bootstrapped:
     ipc_gbps: Optional[dict] = None
 
 
+def _wait_port(host: str, port: int, timeout_s: float, poll: float = 0.002) -> bool:
+    deadline = time.time() + timeout_s
+    while time.time() < deadline:
+        try:
+            with socket.create_connection((host, port), timeout=0.5):
+                return True
+        except OSError:
+            time.sleep(poll)
+    return False
+
+
 def _env_int(k, d):
     return int(os.environ.get(k, str(d)))
 
@@ -73,7 +84,12 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
         if store is not None:
             kw["store"] = store
         else:
-            kw["init_method"] = f"tcp://{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"
+            host, port = os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"])
+            if rank != 0:
+                # c10d's client connect retries back off to ~1 s; ranks forked
+                # in the same ms as rank 0 would otherwise sleep through its bind
+                _wait_port(host, port, timeout_s)
+            kw["init_method"] = f"tcp://{host}:{port}"
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         if ipc_probe and gpu:

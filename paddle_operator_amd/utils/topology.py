@@ -144,7 +144,13 @@ def _from_sysfs() -> Optional[Topology]:
         nodes.append((d, props))
     if not nodes:
         return None
-    gpus = [GPU(i, "", int(p.get("numa_node", "-1")) if "numa_node" in p else -1) for i, (_, p) in enumerate(nodes)]
+    gpus = []
+    for i, (_, p) in enumerate(nodes):
+        loc = int(p.get("location_id", "0"))
+        bdf = "%04x:%02x:%02x.%x" % (int(p.get("domain", "0")), (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 0x7) \
+            if loc else ""
+        cpus = numa_cpus(bdf) if bdf else []
+        gpus.append(GPU(i, bdf, int(p.get("numa_node", "-1")) if "numa_node" in p else -1, cpus))
     N = len(gpus)
     ids = {int(os.path.basename(d)): i for i, (d, _) in enumerate(nodes)}
     lt = [["self" if a == b else "undefined" for b in range(N)] for a in range(N)]
@@ -176,7 +182,10 @@ def gpu_topology() -> Topology:
 
 def pin_to_gpu(local_rank: int, topo: Optional[Topology] = None) -> List[int]:
     """Restrict this process to the NUMA-local CPUs of its GPU (no-op if unknown)."""
-    topo = topo or gpu_topology()
+    # KFD sysfs is a handful of small reads; rocm_smi init costs ~0.2 s per rank
+    topo = topo or _from_sysfs()
+    if topo is None:
+        return []
     visible = os.environ.get("HIP_VISIBLE_DEVICES")
     phys = local_rank
     if visible:

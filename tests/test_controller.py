@@ -382,3 +382,37 @@ def test_exec_agent_elastic_scale_out(tmp_path):
         assert worlds == {2, 3}
     finally:
         cl.stop()
+
+
+def test_zygote_warm_launch_and_kill(tmp_path):
+    """bin/pdo-launch forks ranks from the per-node zygote; a pod kill reaches the rank."""
+    pdo_launch = os.path.join(REPO, "bin", "pdo-launch")
+    if not os.path.exists(pdo_launch):
+        pytest.skip("bin/pdo-launch not built")
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), zygote=True)
+    t_end = time.time() + 120
+    while not cl.zygotes_ready() and time.time() < t_end:
+        time.sleep(0.05)
+    assert cl.zygotes_ready()
+    cont = _launcher_container(["--workload", "noop", "--exit-after-ready"])
+    cont["command"] = [pdo_launch] + cont["command"][3:]
+    cl.create(T.paddlejob("z", worker={"replicas": 2, "template": {"spec": {"containers": [cont]}}},
+                          clean_pod_policy="Never"))
+    try:
+        assert cl.wait_phase("z", T.Phase.Completed, timeout=60), cl.job("z")["status"]
+        text = open(os.path.join(cl.sandbox("z-worker-1"), "paddle.log")).read()
+        ready = [json.loads(l[10:]) for l in text.splitlines() if l.startswith("PDO_READY ")]
+        assert ready and ready[0]["world"] == 2
+        # ready well under a cold interpreter's import-torch time
+        assert ready[0]["t_ready"] - ready[0]["t_start"] < 1.0, ready
+        # a long-running rank: SIGTERM on the pod is relayed through the client
+        cont2 = _launcher_container(["--workload", "resnet50", "--tiny", "--steps", "100000"])
+        cont2["command"] = [pdo_launch] + cont2["command"][3:]
+        cl.create(T.paddlejob("zk", worker={"replicas": 1, "template": {"spec": {"containers": [cont2]}}},
+                              clean_pod_policy="Never"))
+        assert cl.wait_phase("zk", T.Phase.Running, timeout=60)
+        time.sleep(1.0)
+        assert cl.kill("zk-worker-0", 15)
+        assert cl.wait_phase("zk", T.Phase.Failed, timeout=30), cl.job("zk")["status"]
+    finally:
+        cl.stop()
