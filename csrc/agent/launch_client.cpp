@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pdo-launch: container entry point of a PaddleJob rank.
 //
 // Warm path: PDO_ZYGOTE names the per-node zygote's unix socket

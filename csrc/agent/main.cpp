@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pdo-agent: standalone kubelet-lite joining a pdo-manager (local backend)
 // from another host / container:
 //   pdo-agent --server http://manager:8082 --node gpu-node-1 --gpus 8

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pdo-agent: "kubelet-lite" for the local backend.
 //
 // Runs the pods bound to one node.  Exec mode starts real processes (one

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // PaddleJob API (batch.paddlepaddle.org/v1) for the pdo control plane.
 //
 // Schema parity with the reference CRD (api/v1/paddlejob_types.go:25-281):

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Kubernetes-compatible REST front end over store::Store (local backend).
 //
 // Same paths, verbs and list/watch wire format as kube-apiserver for the

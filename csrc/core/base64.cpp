@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // base64 (RFC 4648) for the etcd-v3 JSON gateway wire format (keys/values
 // are base64-encoded bytes there).
 #include "base64.h"

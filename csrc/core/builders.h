@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Pure object builders: PaddleJob → Pod / ConfigMap / Service / PodGroup.
 //
 // Behavioural parity with controllers/paddlejob_helper.go (constructPod

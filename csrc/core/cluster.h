@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Local single-node (or simulated multi-node) cluster backend.
 //
 // Wires the object store (API server), pdo-kv, the gang scheduler, one

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // PaddleJob controller: watches → workqueue → planner → executor.
 //
 // Counterpart of the reference's PaddleJobReconciler + SetupWithManager

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Host-network port-block allocator (Intranet=Host).
 //
 // Reference: controllers/paddlejob_controller.go:407-458 (HostPortMap,

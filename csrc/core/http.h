@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Minimal HTTP/1.1 server and client (no external dependencies).
 //
 // Server: one acceptor thread + one thread per connection (the manager, the

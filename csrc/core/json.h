@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Minimal, dependency-free JSON DOM for the pdo control plane.
 //
 // Kubernetes objects travel as JSON; the control plane mutates only a few

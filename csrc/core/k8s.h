@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Kubernetes REST backend: the same controller against a real apiserver.
 //
 // * Config: --master URL, --kubeconfig (YAML or JSON; token / client cert /

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // etcd-v3 JSON-gateway front end for KVStore + a matching client.
 //
 // Routes (POST, JSON bodies, base64 keys/values, int64 as strings — the

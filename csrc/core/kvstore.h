@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pdo-kv: an etcd-v3-subset key/value store (MVCC revisions, range/prefix
 // reads, transactions with compare-and-swap, leases with TTL, watches with
 // history replay).

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 #include "log.h"
 
 #include <sys/time.h>

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Structured logging (zap-compatible flags: --zap-devel, --zap-log-level,
 // --zap-encoder=json|console; reference main.go:79-85).
 #pragma once

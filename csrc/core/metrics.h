@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Prometheus text-exposition registry (counters, gauges, histograms).
 //
 // The reference exposes controller-runtime's default registry on

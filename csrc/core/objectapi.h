@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Write side of the API used by the controller and the agent: the local
 // store (StoreApi) or a remote apiserver (k8s::RestApi).
 #pragma once

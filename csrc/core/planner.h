@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Reconcile planner: observed state → ordered action list (+ requeue hint).
 //
 // The reference Reconcile (controllers/paddlejob_controller.go:101-333)

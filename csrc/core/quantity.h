@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Kubernetes resource.Quantity arithmetic (subset) for PodGroup minResources.
 // Parses "2", "500m", "1.5", "4Gi", "10k", "1e3"; sums keep the first
 // operand's format; String() follows the canonical forms of apimachinery

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Scheduler stand-in for the local backend: default FIFO bin-packing on
 // amd.com/gpu + Volcano-style gang admission for PodGroups.
 //

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Status aggregation + phase/mode state machine of a PaddleJob.
 //
 // Reference semantics: controllers/paddlejob_controller.go:335-381

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // In-memory Kubernetes-style object store: the API server of the `local`
 // cluster backend (envtest's kube-apiserver + etcd, plus what envtest lacks).
 //

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Deduplicating, rate-limited work queue with delayed requeue.
 //
 // Semantics of client-go's workqueue as controller-runtime uses it for the

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Minimal YAML → JSON DOM reader for kubeconfig files and Kubernetes
 // manifests (block mappings/sequences, plain/quoted scalars, literal `|` and
 // folded `>` blocks, simple flow collections, comments, `---` documents).

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Causal flash attention forward / backward for head_dim 64 on gfx950.
 //
 // Layout: the QKV GEMM output is consumed in place, qkv = [B, S, 3, H, 64]

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pybind11 / PyTorch binding of the paddle_operator_amd HIP kernels.
 // Compiled by hipcc for gfx950 (tools/build.py) — no hipify, no CUDA names.
 // Every entry point checks device, dtype, contiguity and shape before launch:

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Multi-tensor bucket kernels for the RCCL data-parallel path (gfx950).
 // The flat-arena DDP needs no copies for its own gradients; these kernels
 // serve everything else that must travel through a bucket (parameter

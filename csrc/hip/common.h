@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Shared helpers for the CDNA4 (gfx950) kernels of paddle_operator_amd.
 //
 // Conventions: wave = 64 lanes; bf16 is clang's native __bf16 (casts lower to

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Token + position embedding (gfx950).
 // Forward: one wave per token row, y = wte[idx] + wpe[pos] with 16-B vectors.
 // Backward: d(wte) by f32 atomics shaped as 256 contiguous bytes per wave

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // bias + GELU(tanh) forward and backward for the GPT-2 MLP (gfx950).
 // The GEMM producing x runs without bias (plain hipBLASLt); the bias add, the
 // activation and — in backward — the bias gradient column reduction are fused

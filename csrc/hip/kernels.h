@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Host-side launch API of the paddle_operator_amd HIP kernels (gfx950).
 // Raw pointers + hipStream_t only: no torch headers here, so each kernel TU
 // compiles in seconds; `bind.cpp` adapts torch tensors to these calls.

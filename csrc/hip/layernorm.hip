@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // LayerNorm forward/backward (optionally fused with the residual add) for
 // gfx950.  One wave per row: a row of C bf16 is held in registers as VPL
 // vectors of 8 (16-B loads), statistics are two-pass in registers (exact

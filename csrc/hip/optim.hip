@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Fused AdamW over the flat parameter arena + gradient global-norm (gfx950).
 // One pass: bf16 grad → ×(grad_scale · clip_coef) → fp32 moments/master →
 // bf16 compute copy.  The clip coefficient is read from device memory

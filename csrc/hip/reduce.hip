@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Column reductions (bias / norm-weight gradients) for gfx950.
 //
 // out[c] = Σ_r in[r][c] as a deterministic two-level tree: level 1 gives each

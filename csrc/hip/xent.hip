@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Softmax cross-entropy over a padded vocabulary (gfx950).
 // Forward: one 256-thread block per row, single pass with an online
 // (max, sum-exp) pair per thread over 16-B vectors, block combine → lse and the

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pdo-kv: standalone etcd-v3-subset server (JSON gateway API).
 // Replaces deploy/elastic/etcd.yaml's bitnami/etcd for elastic PaddleJobs and
 // the launcher rendezvous.  Usage:

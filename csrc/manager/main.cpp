@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // pdo-manager: the PaddleJob operator process (reference: main.go).
 //
 // Flag parity with the reference (main.go:61-83):

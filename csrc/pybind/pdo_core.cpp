@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Python binding of the native control plane (paddle_operator_amd._pdo_core).
 // Objects cross the boundary as plain Python dict/list/str/int/float/bool.
 #include <pybind11/functional.h>

@@ -1,3 +1,4 @@
+// SPDX-License-Identifier: Apache-2.0
 // Native unit tests of the control plane (no framework dependency).
 // Built in the normal build and in sanitizer builds:
 //   cmake -DPDO_SANITIZE=address,undefined …   /  -DPDO_SANITIZE=thread …
