@@ -1,6 +1,8 @@
 // SPDX-License-Identifier: Apache-2.0
 #include "apiserver.h"
 
+#include <fstream>
+
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -133,7 +135,7 @@ static bool parse_path(const std::string& path, const KindInfo** kind, std::stri
 }
 
 void mount_apiserver(http::Server& srv, store::Store& st, WatchHub& hub, Cluster* cluster) {
-  auto handler = [&st, &hub](const http::Request& q) -> http::Response {
+  auto handler = [&st, &hub, cluster](const http::Request& q) -> http::Response {
     const KindInfo* k = nullptr;
     std::string ns, name, sub;
     if (!parse_path(q.path, &k, &ns, &name, &sub)) return status_resp(404, "NotFound", "unknown path " + q.path);
@@ -204,6 +206,25 @@ void mount_apiserver(http::Server& srv, store::Store& st, WatchHub& hub, Cluster
         list["items"] = items;
         http::Response r;
         r.body = list.dump();
+        return r;
+      }
+      if (q.method == "GET" && sub == "log" && k->kind == "Pod") {
+        // kubectl logs: local backend reads the container log from the agent's sandbox
+        st.get(k->kind, ns, name);  // 404 if the pod does not exist
+        Agent* a = cluster ? cluster->agent_for(ns, name) : nullptr;
+        std::string dir = a ? a->sandbox_of(ns, name) : "";
+        if (dir.empty()) return status_resp(404, "NotFound", "no log for pod " + name);
+        std::string c = q.param("container");
+        if (c.empty()) c = st.get(k->kind, ns, name).at_path("spec.containers").arr().front().get("name").str();
+        std::ifstream f(dir + "/" + c + ".log", std::ios::binary);
+        std::stringstream buf;
+        buf << f.rdbuf();
+        std::string body = buf.str();
+        const std::string tb = q.param("limitBytes");
+        if (!tb.empty() && (size_t)atoll(tb.c_str()) < body.size()) body = body.substr(body.size() - atoll(tb.c_str()));
+        http::Response r;
+        r.content_type = "text/plain";
+        r.body = body;
         return r;
       }
       if (q.method == "GET") {
