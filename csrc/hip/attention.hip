@@ -170,19 +170,26 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         tmax = fmaxf(tmax, fmaxf(a, bb));
       }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mn);
-      m = mn;
+      // deferred rescale: keep a stale running max unless it grows by more
+      // than 2^8 (P ≤ 256 stays exact enough in bf16, fp32 accumulation), so
+      // after the first tiles the O/l rescale is skipped wave-uniformly
+      const bool grow = tmax > m + 8.f;
+      if (__any(grow)) {
+        const float mn = grow ? fmaxf(m, tmax) : m;
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+      }
       float ls = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s0[r] = exp2f(s0[r] - mn);
-        s1[r] = exp2f(s1[r] - mn);
+        s0[r] = __builtin_amdgcn_exp2f(s0[r] - m);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r] - m);
         ls += s0[r] + s1[r];
       }
-      l = l * alpha + ls;
-      o0 *= alpha;
-      o1 *= alpha;
+      l += ls;
 #pragma unroll
       for (int sst = 0; sst < 2; ++sst) {
         const bf16x8 p0 = pack8(s0, sst), p1 = pack8(s1, sst);
@@ -321,7 +328,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g + e;
-            float p = exp2f(sacc[r] * c2 - l4[e]);
+            float p = __builtin_amdgcn_exp2f(sacc[r] * c2 - l4[e]);
             if (diag && (q0 + qr + e) < key) p = 0.f;
             sacc[r] = p;
             dpacc[r] = p * (dpacc[r] - d4[e]);
@@ -411,7 +418,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          float p = exp2f(s[r] * c2 - lq);
+          float p = __builtin_amdgcn_exp2f(s[r] * c2 - lq);
           if (diag && kr > q) p = 0.f;
           s[r] = p * (dp[r] - dq_delta);  // dS^T
         }

@@ -201,6 +201,14 @@ void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor master, at::Tensor m1, at
                            cur_stream()), "adamw_flat");
 }
 
+// out (+)= sum over the leading dim of part [s, ...] (split-K weight gradients)
+void splitk_add(at::Tensor part, at::Tensor out, bool accumulate) {
+  CHECK_IN(part); CHECK_BF16(part); CHECK_BF16(out);
+  TORCH_CHECK(out.is_contiguous() && part.size(0) >= 1 && part[0].numel() == out.numel());
+  CHECK_RC(pdo::splitk_add(bp(part), (int)part.size(0), out.numel(), bp(out), accumulate ? 1 : 0, cur_stream()),
+           "splitk_add");
+}
+
 // ---------------------------------------------------------------- attention
 std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t n_head) {
   CHECK_IN(qkv); CHECK_BF16(qkv);
@@ -347,6 +355,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("sumsq", &sumsq);
   m.def("adamw_flat", &adamw_flat);
+  m.def("splitk_add", &splitk_add);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("scale_", &scale_);

@@ -23,6 +23,7 @@ int colsum_scratch_floats(int G, int C);
 void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st);
 int bias_grad_scratch_floats(long long N, int F);
 int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st);
+int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 
 // gelu.hip
 int bias_gelu_fwd(const bf16* x, const bf16* b, bf16* y, long long N, int F, hipStream_t st);

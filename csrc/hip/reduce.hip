@@ -95,4 +95,37 @@ int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipS
   return 0;
 }
 
+
+
+// ----------------------------------------------------------------------------
+// split-K combine for long-K weight-gradient GEMMs:
+//   out[i] (+)= sum_s part[s][i]   (bf16 partials, fp32 sum, bf16 out)
+// dW = dY^T X has K = tokens (16-64k) but only M·N/256² = 16-64 output tiles,
+// too few to fill 256 CUs; the GEMM runs as a batched [s] GEMM over token
+// slices and this pass folds the slices straight into the gradient arena.
+// ----------------------------------------------------------------------------
+template <int S_MAX>
+__global__ __launch_bounds__(256) void splitk_add_kernel(const bf16* __restrict__ part, int s, long long n,
+                                                         bf16* __restrict__ out, int accumulate) {
+  const long long i8 = (blockIdx.x * 256LL + threadIdx.x);
+  if (i8 * 8 >= n) return;
+  f32x8 acc = accumulate ? to_f32(reinterpret_cast<const bf16x8*>(out)[i8]) : f32x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16x8* p = reinterpret_cast<const bf16x8*>(part) + i8;
+  const long long stride = n / 8;
+#pragma unroll
+  for (int k = 0; k < S_MAX; ++k)
+    if (k < s) acc += to_f32(p[k * stride]);
+  reinterpret_cast<bf16x8*>(out)[i8] = to_bf16(acc);
+}
+
+int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st) {
+  if (n % 8 != 0 || s < 1 || s > 16) return -2;
+  const unsigned grid = (unsigned)((n / 8 + 255) / 256);
+  if (s <= 8)
+    splitk_add_kernel<8><<<grid, 256, 0, st>>>(part, s, n, out, accumulate);
+  else
+    splitk_add_kernel<16><<<grid, 256, 0, st>>>(part, s, n, out, accumulate);
+  return 0;
+}
+
 }  // namespace pdo

@@ -13,6 +13,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -168,7 +170,16 @@ class _LinearFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             if _direct_ok(w):
-                w.grad.view(Fo, K).addmm_(dy2.t(), x2)
+                g = w.grad.view(Fo, K)
+                s = _splitk(dy2.shape[0], Fo, K)
+                if s > 1:
+                    # long-K / few-tile dW: batched GEMM over token slices + fused fold into the arena
+                    T = dy2.shape[0] // s
+                    part = torch.bmm(dy2.view(s, T, Fo).transpose(1, 2), x2.view(s, T, K),
+                                     out=_workspace(dy2.device, s * Fo * K).view(s, Fo, K))
+                    _native.require_hip().splitk_add(part, g, True)
+                else:
+                    g.addmm_(dy2.t(), x2)
                 w._pdo_ready(w)
             else:
                 dw = dy2.t() @ x2
@@ -176,6 +187,29 @@ class _LinearFn(torch.autograd.Function):
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _native.require_hip().bias_grad(dy2.contiguous()) if use_hip(dy2) else dy2.float().sum(0).to(dy.dtype)
         return dx, dw, db
+
+
+_WS = {}
+
+
+def _workspace(device, numel):
+    """Grow-only bf16 scratch per device (split-K partials)."""
+    buf = _WS.get(device)
+    if buf is None or buf.numel() < numel:
+        buf = torch.empty(numel, dtype=torch.bfloat16, device=device)
+        _WS[device] = buf
+    return buf[:numel]
+
+
+def _splitk(tokens: int, m: int, n: int) -> int:
+    """Token-slice count for dW = dY^T X: aim for ≥256 output tiles of 256² (one per CU)."""
+    if tokens < 8192 or os.environ.get("PDO_SPLITK", "1") == "0":
+        return 1
+    tiles = max(1, (m * n) // 65536)
+    s = 1
+    while s < 8 and tiles * s < 256 and tokens % (2 * s) == 0 and tokens // (2 * s) >= 2048:
+        s *= 2
+    return s
 
 
 def _direct_ok(p) -> bool:

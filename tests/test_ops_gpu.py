@@ -128,6 +128,33 @@ def test_linear_direct_arena_grad(cuda):
     assert m.w.grad.data_ptr() == fp_.grads[fp_.slots[[s.name for s in fp_.slots].index("w")].offset:].data_ptr()
 
 
+@pytest.mark.parametrize("T,Fo,K", [(16384, 1024, 1024), (8192, 3072, 512)])
+def test_linear_splitk_weight_grad(cuda, T, Fo, K):
+    """Long-K dW takes the batched split-K path + HIP fold into the arena (accumulating)."""
+    from paddle_operator_amd.parallel.flat import FlatParams
+    from paddle_operator_amd import ops
+
+    assert ops._splitk(T, Fo, K) > 1
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.randn(Fo, K) * 0.02)
+
+        def forward(self, x):
+            return ops.linear(x, self.w)
+
+    m = M().to(cuda).bfloat16()
+    FlatParams(m, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(11)
+    x = torch.randn(T, K, device=cuda, generator=g).bfloat16()
+    dy = torch.randn(T, Fo, device=cuda, generator=g).bfloat16()
+    for _ in range(2):
+        m(x).backward(dy)
+    ref = 2 * (dy.float().t() @ x.float())
+    assert rel_err(m.w.grad, ref) < 2e-2
+
+
 @pytest.mark.parametrize("N,F", [(1024, 4096), (77, 3072)])
 def test_bias_gelu(cuda, N, F):
     ops = _ops()

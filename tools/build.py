@@ -70,7 +70,10 @@ def build_hip(jobs=8, verbose=False):
     headers = glob.glob(os.path.join(src_dir, "*.h"))
     kernels = sorted(glob.glob(os.path.join(src_dir, "*.hip")))
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
-              "-Wno-unused-result", "-munsafe-fp-atomics"]
+              "-Wno-unused-result", "-munsafe-fp-atomics",
+              # MFMA accumulators in arch VGPRs: no v_accvgpr copies around the
+              # VALU work on accumulators (softmax / rescale / epilogues)
+              "-mllvm", "-amdgpu-mfma-vgpr-form"]
     jobs_list = []
     for s in kernels:
         o = os.path.join(obj_dir, os.path.basename(s) + ".o")
