@@ -28,6 +28,7 @@
 namespace pdo {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int HD = 64;     // head dim
@@ -73,6 +74,18 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
   for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
   return r;
 }
+
+// Retire loop-invariant operand loads BEFORE the tile loop.  Otherwise
+// hipcc's waitcnt pass treats them as possibly pending at the loop's first
+// MFMA; vmcnt is in-order, so every iteration then waits for its own K/V
+// prefetch (issued just before) — the global-load latency lands on the
+// critical path of every tile.  An empty asm use forces the wait here.
+template <int N>
+__device__ __forceinline__ void retire(const bf16x8 (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(v[i]));
+}
+__device__ __forceinline__ void retire(float x) { asm volatile("" ::"v"(x)); }
 
 // ----- global → register → LDS staging of a [64 rows][64] tile (256 threads) -----
 struct Stage {
@@ -126,6 +139,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
   bf16x8 qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
+  retire(qf);
 
   f32x16 o0 = zero16(), o1 = zero16();
   float m = -INFINITY, l = 0.f;
@@ -156,20 +170,21 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
       }
       const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
+      // VALU diet (D=64 forward is VALU-bound, not MFMA-bound): mask and max
+      // on the raw scores (c2 > 0 commutes with max), then ONE fma + v_exp
+      // per element and packed row-sum adds
+      if (diag) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key0 + kr > q) s0[r] = -INFINITY;
+          if (key0 + 32 + kr > q) s1[r] = -INFINITY;
+        }
+      }
       float tmax = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hh;
-        float a = s0[r] * c2, bb = s1[r] * c2;
-        if (diag) {
-          if (key0 + kr > q) a = -INFINITY;
-          if (key0 + 32 + kr > q) bb = -INFINITY;
-        }
-        s0[r] = a;
-        s1[r] = bb;
-        tmax = fmaxf(tmax, fmaxf(a, bb));
-      }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
       // deferred rescale: keep a stale running max unless it grows by more
       // than 2^8 (P ≤ 256 stays exact enough in bf16, fp32 accumulation), so
       // after the first tiles the O/l rescale is skipped wave-uniformly
@@ -182,14 +197,17 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         o0 *= alpha;
         o1 *= alpha;
       }
-      float ls = 0.f;
+      const float nm = -m;
+      f32x2 ls2 = {0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s0[r] = __builtin_amdgcn_exp2f(s0[r] - m);
-        s1[r] = __builtin_amdgcn_exp2f(s1[r] - m);
-        ls += s0[r] + s1[r];
+      for (int r = 0; r < 16; r += 2) {
+        s0[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c2, nm));
+        s0[r + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r + 1], c2, nm));
+        s1[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c2, nm));
+        s1[r + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r + 1], c2, nm));
+        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
       }
-      l += ls;
+      l += ls2[0] + ls2[1];
 #pragma unroll
       for (int sst = 0; sst < 2; ++sst) {
         const bf16x8 p0 = pack8(s0, sst), p1 = pack8(s1, sst);
@@ -273,26 +291,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
     kf[ks] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)key * rs + 16 * ks + 8 * hh);
     vf[ks] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)key * rs + 16 * ks + 8 * hh);
   }
+  retire(kf);
+  retire(vf);
   f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
   const int qt0 = (kb * 128) / TROWS;
   const int nqt = S / TROWS;
   const int wave_kmin = kb * 128 + w * 32;
 
   Stage sq, sd;
-  float st_l = 0.f, st_d = 0.f;
+  // threads 0-63 carry lse·log2e, 64-127 delta of the staged query tile (one
+  // register, one load: a two-variable select here became a scratch array)
+  float st_v = 0.f;
+  const float* st_src = tid < 64 ? lse_bh + tid : del_bh + (tid - 64);
+  const float st_mul = tid < 64 ? LOG2E : 1.f;
   auto load_tile = [&](int qt) {
     stage_load(sq, qbase, rs, qt * TROWS, tid);
     stage_load(sd, dobase, ors, qt * TROWS, tid);
-    if (tid < 64) st_l = lse_bh[qt * TROWS + tid] * LOG2E;
-    else if (tid < 128) st_d = del_bh[qt * TROWS + tid - 64];
+    if (tid < 128) st_v = st_src[qt * TROWS];  // scaled at store time: no wait here
   };
   auto store_tile = [&](int buf) {
     bf16* T = smem + buf * 2 * TROWS * HD;
     stage_store(sq, T, tid);
     stage_store(sd, T + TROWS * HD, tid);
-    float* ss = sstat + buf * 2 * TROWS;
-    if (tid < 64) ss[tid] = st_l;
-    else if (tid < 128) ss[tid] = st_d;
+    if (tid < 128) sstat[buf * 2 * TROWS + tid] = st_v * st_mul;
   };
   load_tile(qt0);
   store_tile(0);
@@ -386,6 +407,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ 
   }
   const float lq = lse[(size_t)bh * S + q] * LOG2E;
   const float dq_delta = delta[(size_t)bh * S + q];
+  retire(qf);
+  retire(df);
+  retire(lq);
+  retire(dq_delta);
   f32x16 a0 = zero16(), a1 = zero16();
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;

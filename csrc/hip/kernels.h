@@ -23,6 +23,11 @@ int colsum_scratch_floats(int G, int C);
 void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st);
 int bias_grad_scratch_floats(long long N, int F);
 int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st);
+// hipBLASLt column-major matmul with epilogue (blaslt.hip); <0 = no solution
+int lt_matmul(int dev, int epi, int ta, int tb, long long m, long long n, long long k, const bf16* A, long long lda,
+              const bf16* B, long long ldb, bf16* D, long long ldd, const void* bias, int bias_is_f32, void* aux,
+              long long ldaux, void* ws, size_t ws_bytes, hipStream_t st);
+const char* lt_last_error();
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 
 // gelu.hip

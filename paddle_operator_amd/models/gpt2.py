@@ -108,8 +108,7 @@ class Block(nn.Module):
         a = ops.attention(self.qkv(h), cfg.n_head)
         a = self.proj.forward_nobias(a)
         x, h2 = ops.add_layer_norm(x, a, self.ln2_w, self.ln2_b, cfg.ln_eps, rbias=self.proj.bias)
-        m = ops.bias_gelu(self.fc.forward_nobias(h2), self.fc.bias)
-        m = self.fc_proj.forward_nobias(m)
+        m = ops.mlp(h2, self.fc.weight, self.fc.bias, self.fc_proj.weight)
         return x, m, self.fc_proj.bias
 
 

@@ -167,22 +167,7 @@ class _LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ w).view(x.shape)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            if _direct_ok(w):
-                g = w.grad.view(Fo, K)
-                s = _splitk(dy2.shape[0], Fo, K)
-                if s > 1:
-                    # long-K / few-tile dW: batched GEMM over token slices + fused fold into the arena
-                    T = dy2.shape[0] // s
-                    part = torch.bmm(dy2.view(s, T, Fo).transpose(1, 2), x2.view(s, T, K),
-                                     out=_workspace(dy2.device, s * Fo * K).view(s, Fo, K))
-                    _native.require_hip().splitk_add(part, g, True)
-                else:
-                    g.addmm_(dy2.t(), x2)
-                w._pdo_ready(w)
-            else:
-                dw = dy2.t() @ x2
+        dw = _weight_grad(w, dy2, x2) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _native.require_hip().bias_grad(dy2.contiguous()) if use_hip(dy2) else dy2.float().sum(0).to(dy.dtype)
@@ -210,6 +195,26 @@ def _splitk(tokens: int, m: int, n: int) -> int:
     while s < 8 and tiles * s < 256 and tokens % (2 * s) == 0 and tokens // (2 * s) >= 2048:
         s *= 2
     return s
+
+
+def _weight_grad(w, dy2, x2):
+    """dW = dy2ᵀ·x2.  Straight into the flat arena when the parameter allows it
+    (returns None), else as a tensor for autograd to accumulate."""
+    Fo, K = dy2.shape[1], x2.shape[1]
+    if not _direct_ok(w):
+        return dy2.t() @ x2
+    g = w.grad.view(Fo, K)
+    s = _splitk(dy2.shape[0], Fo, K)
+    if s > 1:
+        # long-K / few-tile dW: batched GEMM over token slices + fused fold into the arena
+        T = dy2.shape[0] // s
+        part = torch.bmm(dy2.view(s, T, Fo).transpose(1, 2), x2.view(s, T, K),
+                         out=_workspace(dy2.device, s * Fo * K).view(s, Fo, K))
+        _native.require_hip().splitk_add(part, g, True)
+    else:
+        g.addmm_(dy2.t(), x2)
+    w._pdo_ready(w)
+    return None
 
 
 def _direct_ok(p) -> bool:
@@ -244,6 +249,62 @@ class _BiasGeluFn(torch.autograd.Function):
         x2, b = ctx.saved_tensors
         dx, db = m.bias_gelu_bwd(dy.reshape(x2.shape).contiguous(), x2, b)
         return dx.view(ctx.shape), db
+
+
+class _NoFusedEpilogue(RuntimeError):
+    pass
+
+
+class _MLPFn(torch.autograd.Function):
+    """m = gelu(x·W1ᵀ + b1)·W2ᵀ — the GPT-2 MLP without its output bias (folded
+    into the next add+LayerNorm).  Both GELU passes run inside hipBLASLt
+    epilogues (csrc/hip/blaslt.hip): fc1 forward = GELU_AUX_BIAS (writes h
+    and the pre-activation), fc2's input-gradient GEMM = DGELU_BGRAD (writes
+    dh_pre and db1).  No standalone bias-GELU kernels, one fewer pass over the
+    [tokens, 4C] activation each way."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        m = _native.require_hip()
+        x2 = x.reshape(-1, x.shape[-1])
+        r = m.linear_gelu(x2, w1, b1)
+        if not r:
+            raise _NoFusedEpilogue("hipBLASLt GELU_AUX_BIAS unavailable: " + m.lt_last_error())
+        h, hp = r
+        y = h @ w2.t()
+        ctx.save_for_backward(x2, w1, w2, h, hp)
+        ctx.shape = x.shape
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x2, w1, w2, h, hp = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dw2 = _weight_grad(w2, dy2, h) if ctx.needs_input_grad[3] else None
+        r = m.matmul_dgelu(dy2, w2, hp)
+        if r:
+            dh, db1 = r
+        else:  # no DGELU_BGRAD solution: plain GEMM + HIP bias-GELU backward on the post-bias pre-activation
+            dh, db1 = m.bias_gelu_bwd((dy2 @ w2).contiguous(), hp, torch.zeros_like(w1[:, 0]))
+        dw1 = _weight_grad(w1, dh, x2) if ctx.needs_input_grad[1] else None
+        dx = (dh @ w1).view(ctx.shape) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2
+
+
+_FUSED_MLP = [os.environ.get("PDO_FUSED_MLP", "1") != "0"]
+
+
+def mlp(x, w1, b1, w2):
+    """GPT-2 MLP branch without the output bias (see _MLPFn)."""
+    if use_hip(x) and _FUSED_MLP[0]:
+        try:
+            return _MLPFn.apply(x, w1, b1, w2)
+        except _NoFusedEpilogue as e:
+            _FUSED_MLP[0] = False
+            if os.environ.get("PDO_VERBOSE"):
+                print(f"[pdo] fused MLP disabled: {e}")
+    return linear(bias_gelu(linear(x, w1), b1), w2)
 
 
 def bias_gelu(x, b):

@@ -316,3 +316,25 @@ def test_gpt2_tiny_hip_vs_torch(cuda):
     assert abs(loss_h.item() - loss_t.item()) < 2e-2
     for n, p in m.named_parameters():
         assert rel_err(gh[n], p.grad) < 6e-2, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,C", [(2048, 256), (8192, 1024)])
+def test_fused_mlp_epilogues(cuda, T, C):
+    """hipBLASLt GELU_AUX_BIAS / DGELU_BGRAD MLP matches an fp32 reference."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(12)
+    x = torch.randn(T, C, device=cuda, generator=g).bfloat16().requires_grad_()
+    w1 = (0.05 * torch.randn(4 * C, C, device=cuda, generator=g)).bfloat16().requires_grad_()
+    b1 = (0.1 * torch.randn(4 * C, device=cuda, generator=g)).bfloat16().requires_grad_()
+    w2 = (0.05 * torch.randn(C, 4 * C, device=cuda, generator=g)).bfloat16().requires_grad_()
+    y = ops.mlp(x, w1, b1, w2)  # fused hipBLASLt epilogues, or the bias-GELU kernel fallback
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ref = [t.detach().float().requires_grad_() for t in (x, w1, b1, w2)]
+    yf = torch.nn.functional.gelu(ref[0] @ ref[1].t() + ref[2], approximate="tanh") @ ref[3].t()
+    yf.backward(dy.float())
+    assert rel_err(y, yf) < 2e-2
+    for t, r, name in zip((x, w1, b1, w2), ref, ("dx", "dw1", "db1", "dw2")):
+        e = rel_err(t.grad, r.grad)
+        assert e < 3e-2, f"{name} rel err {e}"

@@ -59,7 +59,9 @@ def torch_flags():
     ]
     lib = os.path.join(tdir, "lib")
     ldflags = [f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-               "-ltorch_python", f"-Wl,-rpath,{lib}"]
+               "-ltorch_python", f"-Wl,-rpath,{lib}",
+               # the SAME hipBLASLt torch uses (one copy per process)
+               os.path.join(lib, "libhipblaslt.so")]
     return cflags, ldflags
 
 
@@ -74,11 +76,14 @@ def build_hip(jobs=8, verbose=False):
               # MFMA accumulators in arch VGPRs: no v_accvgpr copies around the
               # VALU work on accumulators (softmax / rescale / epilogues)
               "-mllvm", "-amdgpu-mfma-vgpr-form"]
+    # per-file extras: attention's softmax max-reductions become v_max3 only
+    # without NaN canonicalisation (scores are never NaN; ±inf masks keep working)
+    extra = {"attention.hip": ["-fno-honor-nans"]}
     jobs_list = []
     for s in kernels:
         o = os.path.join(obj_dir, os.path.basename(s) + ".o")
-        if _newer(o, [s] + headers):
-            jobs_list.append([HIPCC] + common + ["-c", s, "-o", o])
+        if _newer(o, [s] + headers + [os.path.abspath(__file__)]):
+            jobs_list.append([HIPCC] + common + extra.get(os.path.basename(s), []) + ["-c", s, "-o", o])
     tcf, tld = torch_flags()
     bind = os.path.join(src_dir, "bind.cpp")
     bind_o = os.path.join(obj_dir, "bind.o")
