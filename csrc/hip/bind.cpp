@@ -212,6 +212,7 @@ void splitk_add(at::Tensor part, at::Tensor out, bool accumulate) {
 // ---------------------------------------------------------------- hipBLASLt fused MLP epilogues
 constexpr int kEpiGeluAuxBias = 164;  // HIPBLASLT_EPILOGUE_GELU_AUX_BIAS
 constexpr int kEpiDGeluBGrad = 208;   // HIPBLASLT_EPILOGUE_DGELU_BGRAD
+constexpr int kEpiDGelu = 192;        // HIPBLASLT_EPILOGUE_DGELU
 constexpr size_t kLtWorkspace = 64ull << 20;
 
 // h = gelu(x·wᵀ + b), h_pre = x·wᵀ + b   (x [T,K], w [N,K], b [N]); empty list = no solution
@@ -239,7 +240,13 @@ std::vector<at::Tensor> matmul_dgelu(at::Tensor dy, at::Tensor w2, at::Tensor h_
   auto ws = at::empty({(long long)kLtWorkspace}, dy.options().dtype(at::kByte));
   int rc = pdo::lt_matmul(dy.get_device(), kEpiDGeluBGrad, 0, 0, N, T, N2, bp(w2), N, bp(dy), N2, bp(dh), N,
                           db.data_ptr(), 0, h_pre.data_ptr(), N, ws.data_ptr(), kLtWorkspace, cur_stream());
-  if (rc != 0) return {};
+  if (rc != 0) {
+    // gfx950 hipBLASLt has DGELU_BGRAD only for small n: DGELU in the GEMM, bias grad by the HIP column reduction
+    rc = pdo::lt_matmul(dy.get_device(), kEpiDGelu, 0, 0, N, T, N2, bp(w2), N, bp(dy), N2, bp(dh), N, nullptr, 0,
+                        h_pre.data_ptr(), N, ws.data_ptr(), kLtWorkspace, cur_stream());
+    if (rc != 0) return {};
+    db = bias_grad(dh);
+  }
   return {dh, db};
 }
 

@@ -255,6 +255,17 @@ class _NoFusedEpilogue(RuntimeError):
     pass
 
 
+_ZB = {}
+
+
+def _zeros_like_bias(b):
+    z = _ZB.get((b.device, b.numel()))
+    if z is None:
+        z = torch.zeros_like(b)
+        _ZB[(b.device, b.numel())] = z
+    return z
+
+
 class _MLPFn(torch.autograd.Function):
     """m = gelu(x·W1ᵀ + b1)·W2ᵀ — the GPT-2 MLP without its output bias (folded
     into the next add+LayerNorm).  Both GELU passes run inside hipBLASLt
@@ -268,9 +279,13 @@ class _MLPFn(torch.autograd.Function):
         m = _native.require_hip()
         x2 = x.reshape(-1, x.shape[-1])
         r = m.linear_gelu(x2, w1, b1)
-        if not r:
-            raise _NoFusedEpilogue("hipBLASLt GELU_AUX_BIAS unavailable: " + m.lt_last_error())
-        h, hp = r
+        if r:
+            h, hp = r
+        else:
+            # gfx950 hipBLASLt has no GELU_AUX_BIAS: bias in the GEMM epilogue
+            # (hp = x·W1ᵀ + b1 is the aux the backward's DGELU epilogue reads), GELU by HIP
+            hp = F.linear(x2, w1, b1)
+            h = m.bias_gelu_fwd(hp, _zeros_like_bias(b1))
         y = h @ w2.t()
         ctx.save_for_backward(x2, w1, w2, h, hp)
         ctx.shape = x.shape
@@ -285,14 +300,18 @@ class _MLPFn(torch.autograd.Function):
         r = m.matmul_dgelu(dy2, w2, hp)
         if r:
             dh, db1 = r
-        else:  # no DGELU_BGRAD solution: plain GEMM + HIP bias-GELU backward on the post-bias pre-activation
-            dh, db1 = m.bias_gelu_bwd((dy2 @ w2).contiguous(), hp, torch.zeros_like(w1[:, 0]))
+        else:  # no DGELU epilogue: plain GEMM + HIP bias-GELU backward on the post-bias pre-activation
+            dh, db1 = m.bias_gelu_bwd((dy2 @ w2).contiguous(), hp, _zeros_like_bias(b1_like(w1)))
         dw1 = _weight_grad(w1, dh, x2) if ctx.needs_input_grad[1] else None
         dx = (dh @ w1).view(ctx.shape) if ctx.needs_input_grad[0] else None
         return dx, dw1, db1, dw2
 
 
 _FUSED_MLP = [os.environ.get("PDO_FUSED_MLP", "1") != "0"]
+
+
+def b1_like(w1):
+    return w1[:, 0]
 
 
 def mlp(x, w1, b1, w2):

@@ -41,7 +41,14 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistIn
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     info = DistInfo(rank, world, local)
+    # PDO_DIST_BACKEND=gloo rehearses the multi-rank GPU path with every rank on
+    # one device (RCCL refuses two ranks per GPU); production is nccl = RCCL
+    backend = backend or os.environ.get("PDO_DIST_BACKEND") or None
     if torch.cuda.is_available():
+        ndev = torch.cuda.device_count()
+        if backend == "gloo" and local >= ndev:
+            local = local % ndev
+            info.local_rank = local
         torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
         if backend is None:

@@ -97,7 +97,20 @@ def build_hip(jobs=8, verbose=False):
     so = os.path.join(PKG, "_pdo_hip.so")
     if _newer(so, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", so] + objs + tld)
+    build_rccl_tools()
     return so
+
+
+def build_rccl_tools():
+    """bin/pdo-allreduce-bench: standalone RCCL bandwidth sweep (no torch)."""
+    src = os.path.join(ROOT, "csrc", "rccl", "allreduce_bench.hip")
+    exe = os.path.join(ROOT, "bin", "pdo-allreduce-bench")
+    if not os.path.exists(src) or not _newer(exe, [src]):
+        return exe
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    _run([HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", src, "-o", exe, "-L/opt/rocm/lib", "-lrccl",
+          "-Wl,-rpath,/opt/rocm/lib"])
+    return exe
 
 
 def build_core(jobs=8):
