@@ -95,12 +95,18 @@ class JobEnv:
         return h, int(p)
 
     def ps_world(self):
-        """PS mode: ranks 0..P-1 are pservers, P.. are trainers (gloo group)."""
+        """PS mode: ranks 0..P-1 are pservers, P..P+T-1 trainers, then heter workers."""
         P = len(self.pserver_endpoints)
         T = len(self.trainer_endpoints) or self.trainers_num
-        rank = self.trainer_id if self.role == "PSERVER" else P + self.trainer_id
+        H = len(self.heter_endpoints)
+        if self.role == "PSERVER":
+            rank = self.trainer_id
+        elif self.role == "HETER":
+            rank = P + T + self.trainer_id
+        else:
+            rank = P + self.trainer_id
         master = self.pserver_endpoints[0] if self.pserver_endpoints else f"{self.pod_ip}:{self.port}"
-        return rank, P + T, master
+        return rank, P + T + H, master
 
     def torch_env(self, local_rank: int = 0, nproc_per_pod: int = 1) -> Dict[str, str]:
         if self.mode == "PS":

@@ -167,11 +167,14 @@ def run_ps(args, jenv) -> int:
     host, port = master.rsplit(":", 1)
     n_ps = len(jenv.pserver_endpoints)
     cfg = WideDeepConfig(vocab_per_slot=1000) if args.tiny else WideDeepConfig()
-    name = f"ps{jenv.trainer_id}" if jenv.role == "PSERVER" else f"trainer{jenv.trainer_id}"
+    n_heter = len(jenv.heter_endpoints)
+    name = {"PSERVER": "ps", "HETER": "heter"}.get(jenv.role, "trainer") + str(jenv.trainer_id)
     opts = rpc.TensorPipeRpcBackendOptions(init_method=f"tcp://{host}:{int(port) + 1}", rpc_timeout=args.timeout,
                                            num_worker_threads=16)
     if jenv.role == "PSERVER":
         psmod.serve(jenv.trainer_id, n_ps, cfg)
+    elif jenv.role == "HETER":
+        psmod.serve_heter(cfg)  # dense tower on this worker's GPU (CPU without one)
     rpc.init_rpc(name, rank=rank, world_size=world, rpc_backend_options=opts)
     # gloo group on the reference's gloo HTTP endpoint (ps-0:2397) for barrier/metrics
     gloo = None
@@ -184,8 +187,9 @@ def run_ps(args, jenv) -> int:
                                t_pg=time.time())
     bootstrap.report_ready(b, jenv.job_key(), jenv.kv_endpoints(), {"role": jenv.role, "workload": "wide_deep"})
     loss_sum = 0.0
-    if jenv.role != "PSERVER" and not args.exit_after_ready:
-        client = psmod.PSClient(n_ps, cfg, sync=args.sync_ps)
+    if jenv.role == "TRAINER" and not args.exit_after_ready:
+        client = (psmod.HeterPSClient(n_ps, n_heter, cfg, sync=args.sync_ps, first=jenv.trainer_id) if n_heter
+                  else psmod.PSClient(n_ps, cfg, sync=args.sync_ps))
         gen = torch.Generator().manual_seed(1000 + jenv.trainer_id)
         B = args.batch or 512
         t0 = time.perf_counter()
@@ -201,7 +205,8 @@ def run_ps(args, jenv) -> int:
         print("PDO_DONE " + json.dumps({"role": "TRAINER", "trainer": jenv.trainer_id, "steps": args.steps,
                                         "seconds": dt, "samples_per_s": B * args.steps / dt,
                                         "first_loss": losses[0] if losses else None, "last_loss": loss_sum,
-                                        "server_stats": client.server_stats()}), flush=True)
+                                        "server_stats": client.server_stats(),
+                                        "heter_stats": client.heter_stats() if n_heter else None}), flush=True)
     if gloo:
         t = torch.tensor([loss_sum])
         dist.all_reduce(t)

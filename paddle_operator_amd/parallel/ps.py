@@ -172,3 +172,94 @@ class PSClient:
 
     def server_stats(self):
         return [rpc.rpc_sync(f"ps{i}", _stats) for i in range(self.n_ps)]
+
+
+# ---------------------------------------------------------------------------
+# Heterogeneous PS (PaddleJob ``spec.heter``; role HETER, PADDLE_HETER_ENDPOINTS,
+# reference paddlejob_types.go:40,47,146-147 / paddlejob_helper.go:266-268):
+# CPU trainers keep the sparse side (pull rows from the pservers, push row
+# gradients), GPU heter workers own the dense tower and run its forward /
+# backward / Adam on an MI355X.  RPC names "heter{i}", ranks after the trainers.
+# ---------------------------------------------------------------------------
+_HETER: Optional["HeterServer"] = None
+
+
+class HeterServer:
+    def __init__(self, cfg: WideDeepConfig, device=None, lr: float = 1e-3, seed: int = 0):
+        self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        torch.manual_seed(seed)
+        self.tower = DeepTower(cfg).to(self.device)
+        self.opt = torch.optim.Adam(self.tower.parameters(), lr=lr)
+        self.lock = threading.Lock()
+        self.steps = 0
+
+    def step(self, deep_rows, wide_rows, inv, dense, label):
+        d = self.device
+        with self.lock:
+            dr = deep_rows.to(d, non_blocking=True).requires_grad_()
+            wr = wide_rows.to(d, non_blocking=True).requires_grad_()
+            logit = self.tower(dr[inv.to(d)], wr[inv.to(d)], dense.to(d))
+            loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, label.to(d))
+            self.opt.zero_grad(set_to_none=True)
+            loss.backward()
+            self.opt.step()
+            self.steps += 1
+            return float(loss.detach()), dr.grad.cpu(), wr.grad.cpu()
+
+    def stats(self):
+        return {"heter_steps": self.steps, "device": str(self.device)}
+
+
+def _heter_step(deep_rows, wide_rows, inv, dense, label):
+    return _HETER.step(deep_rows, wide_rows, inv, dense, label)
+
+
+def _heter_stats():
+    return _HETER.stats()
+
+
+def serve_heter(cfg: WideDeepConfig, device=None, **kw):
+    global _HETER
+    _HETER = HeterServer(cfg, device, **kw)
+    return _HETER
+
+
+class HeterPSClient(PSClient):
+    """Trainer that offloads the dense tower to heter workers (round robin)."""
+
+    def __init__(self, n_ps: int, n_heter: int, cfg: WideDeepConfig, sync: bool = False, first: int = 0):
+        super().__init__(n_ps, cfg, sync)
+        self.n_heter = n_heter
+        self._rr = first
+
+    def step(self, ids, dense, label) -> float:
+        uniq, inv = torch.unique(ids, return_inverse=True)
+        parts = self._split(uniq)
+        futs = [rpc.rpc_async(f"ps{i}", _pull, args=(p,)) if p.numel() else None for i, p in enumerate(parts)]
+        for f in self._pending:
+            f.wait()
+        self._pending = []
+        rows_d, rows_w = [], []
+        for f in futs:
+            if f is None:
+                continue
+            d, w = f.wait()
+            rows_d.append(d)
+            rows_w.append(w)
+        h = self._rr % self.n_heter
+        self._rr += 1
+        loss, gd, gw = rpc.rpc_sync(f"heter{h}", _heter_step,
+                                    args=(torch.cat(rows_d), torch.cat(rows_w), inv, dense, label))
+        off = 0
+        for i, p in enumerate(parts):
+            n = p.numel()
+            if not n:
+                continue
+            self._pending.append(rpc.rpc_async(f"ps{i}", _push, args=(p, gd[off:off + n], gw[off:off + n])))
+            off += n
+        if self.sync:
+            self.flush()
+        return loss
+
+    def heter_stats(self):
+        return [rpc.rpc_sync(f"heter{i}", _heter_stats) for i in range(self.n_heter)]

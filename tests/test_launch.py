@@ -197,3 +197,21 @@ def test_elastic_scale_out_reforms_world(tmp_path):
     assert worlds == [2, 3]
     # the 3-rank generation resumed from a checkpoint written by the 2-rank one
     assert max(r["resume_step"] for r in readies if r["world"] == 3) >= 5
+
+
+def test_heter_ps_mode(tmp_path):
+    """spec.heter: CPU trainers keep the sparse side, the heter worker owns the dense tower."""
+    base = free_port_block()
+    common = {"PADDLE_PSERVERS_IP_PORT_LIST": f"127.0.0.1:{base}",
+              "PADDLE_TRAINER_ENDPOINTS": f"127.0.0.1:{base + 20},127.0.0.1:{base + 40}",
+              "PADDLE_HETER_ENDPOINTS": f"127.0.0.1:{base + 60}", "PADDLE_TRAINERS_NUM": 2}
+    args = ["--workload", "wide_deep", "--tiny", "--steps", "60", "--batch", "256"]
+    procs = [launch(dict(common, TRAINING_ROLE="PSERVER", PADDLE_TRAINER_ID=0), args, tmp_path / "ps0.log"),
+             launch(dict(common, TRAINING_ROLE="HETER", PADDLE_TRAINER_ID=0), args, tmp_path / "h0.log")]
+    procs += [launch(dict(common, TRAINING_ROLE="TRAINER", PADDLE_TRAINER_ID=i), args, tmp_path / f"t{i}.log")
+              for i in range(2)]
+    assert wait_all(procs) == [0, 0, 0, 0], open(tmp_path / "t0.log").read()[-3000:]
+    for i in range(2):
+        d = records(tmp_path / f"t{i}.log", "PDO_DONE")[0]
+        assert d["last_loss"] < d["first_loss"] - 0.05, d
+        assert d["heter_stats"][0]["heter_steps"] >= 60  # this trainer's steps (at least) ran on the heter worker
