@@ -35,8 +35,12 @@ manifests:             ## regenerate deploy/ config/ charts/*/crds
 manifests-check:
 	$(PY) -m paddle_operator_amd.deploy --check
 
-sanitize:              ## host-only ASan/UBSan build of the control plane + tests
-	cmake -S csrc -B build/asan -G Ninja -DPDO_SANITIZE=ON && ninja -C build/asan pdo-core-tests && build/asan/pdo-core-tests
+SAN_CMAKE = -G Ninja -DCMAKE_BUILD_TYPE=Debug -Dpybind11_DIR=$$($(PY) -c 'import pybind11;print(pybind11.get_cmake_dir())')
+sanitize:              ## host-only ASan+UBSan and TSan builds of the control plane, run the native tests
+	cmake -S csrc -B build/asan $(SAN_CMAKE) -DPDO_SANITIZE=address,undefined -DPDO_BIN_DIR=$(CURDIR)/build/asan/bin -DPDO_PKG_DIR=$(CURDIR)/build/asan/pkg
+	ninja -C build/asan pdo-core-tests && UBSAN_OPTIONS=halt_on_error=1 build/asan/bin/pdo-core-tests
+	cmake -S csrc -B build/tsan $(SAN_CMAKE) -DPDO_SANITIZE=thread -DPDO_BIN_DIR=$(CURDIR)/build/tsan/bin -DPDO_PKG_DIR=$(CURDIR)/build/tsan/pkg
+	ninja -C build/tsan pdo-core-tests && TSAN_OPTIONS=halt_on_error=1 build/tsan/bin/pdo-core-tests
 
 docker-build:
 	docker build --target manager -t $(IMG_MANAGER) .

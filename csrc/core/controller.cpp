@@ -91,7 +91,7 @@ bool Controller::process_one(double timeout_s) {
 void Controller::record_event(const Value& obj, const std::string& kind, const std::string& type,
                               const std::string& reason, const std::string& msg) {
   if (!opt_.record_events) return;
-  static std::mt19937_64 rng(std::random_device{}());
+  thread_local std::mt19937_64 rng(std::random_device{}());  // one per worker thread (TSan-clean)
   const Value& md = obj.get("metadata");
   Value ev = Value::object();
   ev["apiVersion"] = "v1";

@@ -1,4 +1,5 @@
 // SPDX-License-Identifier: Apache-2.0
+#include "sync.h"
 #include "kvclient.h"
 
 #include <chrono>
@@ -283,7 +284,7 @@ void mount_gateway(http::Server& srv, KVStore& s) {
         std::deque<std::string> batch;
         {
           std::unique_lock<std::mutex> l(qq->mu);
-          qq->cv.wait_for(l, std::chrono::milliseconds(500), [&] { return !qq->lines.empty(); });
+          wait_for_s(qq->cv, l, 0.5, [&] { return !qq->lines.empty(); });
           batch.swap(qq->lines);
         }
         bool alive = true;

@@ -1,4 +1,5 @@
 // SPDX-License-Identifier: Apache-2.0
+#include "sync.h"
 #include "kvstore.h"
 
 #include <chrono>
@@ -294,7 +295,7 @@ void KVStore::cancel(int64_t watch_id) {
 
 int64_t KVStore::wait_revision(int64_t rev, double timeout_s) {
   std::unique_lock<std::mutex> l(mu_);
-  cv_.wait_for(l, std::chrono::duration<double>(timeout_s), [&] { return rev_ > rev; });
+  wait_for_s(cv_, l, timeout_s, [&] { return rev_ > rev; });
   return rev_;
 }
 

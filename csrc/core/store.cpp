@@ -1,4 +1,5 @@
 // SPDX-License-Identifier: Apache-2.0
+#include "sync.h"
 #include "store.h"
 
 #include <chrono>
@@ -277,7 +278,7 @@ bool Store::has_events() const {
 bool Store::wait_events(double timeout_s) {
   std::unique_lock<std::mutex> l(mu_);
   if (!pending_.empty()) return true;
-  cv_.wait_for(l, std::chrono::duration<double>(timeout_s), [&] { return !pending_.empty(); });
+  wait_for_s(cv_, l, timeout_s, [&] { return !pending_.empty(); });
   return !pending_.empty();
 }
 

@@ -91,7 +91,11 @@ bool WorkQueue::get(std::string* key, double timeout_s) {
                          std::chrono::duration<double>(std::max(0.0, dt)));
       if (w < until) until = w;
     }
-    cv_.wait_until(l, until);
+    // system_clock wait → pthread_cond_timedwait.  (A steady_clock wait is
+    // pthread_cond_clockwait in libstdc++ 11, which gcc-11's TSan does not
+    // intercept: every wait then reads as a held lock / false data race.)
+    cv_.wait_until(l, std::chrono::system_clock::now() +
+                          std::chrono::duration_cast<std::chrono::system_clock::duration>(until - now));
   }
   *key = queue_.front();
   queue_.pop_front();
