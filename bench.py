@@ -9,7 +9,11 @@ tokens/s.  The time from process start until every rank is ready (RCCL
 communicator up, weights broadcast, first barrier passed) is reported as
 ``ready_s`` alongside.  The operator-level launch latency (PaddleJob →
 all-ranks-ready through the control plane) is measured by
-``python -m paddle_operator_amd.bench_launch``.
+``python bench_launch.py``.
+
+Per-GPU micro-batch 64 × 1024 tokens (weak scaling): at 8 GPUs the global
+batch is 512 sequences = 0.5 M tokens, GPT-2's own batch size; GEMM shapes
+are pre-tuned for it (paddle_operator_amd/tuning/*_b64_gfx950.csv).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it runs under ``torch.distributed.run`` one rank per GPU.  W untimed steps,
@@ -36,7 +40,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-medium")
-    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("PDO_MICRO_BATCH", "32")))
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("PDO_MICRO_BATCH", "64")))
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=int, default=64)
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
