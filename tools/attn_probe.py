@@ -3,6 +3,7 @@
     python tools/attn_probe.py [--B 32] [--S 1024] [--H 16]
 """
 import argparse
+import os
 import json
 import sys
 
@@ -44,6 +45,8 @@ def main():
     o, lse = m.attn_fwd(qkv.view(B, S, 3 * H * D), H)
     res["pdo_fwd_us"] = bench(lambda: m.attn_fwd(qkv.view(B, S, 3 * H * D), H))
     res["pdo_bwd_us"] = bench(lambda: m.attn_bwd(dout.view(B, S, H * D), qkv.view(B, S, 3 * H * D), o, lse, H))
+    if os.environ.get("PDO_ATTN_PIPE") is not None:
+        res["pipe"] = os.environ["PDO_ATTN_PIPE"]
     # correctness vs SDPA (fp32 math on bf16 inputs)
     q, k, v = [qkv[:, :, i].transpose(1, 2) for i in range(3)]
     ref = F.scaled_dot_product_attention(q.float(), k.float(), v.float(), is_causal=True)
