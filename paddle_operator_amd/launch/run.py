@@ -24,7 +24,7 @@ T_START = time.time()
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(prog="pdo-launch")
-    ap.add_argument("--workload", default="noop", choices=["gpt2", "resnet50", "wide_deep", "noop"])
+    ap.add_argument("--workload", default="noop", choices=["gpt2", "resnet50", "wide_deep", "deepfm", "noop"])
     ap.add_argument("--model", default="gpt2-medium")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=0, help="per-rank micro batch (0 = workload default)")
@@ -166,7 +166,8 @@ def run_ps(args, jenv) -> int:
     rank, world, master = jenv.ps_world()
     host, port = master.rsplit(":", 1)
     n_ps = len(jenv.pserver_endpoints)
-    cfg = WideDeepConfig(vocab_per_slot=1000) if args.tiny else WideDeepConfig()
+    model = "deepfm" if args.workload == "deepfm" else "wide_deep"
+    cfg = WideDeepConfig(vocab_per_slot=1000, model=model) if args.tiny else WideDeepConfig(model=model)
     n_heter = len(jenv.heter_endpoints)
     name = {"PSERVER": "ps", "HETER": "heter"}.get(jenv.role, "trainer") + str(jenv.trainer_id)
     opts = rpc.TensorPipeRpcBackendOptions(init_method=f"tcp://{host}:{int(port) + 1}", rpc_timeout=args.timeout,
@@ -220,7 +221,7 @@ def main(argv=None) -> int:
     from .env import JobEnv
     jenv = JobEnv.from_env()
     log(f"role={jenv.role} id={jenv.trainer_id} mode={jenv.mode} elastic={jenv.elastic} workload={args.workload}")
-    if jenv.mode == "PS" or args.workload == "wide_deep" and jenv.pserver_endpoints:
+    if jenv.mode == "PS" or args.workload in ("wide_deep", "deepfm") and jenv.pserver_endpoints:
         return run_ps(args, jenv)
     if (jenv.elastic or args.elastic) and not args.worker:
         from .elastic import run_agent

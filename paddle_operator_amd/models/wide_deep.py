@@ -24,6 +24,7 @@ class WideDeepConfig:
     emb_dim: int = 16
     n_dense: int = 13
     hidden: tuple = (400, 400, 400)
+    model: str = "wide_deep"  # "wide_deep" | "deepfm" (deploy/examples/deepfm.yaml)
 
     @property
     def rows(self) -> int:
@@ -49,6 +50,21 @@ class DeepTower(nn.Module):
         return self.mlp(x).squeeze(1) + wide_w.sum(dim=(1, 2)) + self.wide_bias
 
 
+class DeepFMTower(DeepTower):
+    """DeepFM: the wide (first-order) term + a factorisation-machine
+    second-order term over the slot embeddings + the deep MLP, all sharing the
+    same sparse tables (so the PS protocol is unchanged)."""
+
+    def forward(self, deep_emb, wide_w, dense):
+        s = deep_emb.sum(dim=1)  # [B, D]
+        fm = 0.5 * (s * s - (deep_emb * deep_emb).sum(dim=1)).sum(dim=1)
+        return super().forward(deep_emb, wide_w, dense) + fm
+
+
+def make_tower(cfg: WideDeepConfig) -> DeepTower:
+    return DeepFMTower(cfg) if cfg.model == "deepfm" else DeepTower(cfg)
+
+
 class WideDeep(nn.Module):
     """Single-process model (Single / Collective modes and tests)."""
 
@@ -59,7 +75,7 @@ class WideDeep(nn.Module):
         self.wide = nn.Embedding(cfg.rows, 1)
         nn.init.normal_(self.deep_emb.weight, std=0.01)
         nn.init.zeros_(self.wide.weight)
-        self.tower = DeepTower(cfg)
+        self.tower = make_tower(cfg)
 
     def forward(self, ids, dense):
         return self.tower(self.deep_emb(ids), self.wide(ids), dense)

@@ -22,7 +22,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed.rpc as rpc
 
-from ..models.wide_deep import DeepTower, WideDeepConfig, shard_rows
+from ..models.wide_deep import WideDeepConfig, make_tower, shard_rows
 
 _SERVER: Optional["ShardServer"] = None
 
@@ -43,7 +43,7 @@ class ShardServer:
         self.tower: Optional[DeepTower] = None
         if shard == 0:
             torch.manual_seed(seed)
-            self.tower = DeepTower(cfg)
+            self.tower = make_tower(cfg)
             self.opt = torch.optim.Adam(self.tower.parameters(), lr=dense_lr)
 
     def pull(self, ids: torch.Tensor):
@@ -115,7 +115,7 @@ class PSClient:
         self.cfg = cfg
         self.sync = sync
         self.bounds = shard_rows(cfg.rows, n_ps)
-        self.tower = DeepTower(cfg)
+        self.tower = make_tower(cfg)
         self._pending: List = []
 
     def _split(self, uniq: torch.Tensor):
@@ -188,7 +188,7 @@ class HeterServer:
     def __init__(self, cfg: WideDeepConfig, device=None, lr: float = 1e-3, seed: int = 0):
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         torch.manual_seed(seed)
-        self.tower = DeepTower(cfg).to(self.device)
+        self.tower = make_tower(cfg).to(self.device)
         self.opt = torch.optim.Adam(self.tower.parameters(), lr=lr)
         self.lock = threading.Lock()
         self.steps = 0

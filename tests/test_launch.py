@@ -138,13 +138,14 @@ def test_collective_checkpoint_resume(tmp_path):
 
 
 # ----------------------------------------------------------------------------- parameter server
-def test_ps_mode_wide_deep(tmp_path):
+@pytest.mark.parametrize("workload", ["wide_deep", "deepfm"])
+def test_ps_mode_wide_deep(tmp_path, workload):
     base = free_port_block()
     common = {"PADDLE_PSERVERS_IP_PORT_LIST": f"127.0.0.1:{base}",
               "PADDLE_TRAINER_ENDPOINTS": f"127.0.0.1:{base + 20},127.0.0.1:{base + 40}",
               "PADDLE_TRAINERS_NUM": 2, "PADDLE_WITH_GLOO": 1,
               "PADDLE_GLOO_HTTP_ENDPOINT": f"127.0.0.1:{base + 18}"}
-    args = ["--workload", "wide_deep", "--tiny", "--steps", "60", "--batch", "256"]
+    args = ["--workload", workload, "--tiny", "--steps", "60", "--batch", "256"]
     procs = [launch(dict(common, TRAINING_ROLE="PSERVER", PADDLE_TRAINER_ID=0), args, tmp_path / "ps0.log")]
     procs += [launch(dict(common, TRAINING_ROLE="TRAINER", PADDLE_TRAINER_ID=i), args, tmp_path / f"t{i}.log")
               for i in range(2)]
