@@ -250,6 +250,46 @@ std::vector<at::Tensor> matmul_dgelu(at::Tensor dy, at::Tensor w2, at::Tensor h_
   return {dh, db};
 }
 
+// ---------------------------------------------------------------- NHWC BatchNorm + ReLU (+ residual)
+// x: channels_last bf16 [N,C,H,W] (memory NHWC); w,b,running_*: fp32 [C]
+std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor w, at::Tensor b,
+                                   c10::optional<at::Tensor> rm, c10::optional<at::Tensor> rv, double eps,
+                                   double momentum, bool relu) {
+  CHECK_BF16(x); CHECK_F32(w); CHECK_F32(b);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_act_fwd: channels_last bf16 input");
+  const long long C = x.size(1), M = x.numel() / C;
+  auto y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  auto mean = at::empty({C}, w.options()), invstd = at::empty({C}, w.options());
+  auto scratch = at::empty({(long long)pdo::bn_fwd_scratch_floats(M, C)}, w.options());
+  const bf16* rp = nullptr;
+  if (res && res->defined()) {
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(at::MemoryFormat::ChannelsLast));
+    CHECK_BF16((*res));
+    rp = bp(*res);
+  }
+  float* rmp = rm && rm->defined() ? fp(*rm) : nullptr;
+  float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
+  CHECK_RC(pdo::bn_fwd(bp(x), rp, fp(w), fp(b), rmp, rvp, M, (int)C, (float)eps, (float)momentum, relu ? 1 : 0,
+                       bp(y), fp(mean), fp(invstd), fp(scratch), cur_stream()), "bn_fwd");
+  return {y, mean, invstd};
+}
+
+std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor mean, at::Tensor invstd,
+                                   at::Tensor w, bool relu, bool want_dres) {
+  CHECK_BF16(dy); CHECK_BF16(y); CHECK_BF16(x);
+  auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  const long long C = x.size(1), M = x.numel() / C;
+  auto dx = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  at::Tensor dres;
+  if (want_dres) dres = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  auto dw = at::empty({C}, w.options()), db = at::empty({C}, w.options());
+  auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_floats(M, C)}, w.options());
+  CHECK_RC(pdo::bn_bwd(bp(dyc), bp(y), bp(x), fp(mean), fp(invstd), fp(w), M, (int)C, relu ? 1 : 0, bp(dx),
+                       want_dres ? bp(dres) : nullptr, fp(dw), fp(db), fp(scratch), cur_stream()), "bn_bwd");
+  return {dx, dres, dw, db};
+}
+
 // ---------------------------------------------------------------- attention
 std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t n_head) {
   CHECK_IN(qkv); CHECK_BF16(qkv);
@@ -397,6 +437,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("sumsq", &sumsq);
   m.def("adamw_flat", &adamw_flat);
   m.def("splitk_add", &splitk_add);
+  m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_bwd", &bn_act_bwd);
   m.def("linear_gelu", &linear_gelu);
   m.def("lt_last_error", [] { return std::string(pdo::lt_last_error()); });
   // raw probe: epilogue id on D[m,n] = op(A)op(B) with optional bias/aux (diagnostics)

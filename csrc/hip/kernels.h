@@ -28,6 +28,14 @@ int lt_matmul(int dev, int epi, int ta, int tb, long long m, long long n, long l
               const bf16* B, long long ldb, bf16* D, long long ldd, const void* bias, int bias_is_f32, void* aux,
               long long ldaux, void* ws, size_t ws_bytes, hipStream_t st);
 const char* lt_last_error();
+// NHWC BatchNorm (+ReLU, +residual) training forward / backward (batchnorm.hip)
+int bn_fwd_scratch_floats(long long M, int C);
+int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float* running_mean, float* running_var,
+           long long M, int C, float eps, float momentum, int relu, bf16* y, float* mean, float* invstd,
+           float* scratch, hipStream_t st);
+int bn_bwd_scratch_floats(long long M, int C);
+int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, const float* invstd, const float* w,
+           long long M, int C, int relu, bf16* dx, bf16* dres, float* dw, float* db, float* scratch, hipStream_t st);
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 
 // gelu.hip

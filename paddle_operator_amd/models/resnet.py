@@ -3,15 +3,18 @@ elastic ResNet-50) — written out here because torchvision is not part of the
 image.  Standard v1.5 bottleneck architecture (stride on the 3×3 conv).
 
 MI355X choices: channels_last activations + bf16 autocast so MIOpen picks
-its NHWC implicit-GEMM convolutions on the matrix cores; BatchNorm in fp32
-(autocast keeps it there); parameters live in a flat fp32 arena
-(parallel.flat) so the gradient all-reduce buckets are slices.
+its NHWC implicit-GEMM convolutions on the matrix cores; BatchNorm (fp32
+statistics and affine params) fused with ReLU and the residual add into HIP
+kernels (ops.bn_act); parameters live in a flat fp32 arena (parallel.flat) so
+the gradient all-reduce buckets are slices.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from .. import ops
 
 
 class Bottleneck(nn.Module):
@@ -29,13 +32,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        # BN + ReLU (+ residual add) fused into one HIP pass each (ops.bn_act)
         idt = x
-        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        out = F.relu(self.bn2(self.conv2(out)), inplace=True)
-        out = self.bn3(self.conv3(out))
+        out = ops.bn_act(self.bn1, self.conv1(x))
+        out = ops.bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
-            idt = self.downsample(x)
-        return F.relu(out + idt, inplace=True)
+            idt = ops.bn_act(self.downsample[1], self.downsample[0](x), relu=False)
+        return ops.bn_act(self.bn3, self.conv3(out), relu=True, residual=idt)
 
 
 class ResNet(nn.Module):
@@ -70,7 +73,7 @@ class ResNet(nn.Module):
                 nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x):
-        x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        x = ops.bn_act(self.bn1, self.conv1(x))
         x = F.max_pool2d(x, 3, 2, 1)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

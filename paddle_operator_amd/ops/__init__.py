@@ -455,3 +455,49 @@ def embedding(idx, wte, wpe):
         return _EmbedFn.apply(idx.contiguous(), wte, wpe)
     S = idx.shape[1]
     return F.embedding(idx, wte) + wpe[:S].unsqueeze(0)
+
+
+# ----------------------------------------------------------------------------
+# BatchNorm (training) + ReLU (+ residual add) for NHWC bf16 — ResNet-50
+# ----------------------------------------------------------------------------
+
+class _BNActFn(torch.autograd.Function):
+    """y = act(BN(x) [+ residual]) with batch statistics (csrc/hip/batchnorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu):
+        m = _native.require_hip()
+        y, mean, invstd = m.bn_act_fwd(x, residual, w, b, running_mean, running_var, eps, momentum, relu)
+        ctx.save_for_backward(x, y, mean, invstd, w)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x, y, mean, invstd, w = ctx.saved_tensors
+        dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, ctx.relu, ctx.has_res)
+        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None
+
+
+_BN_FUSED = [os.environ.get("PDO_BN_FUSED", "1") != "0"]
+
+
+def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
+    """Training BatchNorm → (+ residual) → ReLU in one HIP forward pass over the
+    activation (plus a statistics pass), and one backward pass (plus stats).
+    Falls back to PyTorch ops outside the fused case (eval mode, CPU, NCHW,
+    C % 8 != 0)."""
+    fused = (_BN_FUSED[0] and use_hip(x) and bn.training and x.dtype == torch.bfloat16 and x.dim() == 4
+             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0
+             and bn.weight is not None and bn.weight.dtype == torch.float32
+             and (residual is None or (residual.dtype == torch.bfloat16
+                                       and residual.is_contiguous(memory_format=torch.channels_last))))
+    if fused:
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        return _BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import glob
 import os
+import shutil
 
 import torch
 
@@ -47,3 +48,28 @@ def enable_tuned_gemms(verbose: bool = False) -> int:
     if verbose:
         print(f"[pdo] tuned GEMM tables loaded: {n}")
     return n
+
+
+def use_shipped_miopen_db(verbose: bool = False) -> str | None:
+    """Point MIOpen's user find-db/perf-db at a private copy of the shipped
+    gfx950 convolution find results (``tuning/miopen/*``), before the first
+    convolution creates a MIOpen handle.  A user-set ``MIOPEN_USER_DB_PATH`` is
+    left alone.  Returns the db directory in use (None if nothing shipped)."""
+    if os.environ.get("MIOPEN_USER_DB_PATH"):
+        return os.environ["MIOPEN_USER_DB_PATH"]
+    src = os.path.join(_DIR, "miopen")
+    files = [f for f in glob.glob(os.path.join(src, "*")) if os.path.isfile(f)]
+    if not files:
+        return None
+    dst = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"pdo-miopen-{os.getuid()}")
+    os.makedirs(dst, exist_ok=True)
+    for f in files:
+        t = os.path.join(dst, os.path.basename(f))
+        if not os.path.exists(t) or os.path.getmtime(t) < os.path.getmtime(f):
+            tmp = f"{t}.{os.getpid()}"
+            shutil.copy2(f, tmp)  # MIOpen appends to its user db: never hand it the tracked file
+            os.replace(tmp, t)  # atomic: ranks of one node share the directory
+    os.environ["MIOPEN_USER_DB_PATH"] = dst
+    if verbose:
+        print(f"[pdo] MIOpen user db: {dst} ({len(files)} shipped files)")
+    return dst

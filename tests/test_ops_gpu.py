@@ -338,3 +338,43 @@ def test_fused_mlp_epilogues(cuda, T, C):
     for t, r, name in zip((x, w1, b1, w2), ref, ("dx", "dw1", "db1", "dw2")):
         e = rel_err(t.grad, r.grad)
         assert e < 3e-2, f"{name} rel err {e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,H,relu,res", [(8, 64, 28, True, False), (4, 256, 14, True, True),
+                                              (16, 128, 7, False, False), (2, 2048, 7, True, True)])
+def test_bn_act_nhwc(cuda, N, C, H, relu, res):
+    """Fused NHWC BatchNorm(+residual)(+ReLU) vs fp32 PyTorch, incl. running stats."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(13)
+    x = (3 + 2 * torch.randn(N, C, H, H, device=cuda, generator=g)).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+    r = None
+    if res:
+        r = torch.randn(N, C, H, H, device=cuda, generator=g).bfloat16()
+        r = r.contiguous(memory_format=torch.channels_last).requires_grad_()
+    bn = torch.nn.BatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(C, device=cuda, generator=g))
+        bn.bias.copy_(0.1 * torch.randn(C, device=cuda, generator=g))
+    bnf = torch.nn.BatchNorm2d(C).to(cuda)
+    bnf.load_state_dict(bn.state_dict())
+    y = ops.bn_act(bn, x, relu=relu, residual=r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf = x.detach().float().requires_grad_()
+    rf = r.detach().float().requires_grad_() if res else None
+    yf = bnf(xf)
+    if res:
+        yf = yf + rf
+    if relu:
+        yf = torch.relu(yf)
+    yf.backward(dy.float())
+    assert rel_err(y, yf) < 2e-2
+    assert rel_err(x.grad, xf.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bnf.weight.grad) < 2e-2
+    assert rel_err(bn.bias.grad, bnf.bias.grad) < 2e-2
+    if res:
+        assert rel_err(r.grad, rf.grad) < 2e-2
+    assert rel_err(bn.running_mean, bnf.running_mean) < 1e-3
+    assert rel_err(bn.running_var, bnf.running_var) < 1e-3

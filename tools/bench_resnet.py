@@ -1,0 +1,41 @@
+"""ResNet-50 training throughput (img/s) on one GPU — BASELINE configs 2/3/5 workload.
+
+    python tools/bench_resnet.py [--batch 256] [--steps 20] [--warmup 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+    from paddle_operator_amd.workloads.resnet import ResNetTrainer
+    t0 = time.time()
+    tr = ResNetTrainer(a.batch, "cuda:0")
+    for _ in range(a.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    t_warm = time.time() - t0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.steps):
+        loss = tr.step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.steps
+    print(json.dumps({"metric": "ResNet-50 train img/s (bf16 autocast, channels_last)", "value": round(a.batch / ms * 1e3, 1),
+                      "ms_per_step": round(ms, 2), "batch": a.batch, "warmup_s": round(t_warm, 1),
+                      "loss": float(loss.detach()), "miopen_find_mode": os.environ.get("MIOPEN_FIND_MODE", "default")}))
+
+
+if __name__ == "__main__":
+    main()
