@@ -275,19 +275,68 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> res, 
   return {y, mean, invstd};
 }
 
-std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor mean, at::Tensor invstd,
-                                   at::Tensor w, bool relu, bool want_dres) {
-  CHECK_BF16(dy); CHECK_BF16(y); CHECK_BF16(x);
+std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor mean,
+                                   at::Tensor invstd, at::Tensor w, at::Tensor b, bool relu, bool want_dres,
+                                   c10::optional<at::Tensor> dw_into, c10::optional<at::Tensor> db_into) {
+  CHECK_BF16(dy); CHECK_BF16(x); CHECK_F32(w); CHECK_F32(b);
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "bn_act_bwd: channels_last x");
   auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  const bf16* yp = nullptr;
+  if (y && y->defined()) {
+    CHECK_BF16((*y));
+    TORCH_CHECK(y->sizes() == x.sizes() && y->is_contiguous(at::MemoryFormat::ChannelsLast));
+    yp = bp(*y);
+  }
+  TORCH_CHECK(!(relu && want_dres && !yp), "bn_act_bwd: residual + ReLU needs the saved output");
   const long long C = x.size(1), M = x.numel() / C;
   auto dx = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
-  auto dw = at::empty({C}, w.options()), db = at::empty({C}, w.options());
+  // dw_into/db_into: the parameters' fp32 .grad (flat arena) — accumulated in place
+  const bool into = dw_into && dw_into->defined() && db_into && db_into->defined();
+  at::Tensor dw, db;
+  if (into) {
+    CHECK_F32((*dw_into)); CHECK_F32((*db_into));
+    TORCH_CHECK(dw_into->numel() == C && db_into->numel() == C && dw_into->is_contiguous() && db_into->is_contiguous());
+    dw = *dw_into;
+    db = *db_into;
+  } else {
+    dw = at::empty({C}, w.options());
+    db = at::empty({C}, w.options());
+  }
   auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_floats(M, C)}, w.options());
-  CHECK_RC(pdo::bn_bwd(bp(dyc), bp(y), bp(x), fp(mean), fp(invstd), fp(w), M, (int)C, relu ? 1 : 0, bp(dx),
-                       want_dres ? bp(dres) : nullptr, fp(dw), fp(db), fp(scratch), cur_stream()), "bn_bwd");
+  CHECK_RC(pdo::bn_bwd(bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M, (int)C, relu ? 1 : 0, bp(dx),
+                       want_dres ? bp(dres) : nullptr, fp(dw), fp(db), into ? 1 : 0, fp(scratch), cur_stream()),
+           "bn_bwd");
+  if (into) return {dx, dres, at::Tensor(), at::Tensor()};
   return {dx, dres, dw, db};
+}
+
+// ---------------------------------------------------------------- NHWC max-pool 3×3/2
+std::vector<at::Tensor> maxpool3s2_fwd(at::Tensor x) {
+  CHECK_BF16(x);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
+              "maxpool3s2_fwd: channels_last bf16 input with C % 8 == 0");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, OH, OW}, x.options(), at::MemoryFormat::ChannelsLast);
+  auto arg = at::empty({N, C, OH, OW}, x.options().dtype(at::kByte), at::MemoryFormat::ChannelsLast);
+  CHECK_RC(pdo::maxpool3s2_fwd(bp(x), (int)N, (int)H, (int)W, (int)C, bp(y), arg.data_ptr<uint8_t>(), cur_stream()),
+           "maxpool3s2_fwd");
+  return {y, arg};
+}
+
+at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W) {
+  CHECK_BF16(dy);
+  auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(arg.scalar_type() == at::kByte && arg.sizes() == dy.sizes() &&
+              arg.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool3s2_bwd: arg");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1, "maxpool3s2_bwd: input size");
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  CHECK_RC(pdo::maxpool3s2_bwd(bp(dyc), arg.data_ptr<uint8_t>(), (int)N, (int)H, (int)W, (int)C, bp(dx),
+                               cur_stream()), "maxpool3s2_bwd");
+  return dx;
 }
 
 // ---------------------------------------------------------------- attention
@@ -439,6 +488,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("splitk_add", &splitk_add);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
+  m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("linear_gelu", &linear_gelu);
   m.def("lt_last_error", [] { return std::string(pdo::lt_last_error()); });
   // raw probe: epilogue id on D[m,n] = op(A)op(B) with optional bias/aux (diagnostics)

@@ -34,8 +34,13 @@ int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float
            long long M, int C, float eps, float momentum, int relu, bf16* y, float* mean, float* invstd,
            float* scratch, hipStream_t st);
 int bn_bwd_scratch_floats(long long M, int C);
+// y may be null: the ReLU mask is then recomputed from x (only valid without a residual)
 int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, const float* invstd, const float* w,
-           long long M, int C, int relu, bf16* dx, bf16* dres, float* dw, float* db, float* scratch, hipStream_t st);
+           const float* b, long long M, int C, int relu, bf16* dx, bf16* dres, float* dw, float* db, int accumulate,
+           float* scratch, hipStream_t st);
+// ResNet stem max-pool 3×3/2 pad 1, NHWC bf16 (pool.hip); arg = uint8 window position
+int maxpool3s2_fwd(const bf16* x, int N, int H, int W, int C, bf16* y, uint8_t* arg, hipStream_t st);
+int maxpool3s2_bwd(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, bf16* dx, hipStream_t st);
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 
 // gelu.hip

@@ -74,7 +74,7 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         x = ops.bn_act(self.bn1, self.conv1(x))
-        x = F.max_pool2d(x, 3, 2, 1)
+        x = ops.max_pool_3x3s2(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

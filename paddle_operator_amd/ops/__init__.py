@@ -462,22 +462,35 @@ def embedding(idx, wte, wpe):
 # ----------------------------------------------------------------------------
 
 class _BNActFn(torch.autograd.Function):
-    """y = act(BN(x) [+ residual]) with batch statistics (csrc/hip/batchnorm.hip)."""
+    """y = act(BN(x) [+ residual]) with batch statistics (csrc/hip/batchnorm.hip).
+
+    Without a residual the backward recomputes the ReLU mask from x, so only
+    x (the conv output autograd keeps anyway) and two [C] vectors are saved."""
 
     @staticmethod
     def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu):
         m = _native.require_hip()
         y, mean, invstd = m.bn_act_fwd(x, residual, w, b, running_mean, running_var, eps, momentum, relu)
-        ctx.save_for_backward(x, y, mean, invstd, w)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        keep_y = relu and ctx.has_res
+        ctx.save_for_backward(x, y if keep_y else None, mean, invstd, w, b)
+        ctx.params = (w, b)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         m = _native.require_hip()
-        x, y, mean, invstd, w = ctx.saved_tensors
-        dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, ctx.relu, ctx.has_res)
+        x, y, mean, invstd, w, b = ctx.saved_tensors
+        pw, pb = ctx.params
+        # gamma/beta gradients straight into the flat arena when allowed
+        direct = _direct_ok(pw) and _direct_ok(pb) and pw.grad.dtype == torch.float32
+        dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, ctx.relu, ctx.has_res,
+                                        pw.grad if direct else None, pb.grad if direct else None)
+        if direct:
+            pw._pdo_ready(pw)
+            pb._pdo_ready(pb)
+            dw = db = None
         return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None
 
 
@@ -501,3 +514,27 @@ def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
+
+
+class _MaxPool3s2Fn(torch.autograd.Function):
+    """3×3 / stride 2 / pad 1 max-pool, NHWC bf16 (csrc/hip/pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y, arg = _native.require_hip().maxpool3s2_fwd(x)
+        ctx.save_for_backward(arg)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        return _native.require_hip().maxpool3s2_bwd(dy, arg, *ctx.hw)
+
+
+def max_pool_3x3s2(x):
+    """ResNet stem pool; HIP gather-backward kernel for channels_last bf16."""
+    if (use_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return _MaxPool3s2Fn.apply(x)
+    return F.max_pool2d(x, 3, 2, 1)

@@ -342,7 +342,8 @@ def test_fused_mlp_epilogues(cuda, T, C):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,C,H,relu,res", [(8, 64, 28, True, False), (4, 256, 14, True, True),
-                                              (16, 128, 7, False, False), (2, 2048, 7, True, True)])
+                                              (16, 128, 7, False, False), (2, 2048, 7, True, True),
+                                              (4, 24, 9, True, False), (3, 40, 5, True, True)])
 def test_bn_act_nhwc(cuda, N, C, H, relu, res):
     """Fused NHWC BatchNorm(+residual)(+ReLU) vs fp32 PyTorch, incl. running stats."""
     ops = _ops()
@@ -378,3 +379,22 @@ def test_bn_act_nhwc(cuda, N, C, H, relu, res):
         assert rel_err(r.grad, rf.grad) < 2e-2
     assert rel_err(bn.running_mean, bnf.running_mean) < 1e-3
     assert rel_err(bn.running_var, bnf.running_var) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,H,W", [(4, 64, 112, 112), (2, 16, 9, 7), (3, 8, 2, 5)])
+def test_maxpool3s2_nhwc(cuda, N, C, H, W):
+    """HIP 3×3/2 max-pool (fwd value + gather backward) vs fp32 PyTorch."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(N, C, H, W, device=cuda, generator=g).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+    y = ops.max_pool_3x3s2(x)
+    xf = x.detach().float().requires_grad_()
+    yf = torch.nn.functional.max_pool2d(xf, 3, 2, 1)
+    assert y.shape == yf.shape
+    assert torch.equal(y.float(), yf)
+    dy = torch.randn(y.shape, device=cuda, generator=g).bfloat16()
+    y.backward(dy)
+    yf.backward(dy.float())
+    assert rel_err(x.grad, xf.grad) < 1e-2

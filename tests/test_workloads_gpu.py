@@ -37,3 +37,33 @@ def test_launcher_gpt2_single_gpu(cuda, tmp_path):
     done = [json.loads(l[9:]) for l in out.stdout.splitlines() if l.startswith("PDO_DONE ")]
     assert done and done[0]["steps"] == 3
     assert os.path.exists(tmp_path / "ck" / "ckpt-00000003.pt")
+
+
+@pytest.mark.gpu
+def test_resnet_arena_grads_match_autograd(cuda):
+    """BN γ/β gradients written straight into the flat arena by the HIP backward
+    (ops.bn_act direct path) equal autograd's accumulated gradients."""
+    import copy
+
+    from paddle_operator_amd.models.resnet import resnet18_like_tiny
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    a = resnet18_like_tiny().to("cuda").to(memory_format=torch.channels_last)
+    for m in a.modules():  # non-zero γ so every gradient path is exercised
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+    b = copy.deepcopy(a)
+    flat = FlatParams(a, dtype=torch.float32, device="cuda")
+    x = torch.randn(8, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    flat.zero_grad()
+    for m in (a, b):
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(x)
+        torch.nn.functional.cross_entropy(out.float(), y).backward()
+    torch.cuda.synchronize()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert pa.grad.data_ptr() >= flat.grads.data_ptr(), n
+        err = (pa.grad.float() - pb.grad.float()).norm() / (pb.grad.float().norm() + 1e-12)
+        assert err < 1e-5, f"{n}: {err}"
