@@ -20,24 +20,28 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def free_port_block(n=40):
-    """A base port p with p..p+n free (best effort)."""
-    for _ in range(50):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        p = s.getsockname()[1]
-        s.close()
-        if p + n < 65000:
-            ok = True
-            for q in range(p, p + n, 7):
-                t = socket.socket()
-                try:
-                    t.bind(("127.0.0.1", q))
-                except OSError:
-                    ok = False
-                finally:
-                    t.close()
-            if ok:
-                return p
+    """A base port p with p..p+n free (best effort).
+
+    Drawn below the kernel's ephemeral range (32768+) so that client sockets
+    of concurrently running tests (pytest-xdist) cannot land inside the block
+    between this probe and the launcher's bind."""
+    import random
+    rng = random.Random(os.getpid() ^ time.time_ns())
+    for _ in range(200):
+        p = rng.randrange(12000, 32000 - n)
+        ok = True
+        for q in range(p, p + n):
+            t = socket.socket()
+            try:
+                t.bind(("127.0.0.1", q))
+            except OSError:
+                ok = False
+            finally:
+                t.close()
+            if not ok:
+                break
+        if ok:
+            return p
     raise RuntimeError("no free port block")
 
 
