@@ -209,6 +209,14 @@ void splitk_add(at::Tensor part, at::Tensor out, bool accumulate) {
            "splitk_add");
 }
 
+at::Tensor transpose(at::Tensor x) {
+  CHECK_IN(x); CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R, C] with R, C % 64 == 0");
+  auto y = at::empty({x.size(1), x.size(0)}, x.options());
+  CHECK_RC(pdo::transpose_bf16(bp(x), bp(y), (int)x.size(0), (int)x.size(1), cur_stream()), "transpose");
+  return y;
+}
+
 // ---------------------------------------------------------------- hipBLASLt fused MLP epilogues
 constexpr int kEpiGeluAuxBias = 164;  // HIPBLASLT_EPILOGUE_GELU_AUX_BIAS
 constexpr int kEpiDGeluBGrad = 208;   // HIPBLASLT_EPILOGUE_DGELU_BGRAD
@@ -486,6 +494,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("sumsq", &sumsq);
   m.def("adamw_flat", &adamw_flat);
   m.def("splitk_add", &splitk_add);
+  m.def("transpose", &transpose);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);

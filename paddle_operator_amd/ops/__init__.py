@@ -205,15 +205,29 @@ def _input_grad(dy2, w):
 
     hipBLASLt's gfx950 kernels for the "NN" layout of dY·W reach 1.1-1.3 PF on
     these shapes, the forward's "TN" family 1.35-1.9 PF (tuned tables).  The
-    explicit Wᵀ copy is ≤ 8 M elements per projection (≈10 µs)."""
+    explicit Wᵀ copy is ≤ 8 M elements per projection; it runs in the LDS-tiled
+    HIP transpose (csrc/hip/transpose.hip) at the HBM rate — PyTorch's strided
+    copy took ≈25 µs per projection weight, 2.4 ms per GPT-2-medium step."""
     if _DX_TN[0] and dy2.is_cuda:
-        return F.linear(dy2, w.t().contiguous())
+        return F.linear(dy2, transpose(w))
     return dy2 @ w
+
+
+def transpose(w):
+    """Contiguous Wᵀ of a 2-D tensor (HIP kernel for bf16 with 64-multiple dims)."""
+    if (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] % 64 == 0
+            and w.shape[1] % 64 == 0 and w.is_contiguous()):
+        return _native.require_hip().transpose(w)
+    return w.t().contiguous()
 
 
 def _weight_grad(w, dy2, x2):
     """dW = dy2ᵀ·x2.  Straight into the flat arena when the parameter allows it
-    (returns None), else as a tensor for autograd to accumulate."""
+    (returns None), else as a tensor for autograd to accumulate.
+
+    (A/B on 1×MI355X: issuing these GEMMs on a side HIP stream to overlap the
+    memory-bound backward kernels gained nothing — 394.5k vs 394.7k tok/s — and
+    stalled one run on cross-stream allocator reuse; they stay in-stream.)"""
     Fo, K = dy2.shape[1], x2.shape[1]
     if not _direct_ok(w):
         return dy2.t() @ x2

@@ -81,6 +81,15 @@ def test_add_layernorm(cuda, N, C, with_rb):
         assert rel_err(rb.grad, rbf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("R,C", [(64, 64), (1024, 4096), (4096, 1024), (50304, 1024), (192, 320)])
+def test_transpose(cuda, R, C):
+    ops = _ops()
+    x = torch.randn(R, C, device=cuda).bfloat16()
+    y = ops.transpose(x)
+    assert y.shape == (C, R) and y.is_contiguous()
+    assert torch.equal(y, x.t())  # a permutation: bitwise
+
+
 @pytest.mark.parametrize("N,F", [(16384, 3072), (100, 1024)])
 def test_bias_grad_and_linear(cuda, N, F):
     ops = _ops()
