@@ -20,6 +20,9 @@
 // LDS tiles are [64 rows][64 bf16] with one XOR swizzle of the 16-B chunk
 // index, chosen so BOTH the row reads (ds_read_b128, 16 rows per lane group)
 // and the transposed reads (4 rows × 64 B per half-wave) are conflict-free.
+// The forward's V tile is only read transposed and uses a swizzle that repeats
+// every 8 rows, so its fragment addresses are per-lane constants plus
+// ds_read immediates (toff_v; 1.6 % on the forward, bitwise-identical output).
 #include <math.h>
 
 #include "common.h"
@@ -122,15 +125,47 @@ __device__ __forceinline__ void store_acc_rows(bf16* dst_row, const f32x16& acc,
 // ============================================================================
 // forward
 // ============================================================================
+// ----- V tile: a transposed-read-only swizzle -----
+// V is only ever read transposed (ds_read_b64_tr_b16, 4 rows × 64 B per
+// 32-lane half).  Rows r and r+2 share banks, so the 16-B chunk index is XORed
+// with 4·bit1(r) only: a row's swizzle then repeats every 8 rows, every
+// transposed fragment of the tile is ONE per-lane base address (two: V columns
+// 0-31 / 32-63) plus a compile-time row offset, i.e. a ds_read immediate — no
+// per-tile address arithmetic.  K keeps the row-read swizzle (toff).
+__device__ __forceinline__ int toff_v(int r, int ch) { return r * HD + ((ch ^ (((r >> 1) & 1) << 2)) << 3); }
+
+__device__ __forceinline__ void stage_store_v(const Stage& st, bf16* T, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *reinterpret_cast<bf16x8*>(T + toff_v(r, ch)) = st.v[i];
+  }
+}
+
+// per-lane element offset of the tr fragment rows k0 = 0 (lo) for V columns cbase
+__device__ __forceinline__ int tr_base_v(int cbase, int lane) {
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  const int col = cbase + 16 * (g & 1) + 4 * p;
+  const int r0 = 4 * (g >> 1) + q;
+  return toff_v(r0, col >> 3) + (col & 7);
+}
+
+template <int K0>
+__device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Tlane + K0 * HD));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Tlane + (K0 + 8) * HD));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                    float* __restrict__ lse, int B, int S, int H, float c2) {
+                                                     float* __restrict__ lse, int B, int S, int H, float c2) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   const int bh = blockIdx.x % (B * H);
   const int qb = nqb - 1 - blockIdx.x / (B * H);  // heaviest query blocks first
   const int b = bh / H, h = bh % H;
-  const size_t rs = (size_t)3 * H * HD;  // row stride (elements) between positions
+  const size_t rs = (size_t)3 * H * HD;
   const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
   const bf16* kbase = qbase + (size_t)H * HD;
   const bf16* vbase = qbase + (size_t)2 * H * HD;
@@ -141,6 +176,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
   for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
   retire(qf);
 
+  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
   f32x16 o0 = zero16(), o1 = zero16();
   float m = -INFINITY, l = 0.f;
   const int ntiles = (qb * 128 + 128) / TROWS;
@@ -150,7 +186,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
   stage_load(sk, kbase, rs, 0, tid);
   stage_load(sv, vbase, rs, 0, tid);
   stage_store(sk, smem, tid);
-  stage_store(sv, smem + TROWS * HD, tid);
+  stage_store_v(sv, smem + TROWS * HD, tid);
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
@@ -169,25 +205,20 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
         s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
       }
-      const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
-      // VALU diet (D=64 forward is VALU-bound, not MFMA-bound): mask and max
-      // on the raw scores (c2 > 0 commutes with max), then ONE fma + v_exp
-      // per element and packed row-sum adds
-      if (diag) {
+      if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
+        // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
+        const int d = q - key0 - 4 * hh;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (key0 + kr > q) s0[r] = -INFINITY;
-          if (key0 + 32 + kr > q) s1[r] = -INFINITY;
+          const int c = (r & 3) + 8 * (r >> 2);
+          s0[r] = c > d ? -INFINITY : s0[r];
+          s1[r] = c + 32 > d ? -INFINITY : s1[r];
         }
       }
       float tmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
-      // deferred rescale: keep a stale running max unless it grows by more
-      // than 2^8 (P ≤ 256 stays exact enough in bf16, fp32 accumulation), so
-      // after the first tiles the O/l rescale is skipped wave-uniformly
       const bool grow = tmax > m + 8.f;
       if (__any(grow)) {
         const float mn = grow ? fmaxf(m, tmax) : m;
@@ -208,19 +239,27 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
       }
       l += ls2[0] + ls2[1];
-#pragma unroll
-      for (int sst = 0; sst < 2; ++sst) {
-        const bf16x8 p0 = pack8(s0, sst), p1 = pack8(s1, sst);
-        o0 = mfma(tr_frag(Vt, 16 * sst, 0, lane), p0, o0);
-        o1 = mfma(tr_frag(Vt, 16 * sst, 32, lane), p0, o1);
-        o0 = mfma(tr_frag(Vt, 32 + 16 * sst, 0, lane), p1, o0);
-        o1 = mfma(tr_frag(Vt, 32 + 16 * sst, 32, lane), p1, o1);
+      const bf16* V0 = Vt + vb0;
+      const bf16* V1 = Vt + vb1;
+      {
+        const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
+        o0 = mfma(tr_frag_v<0>(V0), p0, o0);
+        o1 = mfma(tr_frag_v<0>(V1), p0, o1);
+        o0 = mfma(tr_frag_v<32>(V0), p1, o0);
+        o1 = mfma(tr_frag_v<32>(V1), p1, o1);
+      }
+      {
+        const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
+        o0 = mfma(tr_frag_v<16>(V0), p0, o0);
+        o1 = mfma(tr_frag_v<16>(V1), p0, o1);
+        o0 = mfma(tr_frag_v<48>(V0), p1, o0);
+        o1 = mfma(tr_frag_v<48>(V1), p1, o1);
       }
     }
     if (more) {
       bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
       stage_store(sk, Kn, tid);
-      stage_store(sv, Kn + TROWS * HD, tid);
+      stage_store_v(sv, Kn + TROWS * HD, tid);
     }
     __syncthreads();
   }
