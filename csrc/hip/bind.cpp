@@ -63,8 +63,12 @@ std::vector<at::Tensor> add_layernorm_fwd(at::Tensor x, at::Tensor r, at::Tensor
   return {h, y, mean, rstd};
 }
 
+// grads (optional): destination tensors for dgamma, dbeta (, drbias) — e.g. the
+// parameters' slices of the flat gradient arena — accumulated in place; the
+// result then holds dx only
 std::vector<at::Tensor> ln_bwd_impl(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
-                                    c10::optional<at::Tensor> dres, bool rbias) {
+                                    c10::optional<at::Tensor> dres, bool rbias,
+                                    c10::optional<std::vector<at::Tensor>> grads) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(w); CHECK_IN(mean); CHECK_IN(rstd);
   CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(w); CHECK_F32(mean); CHECK_F32(rstd);
   TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && w.numel() == x.size(1));
@@ -80,20 +84,38 @@ std::vector<at::Tensor> ln_bwd_impl(at::Tensor dy, at::Tensor x, at::Tensor w, a
   const int G = pdo::layernorm_bwd_grid(N);
   const int NA = rbias ? 3 : 2;
   auto part = at::empty({G * NA * C + pdo::colsum_scratch_floats(G, NA * C)}, x.options().dtype(at::kFloat));
-  auto out = at::empty({NA, C}, w.options());
+  pdo::ColOut co;
+  co.seg = C;
+  at::Tensor out;
+  if (grads.has_value()) {
+    TORCH_CHECK((int)grads->size() == NA, "layernorm_bwd: need ", NA, " gradient destinations");
+    for (int i = 0; i < NA; ++i) {
+      const at::Tensor& g = (*grads)[i];
+      CHECK_IN(g); CHECK_BF16(g);
+      TORCH_CHECK(g.numel() == C);
+      co.p[i] = bp(g);
+    }
+    co.acc = 1;
+  } else {
+    out = at::empty({NA, C}, w.options());
+    for (int i = 0; i < NA; ++i) co.p[i] = bp(out) + (size_t)i * C;
+  }
   CHECK_RC(pdo::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), dr, bp(dx), fp(part),
-                              fp(part) + (size_t)G * NA * C, bp(out), rbias, N, C, cur_stream()), "layernorm_bwd");
+                              fp(part) + (size_t)G * NA * C, co, rbias, N, C, cur_stream()), "layernorm_bwd");
+  if (grads.has_value()) return {dx};
   if (rbias) return {dx, out[0], out[1], out[2]};
   return {dx, out[0], out[1]};
 }
 
-std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd) {
-  return ln_bwd_impl(dy, x, w, mean, rstd, c10::nullopt, false);
+std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
+                                      c10::optional<std::vector<at::Tensor>> grads) {
+  return ln_bwd_impl(dy, x, w, mean, rstd, c10::nullopt, false, grads);
 }
 
 std::vector<at::Tensor> layernorm_bwd_add(at::Tensor dy, at::Tensor h, at::Tensor w, at::Tensor mean,
-                                          at::Tensor rstd, at::Tensor dres, bool rbias) {
-  return ln_bwd_impl(dy, h, w, mean, rstd, dres, rbias);
+                                          at::Tensor rstd, at::Tensor dres, bool rbias,
+                                          c10::optional<std::vector<at::Tensor>> grads) {
+  return ln_bwd_impl(dy, h, w, mean, rstd, dres, rbias, grads);
 }
 
 // ---------------------------------------------------------------- bias + gelu
@@ -105,7 +127,8 @@ at::Tensor bias_gelu_fwd(at::Tensor x, at::Tensor b) {
   return y;
 }
 
-std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b) {
+// db_out (optional): accumulate the bias gradient there (arena slice); returns {dx} then
+std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b, c10::optional<at::Tensor> db_out) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(b); CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(b);
   TORCH_CHECK(x.dim() == 2 && dy.sizes() == x.sizes() && b.numel() == x.size(1));
   const long long N = x.size(0);
@@ -113,21 +136,36 @@ std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b)
   auto dx = at::empty_like(x);
   const int G = pdo::bias_gelu_bwd_groups(N, F);
   auto part = at::empty({(int64_t)G * F + pdo::colsum_scratch_floats(G, F)}, x.options().dtype(at::kFloat));
-  auto db = at::empty_like(b);
+  at::Tensor db;
+  if (db_out.has_value()) {
+    db = *db_out;
+    CHECK_IN(db); CHECK_BF16(db);
+    TORCH_CHECK(db.numel() == F);
+  } else {
+    db = at::empty_like(b);
+  }
   CHECK_RC(pdo::bias_gelu_bwd(bp(dy), bp(x), bp(b), bp(dx), fp(part), fp(part) + (size_t)G * F, bp(db), N, F,
-                              cur_stream()), "bias_gelu_bwd");
+                              cur_stream(), db_out.has_value() ? 1 : 0), "bias_gelu_bwd");
+  if (db_out.has_value()) return {dx};
   return {dx, db};
 }
 
-// db = colsum(dy) for a [N, F] bf16 gradient
-at::Tensor bias_grad(at::Tensor dy) {
+// db = colsum(dy) for a [N, F] bf16 gradient; with `out`, accumulated into it
+at::Tensor bias_grad(at::Tensor dy, c10::optional<at::Tensor> out) {
   CHECK_IN(dy); CHECK_BF16(dy);
   TORCH_CHECK(dy.dim() == 2);
   const long long N = dy.size(0);
   const int F = dy.size(1);
   auto scratch = at::empty({pdo::bias_grad_scratch_floats(N, F)}, dy.options().dtype(at::kFloat));
-  auto db = at::empty({F}, dy.options());
-  CHECK_RC(pdo::bias_grad(bp(dy), N, F, bp(db), fp(scratch), cur_stream()), "bias_grad");
+  at::Tensor db;
+  if (out.has_value()) {
+    db = *out;
+    CHECK_IN(db); CHECK_BF16(db);
+    TORCH_CHECK(db.numel() == F);
+  } else {
+    db = at::empty({F}, dy.options());
+  }
+  CHECK_RC(pdo::bias_grad(bp(dy), N, F, bp(db), fp(scratch), cur_stream(), out.has_value() ? 1 : 0), "bias_grad");
   return db;
 }
 
@@ -253,7 +291,7 @@ std::vector<at::Tensor> matmul_dgelu(at::Tensor dy, at::Tensor w2, at::Tensor h_
     rc = pdo::lt_matmul(dy.get_device(), kEpiDGelu, 0, 0, N, T, N2, bp(w2), N, bp(dy), N2, bp(dh), N, nullptr, 0,
                         h_pre.data_ptr(), N, ws.data_ptr(), kLtWorkspace, cur_stream());
     if (rc != 0) return {};
-    db = bias_grad(dh);
+    db = bias_grad(dh, c10::nullopt);
   }
   return {dh, db};
 }
@@ -482,11 +520,13 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("add_layernorm_fwd", &add_layernorm_fwd, py::arg("x"), py::arg("r"), py::arg("w"), py::arg("b"),
         py::arg("eps"), py::arg("rbias") = py::none());
-  m.def("layernorm_bwd", &layernorm_bwd);
-  m.def("layernorm_bwd_add", &layernorm_bwd_add);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"),
+        py::arg("rstd"), py::arg("grads") = py::none());
+  m.def("layernorm_bwd_add", &layernorm_bwd_add, py::arg("dy"), py::arg("h"), py::arg("w"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dres"), py::arg("rbias"), py::arg("grads") = py::none());
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
-  m.def("bias_grad", &bias_grad);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("b"), py::arg("db_out") = py::none());
+  m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out") = py::none());
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("embed_fwd", &embed_fwd);

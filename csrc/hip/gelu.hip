@@ -86,12 +86,14 @@ int bias_gelu_bwd_groups(long long N, int F) {
 }
 
 int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, float* scratch, bf16* db,
-                  long long N, int F, hipStream_t st) {
+                  long long N, int F, hipStream_t st, int accumulate) {
   if (F % 8) return -2;
   const int gx = (F / 8 + 255) / 256;
   const int gy = bias_gelu_bwd_groups(N, F);
   bias_gelu_bwd_kernel<<<dim3(gx, gy), 256, 0, st>>>(dy, x, b, dx, part, (int)N, F);
-  colsum(part, gy, F, F, db, scratch, st);
+  ColOut co = ColOut::one(db, F);
+  co.acc = accumulate;
+  colsum(part, gy, F, F, co, scratch, st);
   return 0;
 }
 

@@ -10,19 +10,35 @@
 namespace pdo {
 typedef __bf16 bf16;
 
+// Destination of a column sum: columns [k·seg, (k+1)·seg) go to p[k] (≤ 3
+// segments, seg % 4 == 0); acc = add into the existing bf16 values.
+struct ColOut {
+  bf16* p[3] = {nullptr, nullptr, nullptr};
+  int seg = 1 << 30;
+  int acc = 0;
+  static ColOut one(bf16* o, int C) {
+    ColOut c;
+    c.p[0] = o;
+    c.seg = C;
+    return c;
+  }
+};
+
 // layernorm.hip
 int layernorm_fwd(const bf16* x, const bf16* r, const bf16* rb, const bf16* w, const bf16* b, bf16* h, bf16* y,
                   float* mean, float* rstd, int N, int C, float eps, hipStream_t st);
 int layernorm_bwd_grid(int N);
+// out: where dgamma | dbeta | (drbias) go (ColOut segments of C columns)
 int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
-                  const bf16* dres, bf16* dx, float* part, float* scratch, bf16* out, bool rbias, int N, int C,
-                  hipStream_t st);
+                  const bf16* dres, bf16* dx, float* part, float* scratch, const ColOut& out, bool rbias, int N,
+                  int C, hipStream_t st);
 
 // reduce.hip
 int colsum_scratch_floats(int G, int C);
 void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st);
+void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* scratch, hipStream_t st);
 int bias_grad_scratch_floats(long long N, int F);
-int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st);
+int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st, int accumulate = 0);
 // hipBLASLt column-major matmul with epilogue (blaslt.hip); <0 = no solution
 int lt_matmul(int dev, int epi, int ta, int tb, long long m, long long n, long long k, const bf16* A, long long lda,
               const bf16* B, long long ldb, bf16* D, long long ldd, const void* bias, int bias_is_f32, void* aux,
@@ -49,7 +65,7 @@ int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, 
 int bias_gelu_fwd(const bf16* x, const bf16* b, bf16* y, long long N, int F, hipStream_t st);
 int bias_gelu_bwd_groups(long long N, int F);
 int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float* part, float* scratch, bf16* db,
-                  long long N, int F, hipStream_t st);
+                  long long N, int F, hipStream_t st, int accumulate = 0);
 
 // xent.hip
 int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,

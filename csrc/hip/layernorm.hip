@@ -200,13 +200,14 @@ int layernorm_bwd_grid(int N) {
   return g;
 }
 
-// out: bf16 [NA*C] = dgamma | dbeta | (drbias); part: [grid][NA*C] f32;
+// out: dgamma | dbeta | (drbias) as C-column segments; part: [grid][NA*C] f32;
 // scratch: colsum_scratch_floats(grid, NA*C)
 int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
-                  const bf16* dres, bf16* dx, float* part, float* scratch, bf16* out, bool rbias, int N, int C,
-                  hipStream_t st) {
+                  const bf16* dres, bf16* dx, float* part, float* scratch, const ColOut& out, bool rbias, int N,
+                  int C, hipStream_t st) {
   if (C % 8 != 0 || C > 4096) return -2;
   if (rbias && !dres) return -4;
+  if (out.seg != C) return -5;
   const int grid = layernorm_bwd_grid(N);
   const int vpl = vpl_for(C);
   if (vpl > 4) return -3;  // register/LDS budget of the in-block combine

@@ -15,7 +15,7 @@ namespace pdo {
 constexpr int RPB = 64;  // rows per level-1 workgroup
 
 __global__ __launch_bounds__(512) void colsum_f32_pass(const float* __restrict__ in, int G, int C, int ld, int rpb,
-                                                       float* __restrict__ out_part, bf16* __restrict__ out_bf16) {
+                                                       float* __restrict__ out_part, ColOut co) {
   __shared__ f32x4 red[8][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = (blockIdx.x * 64 + lane) * 4;
@@ -32,9 +32,17 @@ __global__ __launch_bounds__(512) void colsum_f32_pass(const float* __restrict__
     f32x4 t = red[0][lane];
 #pragma unroll
     for (int i = 1; i < 8; ++i) t += red[i][lane];
-    if (out_bf16) {
+    if (co.p[0]) {
+      // segment k of `co.seg` columns goes to co.p[k] (e.g. straight into the
+      // parameters' slices of the flat gradient arena), optionally accumulated
+      const int k = col / co.seg, c = col - k * co.seg;
+      bf16* dst = co.p[k] + c;
+      if (co.acc) {
+        const bf16x4 old = *reinterpret_cast<const bf16x4*>(dst);
+        t += f32x4{(float)old[0], (float)old[1], (float)old[2], (float)old[3]};
+      }
       bf16x4 o = {(bf16)t[0], (bf16)t[1], (bf16)t[2], (bf16)t[3]};
-      *reinterpret_cast<bf16x4*>(out_bf16 + col) = o;
+      *reinterpret_cast<bf16x4*>(dst) = o;
     } else {
       *reinterpret_cast<f32x4*>(out_part + (size_t)blockIdx.y * C + col) = t;
     }
@@ -68,15 +76,19 @@ __global__ __launch_bounds__(512) void colsum_bf16_pass(const bf16* __restrict__
 int colsum_scratch_floats(int G, int C) { return ((G + RPB - 1) / RPB) * C; }
 
 // part: [G][ld] f32 (first C columns used).  scratch: colsum_scratch_floats(G, C)
-void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st) {
+void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* scratch, hipStream_t st) {
   const int gx = (C / 4 + 63) / 64;
   if (G <= RPB) {
     colsum_f32_pass<<<dim3(gx, 1), 512, 0, st>>>(part, G, C, ld, RPB, nullptr, out);
     return;
   }
   const int gs = (G + RPB - 1) / RPB;
-  colsum_f32_pass<<<dim3(gx, gs), 512, 0, st>>>(part, G, C, ld, RPB, scratch, nullptr);
+  colsum_f32_pass<<<dim3(gx, gs), 512, 0, st>>>(part, G, C, ld, RPB, scratch, ColOut{});
   colsum_f32_pass<<<dim3(gx, 1), 512, 0, st>>>(scratch, gs, C, C, gs, nullptr, out);
+}
+
+void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st) {
+  colsum(part, G, C, ld, ColOut::one(out, C), scratch, st);
 }
 
 int bias_grad_scratch_floats(long long N, int F) {
@@ -84,14 +96,16 @@ int bias_grad_scratch_floats(long long N, int F) {
   return gs * F;
 }
 
-// db[f] = Σ_n dy[n][f]  (bf16 in, bf16 out); scratch: bias_grad_scratch_floats
-int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st) {
+// db[f] (+)= Σ_n dy[n][f]  (bf16 in, bf16 out); scratch: bias_grad_scratch_floats
+int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st, int accumulate) {
   if (F % 8) return -2;
   const int gx = (F / 8 + 63) / 64;
   const int gs = (int)((N + 255) / 256);
   colsum_bf16_pass<<<dim3(gx, gs), 512, 0, st>>>(dy, (int)N, F, 256, scratch);
   const int gx2 = (F / 4 + 63) / 64;
-  colsum_f32_pass<<<dim3(gx2, 1), 512, 0, st>>>(scratch, gs, F, F, gs, nullptr, db);
+  ColOut co = ColOut::one(db, F);
+  co.acc = accumulate;
+  colsum_f32_pass<<<dim3(gx2, 1), 512, 0, st>>>(scratch, gs, F, F, gs, nullptr, co);
   return 0;
 }
 

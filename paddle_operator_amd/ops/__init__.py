@@ -85,12 +85,18 @@ class _LayerNormFn(torch.autograd.Function):
         y, mean, rstd = m.layernorm_fwd(x2, w, b, eps)
         ctx.save_for_backward(x2, w, mean, rstd)
         ctx.shape = x.shape
+        ctx.params = (w, b)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         m = _native.require_hip()
         x2, w, mean, rstd = ctx.saved_tensors
+        gd = _arena_grads(ctx.params)
+        if gd is not None:
+            (dx,) = m.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, w, mean, rstd, grads=gd)
+            _signal_ready(ctx.params)
+            return dx.view(ctx.shape), None, None, None
         dx, dw, db = m.layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, w, mean, rstd)
         return dx.view(ctx.shape), dw, db, None
 
@@ -118,14 +124,20 @@ class _AddLayerNormFn(torch.autograd.Function):
         ctx.save_for_backward(h, w, mean, rstd)
         ctx.shape = x.shape
         ctx.has_rbias = rbias is not None
+        ctx.params = (w, b, rbias) if rbias is not None else (w, b)
         return h.view(x.shape), y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dh, dy):
         m = _native.require_hip()
         h, w, mean, rstd = ctx.saved_tensors
+        gd = _arena_grads(ctx.params)
         outs = m.layernorm_bwd_add(dy.reshape(h.shape).contiguous(), h, w, mean, rstd,
-                                   dh.reshape(h.shape).contiguous(), ctx.has_rbias)
+                                   dh.reshape(h.shape).contiguous(), ctx.has_rbias, grads=gd)
+        if gd is not None:
+            _signal_ready(ctx.params)
+            dx = outs[0].view(ctx.shape)
+            return dx, dx, None, None, None, None
         dx = outs[0].view(ctx.shape)
         drb = outs[3] if ctx.has_rbias else None
         return dx, dx, outs[1], outs[2], drb, None
@@ -170,7 +182,14 @@ class _LinearFn(torch.autograd.Function):
         dw = _weight_grad(w, dy2, x2) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = _native.require_hip().bias_grad(dy2.contiguous()) if use_hip(dy2) else dy2.float().sum(0).to(dy.dtype)
+            if use_hip(dy2):
+                gd = _arena_grads((ctx.b,))
+                db = _native.require_hip().bias_grad(dy2.contiguous(), out=gd[0] if gd else None)
+                if gd is not None:
+                    _signal_ready((ctx.b,))
+                    db = None
+            else:
+                db = dy2.float().sum(0).to(dy.dtype)
         return dx, dw, db
 
 
@@ -187,10 +206,15 @@ def _workspace(device, numel):
 
 
 def _splitk(tokens: int, m: int, n: int) -> int:
-    """Token-slice count for dW = dY^T X: aim for ≥256 output tiles of 256² (one per CU)."""
+    """Token-slice count for dW = dY^T X: aim for ≥256 output tiles of 256² (one per CU).
+
+    The LM-head dW (50304×1024 → 786 tiles, K = 65536) is past that target but
+    still runs 6-8 % faster as 4 token slices (tools/dw_probe.py, tuned)."""
     if tokens < 8192 or os.environ.get("PDO_SPLITK", "1") == "0":
         return 1
     tiles = max(1, (m * n) // 65536)
+    if 256 <= tiles < 2048:
+        return 4 if tokens >= 32768 and tokens % 4 == 0 else 1
     s = 1
     while s < 8 and tiles * s < 256 and tokens % (2 * s) == 0 and tokens // (2 * s) >= 2048:
         s *= 2
@@ -230,7 +254,15 @@ def _weight_grad(w, dy2, x2):
     stalled one run on cross-stream allocator reuse; they stay in-stream.)"""
     Fo, K = dy2.shape[1], x2.shape[1]
     if not _direct_ok(w):
-        return dy2.t() @ x2
+        s = _splitk(dy2.shape[0], Fo, K) if use_hip(dy2) else 1
+        if s == 1:
+            return dy2.t() @ x2
+        T = dy2.shape[0] // s
+        part = torch.bmm(dy2.view(s, T, Fo).transpose(1, 2), x2.view(s, T, K),
+                         out=_workspace(dy2.device, s * Fo * K).view(s, Fo, K))
+        g = torch.empty(Fo, K, device=dy2.device, dtype=dy2.dtype)
+        _native.require_hip().splitk_add(part, g, False)
+        return g
     g = w.grad.view(Fo, K)
     s = _splitk(dy2.shape[0], Fo, K)
     if s > 1:
@@ -251,6 +283,24 @@ def _direct_ok(p) -> bool:
             and torch.is_grad_enabled() is False)
 
 
+def _arena_grads(params):
+    """The parameters' arena gradient slices when every one of them takes a
+    direct write (bf16 flat arena, see parallel.flat), else None.  Kernels that
+    reduce a parameter gradient (LayerNorm γ/β, biases) then accumulate straight
+    into the arena — no gradient tensor, no AccumulateGrad add kernel."""
+    out = []
+    for p in params:
+        if p is None or not _direct_ok(p) or p.grad.dtype != torch.bfloat16:
+            return None
+        out.append(p.grad.view(-1))
+    return out
+
+
+def _signal_ready(params):
+    for p in params:
+        p._pdo_ready(p)
+
+
 def linear(x, w, b=None):
     if use_hip(x):
         return _LinearFn.apply(x, w, b)
@@ -269,12 +319,18 @@ class _BiasGeluFn(torch.autograd.Function):
         y = m.bias_gelu_fwd(x2, b)
         ctx.save_for_backward(x2, b)
         ctx.shape = x.shape
+        ctx.bias = b
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         m = _native.require_hip()
         x2, b = ctx.saved_tensors
+        gd = _arena_grads((ctx.bias,))
+        if gd is not None:
+            (dx,) = m.bias_gelu_bwd(dy.reshape(x2.shape).contiguous(), x2, b, db_out=gd[0])
+            _signal_ready((ctx.bias,))
+            return dx.view(ctx.shape), None
         dx, db = m.bias_gelu_bwd(dy.reshape(x2.shape).contiguous(), x2, b)
         return dx.view(ctx.shape), db
 

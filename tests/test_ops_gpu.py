@@ -164,6 +164,67 @@ def test_linear_splitk_weight_grad(cuda, T, Fo, K):
     assert rel_err(m.w.grad, ref) < 2e-2
 
 
+def test_linear_splitk_nondirect_weight_grad(cuda):
+    """Wide dW (≥256 tiles, K ≥ 32768) outside the arena: split-K into a fresh tensor."""
+    from paddle_operator_amd import ops
+    T, Fo, K = 32768, 4096, 4096
+    assert ops._splitk(T, Fo, K) == 4
+    g = torch.Generator(device=cuda).manual_seed(12)
+    w = (0.02 * torch.randn(Fo, K, device=cuda, generator=g)).bfloat16().requires_grad_()
+    x = torch.randn(T, K, device=cuda, generator=g).bfloat16()
+    dy = torch.randn(T, Fo, device=cuda, generator=g).bfloat16()
+    ops.linear(x, w).backward(dy)
+    assert rel_err(w.grad, dy.float().t() @ x.float()) < 2e-2
+
+
+def test_arena_direct_norm_and_bias_grads(cuda):
+    """LayerNorm γ/β, folded residual biases, bias-GELU and linear biases reduce
+    straight into the flat arena (accumulating, no AccumulateGrad) and match fp32."""
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.parallel.flat import FlatParams
+    N, C = 2048, 1024
+    torch.manual_seed(5)
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w1 = torch.nn.Parameter(1 + 0.1 * torch.randn(C))
+            self.b1 = torch.nn.Parameter(0.1 * torch.randn(C))
+            self.w2 = torch.nn.Parameter(1 + 0.1 * torch.randn(C))
+            self.b2 = torch.nn.Parameter(0.1 * torch.randn(C))
+            self.rb = torch.nn.Parameter(0.1 * torch.randn(C))
+            self.lw = torch.nn.Parameter(0.02 * torch.randn(C, C))
+            self.lb = torch.nn.Parameter(0.1 * torch.randn(C))
+            self.gb = torch.nn.Parameter(0.1 * torch.randn(C))
+
+        def forward(self, x, r, hip=True):
+            if hip:
+                h = ops.layer_norm(x, self.w1, self.b1)
+                _, y = ops.add_layer_norm(x, r + h, self.w2, self.b2, rbias=self.rb)
+                return ops.bias_gelu(ops.linear(y, self.lw, self.lb), self.gb)
+            F_ = torch.nn.functional
+            h = F_.layer_norm(x, (C,), self.w1, self.b1)
+            y = F_.layer_norm(x + r + h + self.rb, (C,), self.w2, self.b2)
+            return ops.ref_bias_gelu(F_.linear(y, self.lw, self.lb), self.gb)
+
+    m = M().to(cuda)
+    ref = M().to(cuda)
+    ref.load_state_dict(m.state_dict())
+    m = m.bfloat16()
+    FlatParams(m, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(6)
+    x = torch.randn(N, C, device=cuda, generator=g)
+    r = torch.randn(N, C, device=cuda, generator=g)
+    dy = torch.randn(N, C, device=cuda, generator=g)
+    for _ in range(2):  # accumulates like two micro-batches
+        m(x.bfloat16(), r.bfloat16()).backward(dy.bfloat16())
+    for _ in range(2):
+        ref(x, r, hip=False).backward(dy)
+    for name, p in m.named_parameters():
+        q = dict(ref.named_parameters())[name]
+        assert rel_err(p.grad, q.grad) < 3e-2, name
+
+
 @pytest.mark.parametrize("N,F", [(1024, 4096), (77, 3072)])
 def test_bias_gelu(cuda, N, F):
     ops = _ops()
