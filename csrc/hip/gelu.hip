@@ -3,48 +3,71 @@
 // The GEMM producing x runs without bias (plain hipBLASLt); the bias add, the
 // activation and — in backward — the bias gradient column reduction are fused
 // here, so the [N, 4C] activation makes exactly one HBM round trip per pass.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace pdo {
 
-__device__ __forceinline__ float fast_tanh(float u) {
-  // tanh(u) = 1 - 2 / (exp(2u) + 1); saturates correctly at ±inf
-  return 1.f - __fdividef(2.f, __expf(2.f * u) + 1.f);
+// 0.5·x·(1 + tanh u) = x·σ(2u), u = k0(x + k1x³): one exp2 and one rcp per
+// element, no 64-bit modulo (the grid stride is a multiple of the row width,
+// so each thread's bias vector is fixed) and, in backward, U rows of
+// independent 16-B loads in flight per thread before any math.
+// Measured at [65536, 4096] bf16 (tools/elt_probe.py): forward 241 → 205 µs
+// (5.25 TB/s, above a plain torch copy's 4.69), backward 355 → 317 µs, against
+// the tanh form with a per-vector 64-bit modulo.
+constexpr float GK0 = 0.7978845608028654f, GK1 = 0.044715f;
+constexpr float GL2E = 1.4426950408889634f;
+
+__device__ __forceinline__ float gelu_sig(float x) {
+  const float t = x * x;
+  const float z = x * __builtin_fmaf(t, -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);  // -2u·log2(e)
+  const float e = __builtin_amdgcn_exp2f(z);
+  return x * __builtin_amdgcn_rcpf(1.f + e);
 }
 
-__device__ __forceinline__ float gelu_f(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + fast_tanh(k0 * (x + k1 * x * x * x)));
+// d/dx x·σ(2u) = s + x·s·(1-s)·2u', s = σ(2u)
+__device__ __forceinline__ float gelu_sig_grad(float x) {
+  const float t = x * x;
+  const float z = x * __builtin_fmaf(t, -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);
+  const float e = __builtin_amdgcn_exp2f(z);
+  const float sg = __builtin_amdgcn_rcpf(1.f + e);
+  const float w = __builtin_fmaf(t, 6.f * GK0 * GK1, 2.f * GK0);  // 2u'
+  const float q = x * (1.f - sg) * w;  // (1 - s), not e·s: e = inf at x ≪ 0
+  return __builtin_fmaf(sg, q, sg);
 }
 
-__device__ __forceinline__ float gelu_g(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float x2 = x * x;
-  const float t = fast_tanh(k0 * (x + k1 * x2 * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
-}
-
-// grid-stride over 8-element vectors; F % 8 == 0
+template <int U>
 __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
-                                                            bf16* __restrict__ y, long long nvec, int F8) {
+                                                             bf16* __restrict__ y, long long nvec, int F8) {
   const bf16x8* xv = reinterpret_cast<const bf16x8*>(x);
-  const bf16x8* bv = reinterpret_cast<const bf16x8*>(b);
   bf16x8* yv = reinterpret_cast<bf16x8*>(y);
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
-    f32x8 v = to_f32(xv[i]) + to_f32(bv[i % F8]);
-    f32x8 o;
+  const long long stride = (long long)gridDim.x * 256;  // multiple of F8 (host)
+  const long long i0 = blockIdx.x * 256LL + threadIdx.x;
+  const f32x8 bb = to_f32(reinterpret_cast<const bf16x8*>(b)[i0 % F8]);
+  for (long long i = i0; i < nvec; i += U * stride) {
+    bf16x8 in[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = gelu_f(v[j]);
-    yv[i] = to_bf16(o);
+    for (int u = 0; u < U; ++u)
+      if (i + u * stride < nvec) in[u] = xv[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i + u * stride < nvec) {
+        const f32x8 v = to_f32(in[u]) + bb;
+        f32x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = gelu_sig(v[j]);
+        yv[i + u * stride] = to_bf16(o);
+      }
+    }
   }
 }
 
-// block (x: 2048-column stripe, y: row group).  dx = dy * gelu'(x+b),
-// partial db for the stripe written to part[blockIdx.y][col].
+template <int U>
 __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                            const bf16* __restrict__ b, bf16* __restrict__ dx,
-                                                            float* __restrict__ part, int N, int F) {
+                                                             const bf16* __restrict__ b, bf16* __restrict__ dx,
+                                                             float* __restrict__ part, int N, int F) {
   const int c8 = blockIdx.x * 256 + threadIdx.x;
   const int F8 = F >> 3;
   const int rows_per = (N + gridDim.y - 1) / gridDim.y;
@@ -53,16 +76,31 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16* __restri
   f32x8 acc = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c8 < F8) {
     const f32x8 bb = to_f32(reinterpret_cast<const bf16x8*>(b)[c8]);
-#pragma unroll 4
-    for (int r = r0; r < r1; ++r) {
-      const size_t idx = (size_t)r * F8 + c8;
-      f32x8 d = to_f32(reinterpret_cast<const bf16x8*>(dy)[idx]);
-      f32x8 v = to_f32(reinterpret_cast<const bf16x8*>(x)[idx]) + bb;
-      f32x8 o;
+    const bf16x8* dyv = reinterpret_cast<const bf16x8*>(dy);
+    const bf16x8* xv = reinterpret_cast<const bf16x8*>(x);
+    bf16x8* dxv = reinterpret_cast<bf16x8*>(dx);
+    for (int r = r0; r < r1; r += U) {
+      bf16x8 dd[U], xx[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = d[j] * gelu_g(v[j]);
-      reinterpret_cast<bf16x8*>(dx)[idx] = to_bf16(o);
-      acc += o;
+      for (int u = 0; u < U; ++u) {
+        if (r + u < r1) {
+          const size_t idx = (size_t)(r + u) * F8 + c8;
+          dd[u] = dyv[idx];
+          xx[u] = xv[idx];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + u < r1) {
+          const f32x8 d = to_f32(dd[u]);
+          const f32x8 v = to_f32(xx[u]) + bb;
+          f32x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = d[j] * gelu_sig_grad(v[j]);
+          dxv[(size_t)(r + u) * F8 + c8] = to_bf16(o);
+          acc += o;
+        }
+      }
     }
     float* p = part + (size_t)blockIdx.y * F + c8 * 8;
     reinterpret_cast<f32x4*>(p)[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
@@ -73,7 +111,13 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16* __restri
 int bias_gelu_fwd(const bf16* x, const bf16* b, bf16* y, long long N, int F, hipStream_t st) {
   if (F % 8) return -2;
   const long long nvec = N * (long long)(F / 8);
-  bias_gelu_fwd_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(x, b, y, nvec, F / 8);
+  // grid × 256 threads a multiple of F/8: every thread keeps one bias vector
+  const int F8 = F / 8;
+  const long long per = F8 % 256 == 0 ? F8 / 256 : F8;  // blocks per row-width period
+  long long g = std::max<long long>(1, 2048 / per) * per;
+  const long long need = (nvec + 255) / 256;
+  if (g > need) g = (need + per - 1) / per * per;
+  bias_gelu_fwd_kernel<1><<<(unsigned)g, 256, 0, st>>>(x, b, y, nvec, F8);
   return 0;
 }
 
@@ -90,7 +134,7 @@ int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float*
   if (F % 8) return -2;
   const int gx = (F / 8 + 255) / 256;
   const int gy = bias_gelu_bwd_groups(N, F);
-  bias_gelu_bwd_kernel<<<dim3(gx, gy), 256, 0, st>>>(dy, x, b, dx, part, (int)N, F);
+  bias_gelu_bwd_kernel<4><<<dim3(gx, gy), 256, 0, st>>>(dy, x, b, dx, part, (int)N, F);
   ColOut co = ColOut::one(db, F);
   co.acc = accumulate;
   colsum(part, gy, F, F, co, scratch, st);

@@ -97,17 +97,36 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
     adx[i] = adw[i];
   }
   const int nw = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + wid; row < N; row += nw) {
+  // every operand of a row (dy, x and the residual gradient) is requested
+  // up front, and the NEXT row's are requested before this row's two
+  // wave-wide reductions: the reductions' latency hides the loads'
+  bf16x8 nd[VPL], nx[VPL], nr[VPL];
+  auto fetch = [&](int row) {
+    const size_t base = (size_t)row * C;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c8 = lane + i * 64;
+      if (c8 < C8) {
+        nd[i] = reinterpret_cast<const bf16x8*>(dy + base)[c8];
+        nx[i] = reinterpret_cast<const bf16x8*>(x + base)[c8];
+        if (ADD) nr[i] = reinterpret_cast<const bf16x8*>(dres + base)[c8];
+      }
+    }
+  };
+  int row = blockIdx.x * 4 + wid;
+  if (row < N) fetch(row);
+  for (; row < N; row += nw) {
     const size_t base = (size_t)row * C;
     const float mu = mean[row], rs = rstd[row];
-    f32x8 xh[VPL], g[VPL];
+    f32x8 xh[VPL], g[VPL], rr[VPL];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c8 = lane + i * 64;
       if (c8 < C8) {
-        f32x8 d = to_f32(reinterpret_cast<const bf16x8*>(dy + base)[c8]);
-        f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(x + base)[c8]);
+        f32x8 d = to_f32(nd[i]);
+        f32x8 xv = to_f32(nx[i]);
+        if (ADD) rr[i] = to_f32(nr[i]);
         xh[i] = (xv - mu) * rs;
         g[i] = d * wv[i];
         adw[i] += d * xh[i];
@@ -119,6 +138,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
         }
       }
     }
+    if (row + nw < N) fetch(row + nw);
     s1 = wave_sum(s1) * inv_c;
     s2 = wave_sum(s2) * inv_c;
 #pragma unroll
@@ -126,7 +146,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
       const int c8 = lane + i * 64;
       if (c8 < C8) {
         f32x8 o = (g[i] - s1 - xh[i] * s2) * rs;
-        if (ADD) o += to_f32(reinterpret_cast<const bf16x8*>(dres + base)[c8]);
+        if (ADD) o += rr[i];
         if (NA == 3) adx[i] += o;
         reinterpret_cast<bf16x8*>(dx + base)[c8] = to_bf16(o);
       }
@@ -194,8 +214,10 @@ int layernorm_fwd(const bf16* x, const bf16* r, const bf16* rb, const bf16* w, c
 }
 
 int layernorm_bwd_grid(int N) {
-  int g = (N + 15) / 16;  // >= 4 rows per wave
-  if (g > 1024) g = 1024;
+  // one resident round: ≤ 2 waves/SIMD at this kernel's register count
+  // (4 waves per block, 256 CUs × 4 SIMDs × 2 / 4 = 512 blocks), ≥ 4 rows per wave
+  int g = (N + 15) / 16;
+  if (g > 512) g = 512;
   if (g < 1) g = 1;
   return g;
 }
