@@ -247,6 +247,23 @@ void splitk_add(at::Tensor part, at::Tensor out, bool accumulate) {
            "splitk_add");
 }
 
+// out[M][N] (+)= dyᵀ·x for dy [T, M], x [T, N] (bf16, contiguous); false = unsupported shape
+bool gemm_dw(at::Tensor dy, at::Tensor x, at::Tensor out, bool accumulate, int64_t splits) {
+  CHECK_IN(dy); CHECK_IN(x); CHECK_IN(out); CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(out);
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0));
+  const long long T = dy.size(0);
+  const int M = dy.size(1), N = x.size(1);
+  TORCH_CHECK(out.numel() == (int64_t)M * N, "gemm_dw: out must hold M·N elements");
+  int s = pdo::gemm_dw_splits(T, M, N);
+  if (s == 0) return false;
+  if (splits > 0) s = (int)splits;
+  at::Tensor ws;
+  if (s > 1) ws = at::empty({(int64_t)s * M * N}, dy.options());
+  CHECK_RC(pdo::gemm_dw(bp(dy), bp(x), T, M, N, M, N, bp(out), N, accumulate ? 1 : 0, s > 1 ? bp(ws) : nullptr, s,
+                        cur_stream()), "gemm_dw");
+  return true;
+}
+
 at::Tensor transpose(at::Tensor x) {
   CHECK_IN(x); CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R, C] with R, C % 64 == 0");
@@ -535,6 +552,9 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("adamw_flat", &adamw_flat);
   m.def("splitk_add", &splitk_add);
   m.def("transpose", &transpose);
+  m.def("gemm_dw", &gemm_dw, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = true,
+        py::arg("splits") = 0);
+  m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);

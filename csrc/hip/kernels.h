@@ -57,6 +57,11 @@ int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, cons
 // ResNet stem max-pool 3×3/2 pad 1, NHWC bf16 (pool.hip); arg = uint8 window position
 int maxpool3s2_fwd(const bf16* x, int N, int H, int W, int C, bf16* y, uint8_t* arg, hipStream_t st);
 int maxpool3s2_bwd(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, bf16* dx, hipStream_t st);
+// gemm_dw.hip: C[M][N] (+)= Aᵀ·B for token-major A [T][M], B [T][N] (weight gradients)
+// splits: 0 = shape unsupported; ws: splits·M·N bf16 when splits > 1
+int gemm_dw_splits(long long T, int M, int N);
+int gemm_dw(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
+            int accumulate, bf16* ws, int splits, hipStream_t st);
 // transpose.hip: out[C][R] = in[R][C], R and C multiples of 64
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);

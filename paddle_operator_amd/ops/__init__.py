@@ -263,6 +263,23 @@ def _weight_grad(w, dy2, x2):
         g = torch.empty(Fo, K, device=dy2.device, dtype=dy2.dtype)
         _native.require_hip().splitk_add(part, g, False)
         return g
+    if not (_HIP_DW[0] and dy2.is_cuda and w.grad.dtype == torch.bfloat16 and dy2.is_contiguous()
+            and x2.is_contiguous() and _native.require_hip().gemm_dw(dy2, x2, w.grad, True)):
+        _weight_grad_lib(w, dy2, x2)
+    w._pdo_ready(w)
+    return None
+
+
+# dW on the HIP token-major GEMM (csrc/hip/gemm_dw.hip) where its shape
+# contract holds (M, N % 256, tokens % 64); hipBLASLt otherwise.  Measured at
+# the GPT-2-medium B=64 shapes (tools/dw_probe.py --pdo-only): qkv 375 vs 390 µs,
+# proj 131 vs 160, fc1 462 vs 505, fc2 468 vs 506 (hipBLASLt tuned + HIP fold).
+_HIP_DW = [os.environ.get("PDO_HIP_DW", "1") != "0"]
+
+
+def _weight_grad_lib(w, dy2, x2):
+    """Arena dW on hipBLASLt: batched token-slice GEMM + HIP fold, or addmm_."""
+    Fo, K = dy2.shape[1], x2.shape[1]
     g = w.grad.view(Fo, K)
     s = _splitk(dy2.shape[0], Fo, K)
     if s > 1:
@@ -273,8 +290,6 @@ def _weight_grad(w, dy2, x2):
         _native.require_hip().splitk_add(part, g, True)
     else:
         g.addmm_(dy2.t(), x2)
-    w._pdo_ready(w)
-    return None
 
 
 def _direct_ok(p) -> bool:

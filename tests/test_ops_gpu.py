@@ -164,6 +164,30 @@ def test_linear_splitk_weight_grad(cuda, T, Fo, K):
     assert rel_err(m.w.grad, ref) < 2e-2
 
 
+@pytest.mark.parametrize("T,M,N,acc", [(4096, 256, 512, False), (16384, 1024, 1024, True), (65536, 512, 256, True),
+                                       (1024, 768, 256, False)])
+def test_gemm_dw(cuda, T, M, N, acc):
+    """HIP weight-gradient GEMM (token-major operands, transposing LDS reads, split-K) vs fp32."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    g = torch.Generator(device=cuda).manual_seed(13)
+    dy = torch.randn(T, M, device=cuda, generator=g).bfloat16()
+    x = torch.randn(T, N, device=cuda, generator=g).bfloat16()
+    out = torch.randn(M, N, device=cuda, generator=g).bfloat16() if acc else torch.zeros(M, N, device=cuda).bfloat16()
+    ref = out.float() + dy.float().t() @ x.float()
+    assert m.gemm_dw(dy, x, out, True)
+    assert rel_err(out, ref) < 1e-2, m.gemm_dw_splits(T, M, N)
+
+
+def test_gemm_dw_rejects_unsupported_shape(cuda):
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    dy = torch.zeros(1000, 256, device=cuda).bfloat16()  # T % 64 != 0
+    x = torch.zeros(1000, 256, device=cuda).bfloat16()
+    assert m.gemm_dw_splits(1000, 256, 256) == 0
+    assert not m.gemm_dw(dy, x, torch.zeros(256, 256, device=cuda).bfloat16(), True)
+
+
 def test_linear_splitk_nondirect_weight_grad(cuda):
     """Wide dW (≥256 tiles, K ≥ 32768) outside the arena: split-K into a fresh tensor."""
     from paddle_operator_amd import ops

@@ -31,7 +31,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--shapes", default="qkv,proj,fc1,fc2,lm")
+    ap.add_argument("--pdo-only", action="store_true", help="time the HIP dW GEMM against the shipped-table path")
     a = ap.parse_args()
+    if a.pdo_only:
+        return pdo_vs_lib(a)
     from paddle_operator_amd import _native
     m = _native.require_hip()
     tun = torch.cuda.tunable
@@ -79,6 +82,52 @@ def main():
         best = min((v, k) for k, v in res.items() if k.endswith("_us"))
         res["best"] = best[1]
         res["best_tf"] = round(fl / (best[0] * 1e-6) / 1e12, 1)
+        print(json.dumps(res), flush=True)
+
+
+def pdo_vs_lib(a):
+    from paddle_operator_amd import _native, ops
+    from paddle_operator_amd.utils.tuning import enable_tuned_gemms
+    m = _native.require_hip()
+    enable_tuned_gemms()
+    T = a.tokens
+    dev = torch.device("cuda")
+    table = {"qkv": (3072, 1024), "proj": (1024, 1024), "fc1": (4096, 1024), "fc2": (1024, 4096), "lm": (50304, 1024)}
+    for name in a.shapes.split(","):
+        Fo, K = table[name]
+        g = torch.Generator(device=dev).manual_seed(0)
+        dy = (0.01 * torch.randn(T, Fo, device=dev, generator=g)).bfloat16()
+        x = torch.randn(T, K, device=dev, generator=g).bfloat16()
+        w = torch.zeros(Fo, K, device=dev, dtype=torch.bfloat16)
+        fl = 2.0 * T * Fo * K
+        res = {"gemm": name, "splits": m.gemm_dw_splits(T, Fo, K)}
+        gl = torch.zeros(Fo, K, device=dev, dtype=torch.bfloat16)
+
+        class P:  # stand-in parameter with an arena-style grad
+            pass
+        p = P()
+        p.grad = gl
+        p._pdo_direct = True
+        p._pdo_ready = lambda _p: None
+        variants = [int(v) for v in os.environ.get("DW_SPLITS", "0").split(",")]
+        lib, pdo = [], {v: [] for v in variants}
+        for _ in range(5):
+            lib.append(bench(lambda: ops._weight_grad_lib(p, dy, x)))
+            if res["splits"]:
+                for v in variants:
+                    pdo[v].append(bench(lambda: m.gemm_dw(dy, x, w, True, v)))
+        res["lib_us"] = round(sorted(lib)[2], 1)
+        res["lib_tf"] = round(fl / (res["lib_us"] * 1e-6) / 1e12, 1)
+        if res["splits"]:
+            for v in variants:
+                t = sorted(pdo[v])[2]
+                res[f"pdo{v}_us"] = round(t, 1)
+                res[f"pdo{v}_tf"] = round(fl / (t * 1e-6) / 1e12, 1)
+            w.zero_()
+            gl.zero_()
+            m.gemm_dw(dy, x, w, True)
+            ops._weight_grad_lib(p, dy, x)
+            res["maxdiff_rel"] = ((w.float() - gl.float()).abs().max() / gl.float().abs().max()).item()
         print(json.dumps(res), flush=True)
 
 
