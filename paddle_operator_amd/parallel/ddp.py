@@ -37,6 +37,7 @@ class BucketedDDP:
         self._launched = [False] * len(flat.buckets)
         self._next = 0
         self._bucket_of = flat.bucket_of()
+        self._seen = set()
         self._hooks = []
         if self.enabled:
             for s in flat.slots:
@@ -67,6 +68,7 @@ class BucketedDDP:
         self._launched = [False] * len(self.flat.buckets)
         self._works = []
         self._next = 0
+        self._seen = set()
 
     def finish(self):
         """Call after backward: launch stragglers, make the compute stream wait."""
@@ -84,9 +86,22 @@ class BucketedDDP:
 
     # -- internals ----------------------------------------------------------
     def _hook(self, p):
+        """Readiness of one parameter's gradient for this step.
+
+        Two sources call it: the post-accumulate-grad hook and, for gradients
+        a kernel wrote straight into the arena, the op itself (``p._pdo_ready``)
+        right after enqueuing that kernel.  The autograd engine ALSO runs the
+        post-accumulate hook for such a parameter although its Function
+        returned no gradient, so each parameter counts once per step — a
+        double count would launch its bucket's all-reduce before the rest of
+        the bucket was written (caught by tests/test_ddp_gpu.py)."""
         if not self._sync:
             return
-        i = self._bucket_of[id(p)]
+        key = id(p)
+        if key in self._seen:
+            return
+        self._seen.add(key)
+        i = self._bucket_of[key]
         self._pending[i] += 1
         # buckets are issued strictly in index order (identical on every rank,
         # whatever order the autograd engine produced the gradients in)
