@@ -16,7 +16,9 @@
 //     computed as [q × key] so P and dS are the B operands of dV^T = dO^T·P
 //     and dK^T = Q^T·dS; Q / dO tiles stream through LDS.
 //   dQ:   workgroup = 128 queries, S^T / dP^T with the query on the lane,
-//     dQ^T = K^T·dS^T; K / V tiles stream through LDS.
+//     dQ^T = K^T·dS^T; K / V tiles stream through LDS.  Runs first and also
+//     writes delta = rowsum(dO ∘ O) (its dO fragments are already in
+//     registers), which dK/dV then reads: no separate delta pass.
 // LDS tiles are [64 rows][64 bf16] with one XOR swizzle of the 16-B chunk
 // index, chosen so BOTH the row reads (ds_read_b128, 16 rows per lane group)
 // and the transposed reads (4 rows × 64 B per half-wave) are conflict-free.
@@ -272,33 +274,6 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
 }
 
 // ============================================================================
-// backward: delta = rowsum(dO ∘ O)   (one thread per 8 elements, 8 lanes per row)
-// ============================================================================
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ o,
-                                                         float* __restrict__ delta, int B, int S, int H) {
-  const long long gid = blockIdx.x * 256LL + threadIdx.x;
-  const long long row = gid >> 3;  // (b, s, h) row
-  const int part = gid & 7;
-  const long long nrows = (long long)B * S * H;
-  float acc = 0.f;
-  if (row < nrows) {
-    f32x8 a = to_f32(reinterpret_cast<const bf16x8*>(dout + row * HD)[part]);
-    f32x8 c = to_f32(reinterpret_cast<const bf16x8*>(o + row * HD)[part]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * c[j];
-  }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  if (row < nrows && part == 0) {
-    const int h = row % H;
-    const long long bs = row / H;
-    const int s = bs % S, b = bs / S;
-    delta[((size_t)b * H + h) * S + s] = acc;
-  }
-}
-
-// ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
@@ -421,9 +396,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
 // ============================================================================
 __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                       const float* __restrict__ lse, const float* __restrict__ delta,
-                                                       bf16* __restrict__ dqkv, int B, int S, int H, float c2,
-                                                       float scale) {
+                                                       const bf16* __restrict__ o, const float* __restrict__ lse,
+                                                       float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
+                                                       int H, float c2, float scale) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
@@ -445,7 +420,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ 
     df[ks] = *reinterpret_cast<const bf16x8*>(dobase + (size_t)q * ors + 16 * ks + 8 * hh);
   }
   const float lq = lse[(size_t)bh * S + q] * LOG2E;
-  const float dq_delta = delta[(size_t)bh * S + q];
+  // delta = rowsum(dO ∘ O) for this lane's query, from the dO fragments already
+  // in registers (this half-wave's 32 dims) + the other half's via one swap;
+  // written for the dK/dV kernel, which runs after this one
+  float dpart = 0.f;
+  {
+    const bf16* orow = o + ((size_t)(b * S + q) * H + h) * HD;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const f32x8 a = to_f32(df[ks]), c = to_f32(*reinterpret_cast<const bf16x8*>(orow + 16 * ks + 8 * hh));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpart = __builtin_fmaf(a[j], c[j], dpart);
+    }
+  }
+  const float dq_delta = dpart + __shfl_xor(dpart, 32, 64);
+  if (hh == 0) delta[(size_t)bh * S + q] = dq_delta;
   retire(qf);
   retire(df);
   retire(lq);
@@ -516,11 +505,10 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
 int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse, float* delta, bf16* dqkv, int B,
              int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
-  const long long rows = (long long)B * S * H;
-  attn_delta_kernel<<<(unsigned)((rows * 8 + 255) / 256), 256, 0, st>>>(dout, o, delta, B, S, H);
   const int grid = B * H * (S / 128);
+  // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
+  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
   attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
-  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
   return 0;
 }
 
