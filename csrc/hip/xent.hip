@@ -6,6 +6,10 @@
 // reduced deterministically by a one-block kernel that also stores the count
 // for backward.  Backward writes dlogits = (softmax - onehot) * dloss / count
 // in place over the logits buffer (one read + one write of [N, Vp]).
+// (Measured alternative, not kept: one fused pass holding each row in
+// registers, dlogits written in the forward — 4.6 ms vs these two passes'
+// 3.6 ms at [65536, 50304]: with ≤ 1 resident 50k-column row per CU the load,
+// reduce and store phases serialise.)
 #include "common.h"
 #include "kernels.h"
 
