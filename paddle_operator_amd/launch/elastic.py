@@ -137,6 +137,17 @@ class ElasticAgent:
                 time.sleep(self.poll / 2)
         return None
 
+    def gen_done(self, world: dict) -> bool:
+        """A peer of this generation already finished all steps: the job is
+        complete, and peers leaving now is teardown, not a scale event."""
+        for v in self.kv.get_prefix(self.prefix + "done/").values():
+            try:
+                if json.loads(v).get("gen") == world["gen"]:
+                    return True
+            except (ValueError, AttributeError):
+                continue
+        return False
+
     def changed(self, world: dict) -> bool:
         np_ = self.np()
         mem = self.members()
@@ -184,6 +195,9 @@ class ElasticAgent:
                     if rc is not None:
                         break
                     if self.changed(world):
+                        if self.gen_done(world):
+                            rc = self.proc.wait()  # generation completed: let this worker finish too
+                            break
                         _log("membership/np changed → stopping worker for re-rendezvous")
                         self.stop_worker()
                         rc = None

@@ -20,6 +20,7 @@ def short(name: str) -> str:
         return f"hipBLASLt GEMM {kind} MT{m.group(1) if m else '?'}"
     if name.startswith("void "):
         name = name[5:]
+    name = name.replace("(anonymous namespace)::", "")
     # drop the trailing argument list only (templates may contain parentheses)
     depth = 0
     for i, ch in enumerate(name):
