@@ -47,6 +47,7 @@ class JobEnv:
     replicas: int = 1
     pod_name: str = ""
     visible_devices: str = ""
+    cp_size: int = 1
 
     @staticmethod
     def from_env(env: Optional[Dict[str, str]] = None) -> "JobEnv":
@@ -75,6 +76,7 @@ class JobEnv:
             replicas=int(e.get("PDO_REPLICAS", str(num))),
             pod_name=e.get("HOSTNAME", ""),
             visible_devices=e.get("HIP_VISIBLE_DEVICES", ""),
+            cp_size=int(e.get("PDO_CP_SIZE", "1") or 1),
         )
 
     # ------------------------------------------------------------------ modes
@@ -124,6 +126,15 @@ class JobEnv:
             "MASTER_ADDR": host,
             "MASTER_PORT": str(port + STORE_PORT_OFFSET),
         }
+
+    def check_supported(self) -> None:
+        """Context/sequence parallelism is an extension point only (SURVEY §5.7:
+        the reference has none, no BASELINE config needs it — GPT-2-medium at
+        ctx 1024 fits one MI355X).  ``PDO_CP_SIZE`` is read so a job that asks
+        for it fails loudly instead of silently training data-parallel."""
+        if self.cp_size != 1:
+            raise NotImplementedError(f"PDO_CP_SIZE={self.cp_size}: context parallelism is not implemented "
+                                      "(data parallel only; see SURVEY.md §5.7)")
 
     def kv_endpoints(self) -> str:
         return os.environ.get("PDO_KV", "") or self.elastic_server

@@ -64,6 +64,7 @@ def run_collective(args, jenv) -> int:
 
     from . import bootstrap
     from ..utils import checkpoint as ckpt
+    from ..utils import trace
 
     if "RANK" not in os.environ or not args.worker:
         os.environ.update(jenv.torch_env(0, args.nproc_per_pod))
@@ -118,7 +119,8 @@ def run_collective(args, jenv) -> int:
     done = 0
     while step < args.steps:
         in_step[0] = True
-        loss = trainer.step()
+        with trace.range(f"step {step}"):
+            loss = trainer.step()
         if args.throttle_ms:
             time.sleep(args.throttle_ms / 1e3)
         if dev.type == "cuda" and args.ckpt_dir:
@@ -127,7 +129,8 @@ def run_collective(args, jenv) -> int:
         in_step[0] = False
         done += 1
         if args.ckpt_dir and args.ckpt_every and step % args.ckpt_every == 0 and b.rank == 0:
-            ckpt.save(state(), args.ckpt_dir, step)
+            with trace.range("checkpoint"):
+                ckpt.save(state(), args.ckpt_dir, step)
         if step % args.log_every == 0 or step == args.steps:
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
@@ -220,6 +223,7 @@ def main(argv=None) -> int:
     args = parse_args(argv)
     from .env import JobEnv
     jenv = JobEnv.from_env()
+    jenv.check_supported()
     log(f"role={jenv.role} id={jenv.trainer_id} mode={jenv.mode} elastic={jenv.elastic} workload={args.workload}")
     if jenv.mode == "PS" or args.workload in ("wide_deep", "deepfm") and jenv.pserver_endpoints:
         return run_ps(args, jenv)

@@ -18,6 +18,7 @@ from .models.gpt2 import GPT2, GPT2Config
 from .ops.optim import FlatAdamW
 from .parallel.ddp import BucketedDDP
 from .parallel.flat import FlatParams
+from .utils import trace
 
 
 @dataclass
@@ -98,10 +99,14 @@ class GPT2Trainer:
             idx, tgt = self.batch()
         self.flat.zero_grad()
         self.ddp.prepare()
-        loss = self.model(idx, tgt)
-        loss.backward()
-        self.ddp.finish()
-        self.opt.step(grad_scale=self.ddp.grad_scale)
+        with trace.range("forward"):
+            loss = self.model(idx, tgt)
+        with trace.range("backward"):
+            loss.backward()
+        with trace.range("allreduce_drain"):
+            self.ddp.finish()
+        with trace.range("optimizer"):
+            self.opt.step(grad_scale=self.ddp.grad_scale)
         return loss
 
     def tokens_per_step(self):

@@ -184,7 +184,11 @@ def test_elastic_scale_out_reforms_world(tmp_path):
     try:
         # generation 1 (np=2) is training once both ranks reported ready
         kv.wait_count("/pdo/default-ej/ready/", 2, timeout=120)
-        time.sleep(1.5)
+        # scale out only once the 2-rank generation has checkpointed (a fixed
+        # sleep raced with slow steps under a loaded pytest -n run)
+        t_end = time.time() + 120
+        while not list(ck.glob("ckpt-*.pt")) and time.time() < t_end:
+            time.sleep(0.2)
         procs.append(agent(2, 3))
         kv.put("/paddle/default-ej/np", "3")  # what the controller's syncNP does on scale-out
         assert wait_all(procs, timeout=240) == [0, 0, 0], open(tmp_path / "e0.log").read()[-4000:]
