@@ -7,7 +7,7 @@ Here the launcher and the GPT-2 trainer mark their phases (step, forward,
 backward, all-reduce drain, optimizer, checkpoint) so a
 ``rocprofv3 --marker-trace --kernel-trace`` timeline groups kernels by phase.
 
-Calls go straight to ``libroctx64.so`` through ctypes (no torch wrapper).
+Calls go straight to rocprofiler-sdk's roctx library through ctypes (no torch wrapper).
 Disabled unless ``PDO_ROCTX=1``: then ``range()`` is a shared no-op context
 manager, so the instrumented hot loop pays one attribute lookup per phase.
 """
@@ -25,8 +25,11 @@ _NULL = contextlib.nullcontext()
 def _lib():
     global _LIB, _ENABLED
     if _LIB is None:
-        for name in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libroctx64.so"),
-                     "libroctx64.so.4", "libroctx64.so"):
+        lib_dir = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
+        # rocprofiler-sdk's roctx first: rocprofv3 --marker-trace intercepts it
+        # (the legacy roctracer libroctx64 is not seen by rocprofv3)
+        for name in (os.path.join(lib_dir, "librocprofiler-sdk-roctx.so.1"),
+                     os.path.join(lib_dir, "libroctx64.so.4"), "libroctx64.so"):
             try:
                 lib = ctypes.CDLL(name)
             except OSError:

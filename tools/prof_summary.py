@@ -63,6 +63,32 @@ def main():
         if a.steps:
             line += f" {d/1e6/a.steps:.3f} |"
         print(line)
+    try:
+        regs = c.execute("select name, start, end, extdata from regions").fetchall()
+    except sqlite3.Error:
+        regs = []
+    if regs:
+        # roctx ranges (utils/trace.py, PDO_ROCTX=1): host-side span of each phase
+        # and the GPU kernel time that ran inside it (kernels are async, so the
+        # GPU column shows how far the device lags the host)
+        import json
+        ph = defaultdict(lambda: [[], []])
+        for name, s0, s1, ext in regs:
+            try:
+                msg = json.loads(ext).get("message", name)
+            except (ValueError, TypeError):
+                msg = name
+            if msg.startswith("step "):
+                msg = "step"
+            busy = sum(min(e, s1) - max(s, s0) for _, _, s, e in rows if e > s0 and s < s1)
+            ph[msg][0].append(s1 - s0)
+            ph[msg][1].append(busy)
+        print("\n## roctx phases (host span vs GPU kernel-busy time inside it)\n")
+        med = lambda v: sorted(v)[len(v) // 2] / 1e6  # noqa: E731 (warm-up steps skew the mean)
+        print("| phase | count | host ms (median) | GPU busy ms (median) |")
+        print("|---|---|---|---|")
+        for k, (d, b) in sorted(ph.items(), key=lambda x: -med(x[1][0])):
+            print(f"| {k} | {len(d)} | {med(d):.2f} | {med(b):.2f} |")
 
 
 if __name__ == "__main__":
