@@ -264,6 +264,73 @@ bool gemm_dw(at::Tensor dy, at::Tensor x, at::Tensor out, bool accumulate, int64
   return true;
 }
 
+// ---- forward-layout GEMM with fused epilogues (gemm_nt.hip) ----
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
+  return M < (1LL << 31) && N < (1LL << 31) && pdo::gemm_nt_ok((int)M, (int)N, (int)K, (int)K, (int)K, (int)N);
+}
+
+static void nt_check(const at::Tensor& a, const at::Tensor& b) {
+  CHECK_IN(a); CHECK_IN(b); CHECK_BF16(a); CHECK_BF16(b);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_nt: a [M, K], b [N, K]");
+  TORCH_CHECK(gemm_nt_supported(a.size(0), b.size(0), a.size(1)), "gemm_nt: M, N % 256 and K % 64 required");
+}
+
+// c = a·bᵀ (+ bias)
+at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias) {
+  nt_check(a, b);
+  const int M = a.size(0), N = b.size(0), K = a.size(1);
+  auto c = at::empty({M, N}, a.options());
+  const bf16* bptr = nullptr;
+  if (bias.has_value()) {
+    CHECK_IN((*bias)); CHECK_BF16((*bias)); TORCH_CHECK(bias->numel() == N);
+    bptr = bp(*bias);
+  }
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, bptr ? 1 : 0, bptr, nullptr, 0, nullptr,
+                        cur_stream()), "gemm_nt");
+  return c;
+}
+
+// (pre, y): pre = a·bᵀ, y = gelu(pre + bias)
+std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias) {
+  nt_check(a, b);
+  CHECK_IN(bias); CHECK_BF16(bias);
+  const int M = a.size(0), N = b.size(0), K = a.size(1);
+  TORCH_CHECK(bias.numel() == N);
+  auto pre = at::empty({M, N}, a.options());
+  auto y = at::empty({M, N}, a.options());
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(pre), N, 2, bp(bias), bp(y), N, nullptr, cur_stream()),
+           "gemm_nt_gelu");
+  return {pre, y};
+}
+
+// dx = (a·bᵀ) ⊙ gelu'(pre + bias); db = colsum(dx) (accumulated into db_out when given)
+std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre, at::Tensor bias,
+                                      c10::optional<at::Tensor> db_out) {
+  nt_check(a, b);
+  CHECK_IN(pre); CHECK_IN(bias); CHECK_BF16(pre); CHECK_BF16(bias);
+  const int M = a.size(0), N = b.size(0), K = a.size(1);
+  TORCH_CHECK(pre.dim() == 2 && pre.size(0) == M && pre.size(1) == N && bias.numel() == N);
+  auto dx = at::empty({M, N}, a.options());
+  const int G = pdo::gemm_nt_dbias_rows(M);
+  auto part = at::empty({(int64_t)G * N + pdo::colsum_scratch_floats(G, N)}, a.options().dtype(at::kFloat));
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(dx), N, 3, bp(bias), bp(pre), N, fp(part), cur_stream()),
+           "gemm_nt_dgelu");
+  at::Tensor db;
+  pdo::ColOut co;
+  if (db_out.has_value()) {
+    db = *db_out;
+    CHECK_IN(db); CHECK_BF16(db); TORCH_CHECK(db.numel() == N);
+    co = pdo::ColOut::one(bp(db), N);
+    co.acc = 1;
+  } else {
+    db = at::empty_like(bias);
+    co = pdo::ColOut::one(bp(db), N);
+  }
+  pdo::colsum(fp(part), G, N, N, co, fp(part) + (size_t)G * N, cur_stream());
+  if (db_out.has_value()) return {dx};
+  return {dx, db};
+}
+
 at::Tensor transpose(at::Tensor x) {
   CHECK_IN(x); CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R, C] with R, C % 64 == 0");
@@ -555,6 +622,11 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("gemm_dw", &gemm_dw, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = true,
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
+  m.def("gemm_nt_gelu", &gemm_nt_gelu);
+  m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),
+        py::arg("db_out") = py::none());
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);

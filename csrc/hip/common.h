@@ -76,6 +76,29 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 
+// GELU(tanh) in logistic form (gelu.hip, gemm_nt.hip epilogues):
+// 0.5·x·(1 + tanh u) = x·σ(2u), u = k0(x + k1x³): one exp2 and one rcp.
+constexpr float GK0 = 0.7978845608028654f, GK1 = 0.044715f;
+constexpr float GL2E = 1.4426950408889634f;
+
+__device__ __forceinline__ float gelu_sig(float x) {
+  const float t = x * x;
+  const float z = x * __builtin_fmaf(t, -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);  // -2u·log2(e)
+  const float e = __builtin_amdgcn_exp2f(z);
+  return x * __builtin_amdgcn_rcpf(1.f + e);
+}
+
+// d/dx x·σ(2u) = s + x·s·(1-s)·2u', s = σ(2u)
+__device__ __forceinline__ float gelu_sig_grad(float x) {
+  const float t = x * x;
+  const float z = x * __builtin_fmaf(t, -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);
+  const float e = __builtin_amdgcn_exp2f(z);
+  const float sg = __builtin_amdgcn_rcpf(1.f + e);
+  const float w = __builtin_fmaf(t, 6.f * GK0 * GK1, 2.f * GK0);  // 2u'
+  const float q = x * (1.f - sg) * w;  // (1 - s), not e·s: e = inf at x ≪ 0
+  return __builtin_fmaf(sg, q, sg);
+}
+
 // number of workgroups for a grid-stride memory-bound kernel (256 CUs × 8)
 inline int stream_grid(long long work_items, int per_block) {
   long long g = (work_items + per_block - 1) / per_block;

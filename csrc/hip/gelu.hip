@@ -17,26 +17,7 @@ namespace pdo {
 // Measured at [65536, 4096] bf16 (tools/elt_probe.py): forward 241 → 205 µs
 // (5.25 TB/s, above a plain torch copy's 4.69), backward 355 → 317 µs, against
 // the tanh form with a per-vector 64-bit modulo.
-constexpr float GK0 = 0.7978845608028654f, GK1 = 0.044715f;
-constexpr float GL2E = 1.4426950408889634f;
-
-__device__ __forceinline__ float gelu_sig(float x) {
-  const float t = x * x;
-  const float z = x * __builtin_fmaf(t, -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);  // -2u·log2(e)
-  const float e = __builtin_amdgcn_exp2f(z);
-  return x * __builtin_amdgcn_rcpf(1.f + e);
-}
-
-// d/dx x·σ(2u) = s + x·s·(1-s)·2u', s = σ(2u)
-__device__ __forceinline__ float gelu_sig_grad(float x) {
-  const float t = x * x;
-  const float z = x * __builtin_fmaf(t, -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);
-  const float e = __builtin_amdgcn_exp2f(z);
-  const float sg = __builtin_amdgcn_rcpf(1.f + e);
-  const float w = __builtin_fmaf(t, 6.f * GK0 * GK1, 2.f * GK0);  // 2u'
-  const float q = x * (1.f - sg) * w;  // (1 - s), not e·s: e = inf at x ≪ 0
-  return __builtin_fmaf(sg, q, sg);
-}
+// gelu_sig / gelu_sig_grad: common.h (shared with the GEMM epilogues, gemm_nt.hip)
 
 template <int U>
 __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,

@@ -1,0 +1,270 @@
+// SPDX-License-Identifier: Apache-2.0
+// Forward-layout GEMM C[M][N] = A[M][K] · B[N][K]ᵀ (bf16 in, fp32 acc) for
+// gfx950 with fused epilogues — the transformer's projections (A = tokens ×
+// features, B = weight [out][in]) and their input gradients (B = Wᵀ).
+//
+// Both operands are K-contiguous, so every MFMA fragment is a plain 16-B row
+// read.  The tile machinery is gemm_dw.hip's: 256 × 256 × 64 per workgroup,
+// 8 waves as 2 (M) × 4 (N), LDS-DMA staging (global_load_lds_dwordx4, the
+// XOR swizzle applied to the source address), two LDS stages = 128 KiB, and
+// the two waves of each SIMD ping-ponging between an MFMA phase and an
+// LDS-read phase.  LDS rows are 128 B ([256][64] bf16) with attention's
+// swizzle (chunk ^ swz(row)): the 16 rows a ds_read_b128 lane group touches
+// land on 16 distinct bank slots.
+//
+// The MFMA runs with the operands swapped, D = W·Xᵀ, so an accumulator holds
+// 4 consecutive output features of one token per register group (8-B LDS
+// writes); the tile then leaves through LDS as whole rows, where the
+// per-feature terms (GELU, GELU', bias gradient) apply to 16-B vectors with
+// coalesced loads of the saved pre-activation.  Epilogues:
+//   EPI_PLAIN  C = A·Bᵀ
+//   EPI_BIAS   C = A·Bᵀ + bias
+//   EPI_GELU   C = A·Bᵀ (the pre-activation, saved for backward) and
+//              Y = gelu(C + bias) — the fc1 forward with the bias-GELU pass fused
+//   EPI_DGELU  C = (A·Bᵀ) ⊙ gelu'(X + bias), X = the saved pre-activation (read
+//              through Y), and fp32 column partial sums of C for the bias
+//              gradient (one row per (M-tile, wave)) — the fc2 input-gradient
+//              GEMM with the bias-GELU backward pass fused
+// Rounding matches the unfused path bit for bit: the GEMM result is rounded to
+// bf16 before the activation math, as when it made an HBM round trip.
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int TILE = 256 * BK;  // elements of one operand tile [256 rows][64]
+constexpr int NTHR = 512;
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16-B chunk swizzle of a 128-B LDS row (attention.hip's toff)
+__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                       int lda, int ldb, int M, int N, int nk, bf16* __restrict__ C,
+                                                       int ldc, const bf16* __restrict__ bias, bf16* __restrict__ Y,
+                                                       int ldy, float* __restrict__ dbias_part) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [stage][A|B][256][64]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int li = lane & 31, hh = lane >> 5;
+  const int tiles_n = N / BN;
+  const int nwg = (M / BM) * tiles_n;
+  // XCD remap (gemm_dw.hip): each XCD gets a contiguous range of logical ids,
+  // i.e. the N-tiles of a few A row panels, which then share its L2
+  int id = blockIdx.x;
+  {
+    const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // LDS-DMA: one wave-instruction fills 1 KiB = 8 rows of 128 B; lane l →
+  // row 8·(4w+i) + (l>>3), LDS chunk l&7, holding global chunk (l&7) ^ swz(row)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const bf16* srcA[4];
+  const bf16* srcB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 8 * (4 * w + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ swz(r);
+    srcA[i] = A + (size_t)(m0 + r) * lda + ch * 8;
+    srcB[i] = B + (size_t)(n0 + r) * ldb + ch * 8;
+  }
+  // row fragment of k-substep ks (16 k): lane reads row rbase + li, chunk 2ks + hh;
+  // swz(rbase + li) = swz(li) for rbase % 32 == 0, so rbase is a ds_read immediate
+  int fo[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) fo[ks] = li * BK + (((2 * ks + hh) ^ swz(li)) << 3);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem;
+  auto glds = [](const bf16* src, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_byte)
+                 : "memory");
+  };
+  auto load_half = [&](int kt, int buf, int h) {
+    const unsigned abase = lds0 + (unsigned)(buf * 2 * TILE) * 2u, bbase = abase + TILE * 2u;
+#pragma unroll
+    for (int i = 2 * h; i < 2 * h + 2; ++i) {
+      const unsigned off = (unsigned)((4 * wu + i) * 1024);
+      glds(srcA[i] + (size_t)kt * BK, abase + off);
+      glds(srcB[i] + (size_t)kt * BK, bbase + off);
+    }
+  };
+  // Schedule as gemm_dw.hip (see the hazard argument there): waves 4-7 run one
+  // barrier interval behind waves 0-3; per 16-k step R (6 row reads [+ DMA];
+  // lgkmcnt(0)) | barrier | M (8 MFMAs) | barrier; next tile's DMA in steps
+  // 0-1, drained in step 3's R.  (A 4-stage BK=32 ring with one barrier per
+  // 16 MFMAs and no ping-pong measured 4-10 % slower: 1.03-1.05 vs 1.10-1.14 PF.)
+  load_half(0, 0, 0);
+  load_half(0, 0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const bool g1 = wu >= 4;
+  if (g1) __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < nk;
+    const bf16* As = smem + buf * 2 * TILE + wm * 128 * BK;
+    const bf16* Bs = smem + buf * 2 * TILE + TILE + wn * 64 * BK;
+#define PDO_NT_PP(KS, PRE)                                                                         \
+    {                                                                                              \
+      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(As + 0 * 32 * BK + fo[KS]);              \
+      const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(As + 1 * 32 * BK + fo[KS]);              \
+      const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(As + 2 * 32 * BK + fo[KS]);              \
+      const bf16x8 x3 = *reinterpret_cast<const bf16x8*>(As + 3 * 32 * BK + fo[KS]);              \
+      const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(Bs + 0 * 32 * BK + fo[KS]);              \
+      const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(Bs + 1 * 32 * BK + fo[KS]);              \
+      PRE                                                                                          \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      __builtin_amdgcn_s_barrier();                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      __builtin_amdgcn_s_setprio(1);                                                               \
+      acc[0][0] = mfma(w0, x0, acc[0][0]);                                                         \
+      acc[0][1] = mfma(w1, x0, acc[0][1]);                                                         \
+      acc[1][0] = mfma(w0, x1, acc[1][0]);                                                         \
+      acc[1][1] = mfma(w1, x1, acc[1][1]);                                                         \
+      acc[2][0] = mfma(w0, x2, acc[2][0]);                                                         \
+      acc[2][1] = mfma(w1, x2, acc[2][1]);                                                         \
+      acc[3][0] = mfma(w0, x3, acc[3][0]);                                                         \
+      acc[3][1] = mfma(w1, x3, acc[3][1]);                                                         \
+      __builtin_amdgcn_s_setprio(0);                                                               \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      __builtin_amdgcn_s_barrier();                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+    }
+    PDO_NT_PP(0, if (more) load_half(kt + 1, buf ^ 1, 0);)
+    PDO_NT_PP(1, if (more) load_half(kt + 1, buf ^ 1, 1);)
+    PDO_NT_PP(2, )
+    PDO_NT_PP(3, asm volatile("s_waitcnt vmcnt(0)" ::: "memory");)
+#undef PDO_NT_PP
+  }
+  if (!g1) __builtin_amdgcn_s_barrier();  // balance the stagger
+
+  // ---- epilogue ----
+  // acc[i][j][4g + e] = C[m][n], m = wm·128 + 32i + li, n = wn·64 + 32j + 8g + 4hh + e
+  // (tile-relative).  Stage the bf16 tile through LDS — [256][256] = 128 KiB,
+  // the whole array, free once every wave passed the loop's last barrier — and
+  // write it back as 512-B rows, 16 B per lane (the accumulator layout would
+  // scatter 8-B pieces over 32 rows per instruction).  LDS image: 16-B chunk
+  // c of row m at chunk c ^ (m & 31), so the 8-B writes (16 rows per lane
+  // group) and the 16-B row reads are both conflict-free.
+  __syncthreads();
+  unsigned char* lds = reinterpret_cast<unsigned char*>(smem);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == 1) {  // bias before the rounding, as a library bias epilogue
+        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * 64 + 32 * j + 8 * g + 4 * hh);
+        bv = f32x4{(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
+      }
+      const int c = wn * 8 + 4 * j + g;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = wm * 128 + 32 * i + li;
+        const f32x16& a = acc[i][j];
+        const bf16x4 o = {(bf16)(a[4 * g] + bv[0]), (bf16)(a[4 * g + 1] + bv[1]), (bf16)(a[4 * g + 2] + bv[2]),
+                          (bf16)(a[4 * g + 3] + bv[3])};
+        *reinterpret_cast<bf16x4*>(lds + m * 512 + ((c ^ (m & 31)) << 4) + 8 * hh) = o;
+      }
+    }
+  __syncthreads();
+  // row phase: thread t owns 16-B column chunk t & 31 of rows 16·it + (t >> 5)
+  const int c = tid & 31, r0 = tid >> 5;
+  const int n = n0 + 8 * c;
+  f32x8 bv8;
+  if constexpr (EPI >= 2) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
+  f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int r = 16 * it + r0;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + r * 512 + ((c ^ (r & 31)) << 4));
+    const size_t m = (size_t)(m0 + r);
+    if constexpr (EPI <= 1) {
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+    } else if constexpr (EPI == 2) {
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+      const f32x8 x = to_f32(v) + bv8;
+      f32x8 y;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
+      *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
+    } else {
+      const f32x8 x = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n)) + bv8;
+      const f32x8 dy = to_f32(v);
+      f32x8 d;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = dy[e] * gelu_sig_grad(x[e]);
+      colp += d;
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(d);
+    }
+  }
+  if constexpr (EPI == 3) {
+    // lanes l and l+32 share a column chunk: one fp32 partial row per wave
+#pragma unroll
+    for (int e = 0; e < 8; ++e) colp[e] += __shfl_xor(colp[e], 32, 64);
+    if (lane < 32) {
+      float* prow = dbias_part + (size_t)(8 * tm + w) * N + n;
+      *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
+      *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
+    }
+  }
+}
+
+}  // namespace
+
+int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
+  return M > 0 && N > 0 && K >= BK && M % BM == 0 && N % BN == 0 && K % BK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         ldc % 4 == 0 && lda >= K && ldb >= K && ldc >= N;
+}
+
+int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
+
+int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
+            const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
+  if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
+  if (epi != 0 && !bias) return -3;
+  if ((epi == 2 || epi == 3) && (!Y || ldy % 4 || ldy < N)) return -3;
+  if (epi == 3 && !dbias_part) return -3;
+  const long long grid = (long long)(M / BM) * (N / BN);
+  if (grid > 0x7fffffffLL) return -2;
+  const int nk = K / BK;
+  switch (epi) {
+    case 0: gemm_nt_kernel<0><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 1: gemm_nt_kernel<1><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 2: gemm_nt_kernel<2><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 3: gemm_nt_kernel<3><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    default: return -4;
+  }
+  return 0;
+}
+
+}  // namespace pdo

@@ -63,6 +63,13 @@ int gemm_dw_splits(long long T, int M, int N);
 int gemm_dw(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
             int accumulate, bf16* ws, int splits, hipStream_t st);
 // transpose.hip: out[C][R] = in[R][C], R and C multiples of 64
+// gemm_nt.hip: C[M][N] = A[M][K]·B[N][K]ᵀ with a fused epilogue
+// (0 plain, 1 +bias, 2 C = pre-activation & Y = gelu(C + bias),
+//  3 C = (A·Bᵀ)⊙gelu'(Y + bias) & fp32 column partials [gemm_nt_dbias_rows(M)][N])
+int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc);
+int gemm_nt_dbias_rows(int M);
+int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
+            const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 

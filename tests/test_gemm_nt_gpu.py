@@ -1,0 +1,73 @@
+"""gemm_nt (csrc/hip/gemm_nt.hip) numerics against plain PyTorch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from paddle_operator_amd import _native
+    return _native.require_hip()
+
+
+def _mk(M, N, K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16, generator=g) * 0.1
+    return x, w, b
+
+
+def _gelu_grad(x):
+    x = x.detach().requires_grad_(True)
+    (g,) = torch.autograd.grad(F.gelu(x, approximate="tanh").sum(), x)
+    return g
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (768, 256, 192), (512, 1024, 256), (2304, 512, 128)])
+def test_plain_and_bias(hip, M, N, K):
+    x, w, b = _mk(M, N, K)
+    ref = x.float() @ w.float().t()
+    c = hip.gemm_nt(x, w)
+    torch.testing.assert_close(c.float(), ref, atol=2e-2, rtol=1e-2)
+    cb = hip.gemm_nt(x, w, b)
+    torch.testing.assert_close(cb.float(), ref + b.float(), atol=2e-2, rtol=1e-2)
+
+
+def test_gelu_epilogue(hip):
+    M, N, K = 1024, 512, 256
+    x, w, b = _mk(M, N, K, 1)
+    pre, y = hip.gemm_nt_gelu(x, w, b)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(pre.float(), ref, atol=2e-2, rtol=1e-2)
+    # the activation is computed from the bf16-rounded pre-activation (as the unfused path)
+    torch.testing.assert_close(y.float(), F.gelu(pre.float() + b.float(), approximate="tanh"), atol=1e-2, rtol=1e-2)
+    # and bit-identical to the standalone HIP bias-GELU kernel on the same input
+    assert torch.equal(y, hip.bias_gelu_fwd(pre, b))
+
+
+def test_dgelu_epilogue_and_bias_grad(hip):
+    M, N, K = 1024, 512, 256
+    x, w, b = _mk(M, N, K, 2)
+    pre = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    dx, db = hip.gemm_nt_dgelu(x, w, pre, b)
+    dy = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    ref = dy * _gelu_grad(pre.float() + b.float())
+    torch.testing.assert_close(dx.float(), ref, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(db.float(), ref.sum(0), atol=0.5, rtol=2e-2)
+    # accumulate into an existing (arena) gradient
+    acc = torch.ones(N, device="cuda", dtype=torch.bfloat16)
+    (dx2,) = hip.gemm_nt_dgelu(x, w, pre, b, db_out=acc)
+    assert torch.equal(dx2, dx)
+    torch.testing.assert_close(acc.float(), 1.0 + ref.sum(0), atol=0.5, rtol=2e-2)
+
+
+def test_rejects_unsupported_shapes(hip):
+    assert not hip.gemm_nt_supported(300, 256, 64)
+    assert not hip.gemm_nt_supported(256, 256, 96)
+    assert hip.gemm_nt_supported(65536, 4096, 1024)
+    x, w, _ = _mk(320, 256, 64)
+    with pytest.raises(RuntimeError):
+        hip.gemm_nt(x, w)

@@ -1,0 +1,21 @@
+"""Minimal driver for PMC passes: gemm_nt and hipBLASLt on one GPT-2 shape.
+    python tools/nt_only.py [N] [K] [iters]"""
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from paddle_operator_amd import _native  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+it = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+m = _native.require_hip()
+x = torch.randn(65536, K, device="cuda", dtype=torch.bfloat16)
+w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
+for _ in range(it):
+    m.gemm_nt(x, w)
+    F.linear(x, w)
+torch.cuda.synchronize()
