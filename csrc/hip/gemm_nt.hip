@@ -34,32 +34,22 @@ namespace pdo {
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int TILE = 256 * BK;  // elements of one operand tile [256 rows][64]
+constexpr int BM = 256, BN = 256, BK = 32;
+constexpr int STAGES = 5;  // 5 × 32 KiB = the whole 160 KiB LDS
+constexpr int TILE = 256 * BK;  // elements of one operand tile [256 rows][32]
 constexpr int NTHR = 512;
 
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// 16-B chunk swizzle of a 128-B LDS row (attention.hip's toff)
-__device__ __forceinline__ int swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
-
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
+// 16-B chunk swizzle of a 64-B LDS row: a ds_read_b128 lane group reads the
+// 4 chunks of 4 rows ({0-3,12-15,20-27}-style groups); chunk ^= (r>>1)&3 puts
+// every group's 16 (row & 3, chunk) pairs on 16 distinct bank slots
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 3; }
 
 template <int EPI>
 __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                        int lda, int ldb, int M, int N, int nk, bf16* __restrict__ C,
                                                        int ldc, const bf16* __restrict__ bias, bf16* __restrict__ Y,
                                                        int ldy, float* __restrict__ dbias_part) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // [stage][A|B][256][64]
+  __shared__ __attribute__((aligned(16))) bf16 smem[STAGES * 2 * TILE];  // [stage][A|B][256][32]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int li = lane & 31, hh = lane >> 5;
@@ -75,29 +65,28 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
   const int tn = id % tiles_n, tm = id / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // LDS-DMA: one wave-instruction fills 1 KiB = 8 rows of 128 B; lane l →
-  // row 8·(4w+i) + (l>>3), LDS chunk l&7, holding global chunk (l&7) ^ swz(row)
+  // LDS-DMA: one wave-instruction fills 1 KiB = 16 rows of 64 B; lane l →
+  // row 16·(2w+i) + (l>>2), LDS chunk l&3, holding global chunk (l&3) ^ swz(row)
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  const bf16* srcA[4];
-  const bf16* srcB[4];
+  const bf16* srcA[2];
+  const bf16* srcB[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 8 * (4 * w + i) + (lane >> 3);
-    const int ch = (lane & 7) ^ swz(r);
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * (2 * w + i) + (lane >> 2);
+    const int ch = (lane & 3) ^ swz(r);
     srcA[i] = A + (size_t)(m0 + r) * lda + ch * 8;
     srcB[i] = B + (size_t)(n0 + r) * ldb + ch * 8;
   }
-  // row fragment of k-substep ks (16 k): lane reads row rbase + li, chunk 2ks + hh;
-  // swz(rbase + li) = swz(li) for rbase % 32 == 0, so rbase is a ds_read immediate
-  int fo[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) fo[ks] = li * BK + (((2 * ks + hh) ^ swz(li)) << 3);
+  // 16x16x32 fragment: lane reads row rbase + (l&15), chunk l>>4 (the whole
+  // 32-k row); swz depends on row bits 1-2 only, so rbase (% 16) is a ds_read
+  // immediate and every fragment of an operand shares one per-lane offset
+  const int fo = (lane & 15) * BK + (((lane >> 4) ^ swz(lane & 15)) << 3);
 
-  f32x16 acc[4][2];
+  f32x4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem;
   auto glds = [](const bf16* src, unsigned lds_byte) {
@@ -107,95 +96,90 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
                  : "v"(src), "s"(lds_byte)
                  : "memory");
   };
-  auto load_half = [&](int kt, int buf, int h) {
-    const unsigned abase = lds0 + (unsigned)(buf * 2 * TILE) * 2u, bbase = abase + TILE * 2u;
+  // one 32-k stage = 4 DMA wave-instructions per wave (2 A + 2 B)
+  auto load_stage = [&](int s) {
+    const unsigned abase = lds0 + (unsigned)((s % STAGES) * 2 * TILE) * 2u, bbase = abase + TILE * 2u;
 #pragma unroll
-    for (int i = 2 * h; i < 2 * h + 2; ++i) {
-      const unsigned off = (unsigned)((4 * wu + i) * 1024);
-      glds(srcA[i] + (size_t)kt * BK, abase + off);
-      glds(srcB[i] + (size_t)kt * BK, bbase + off);
+    for (int i = 0; i < 2; ++i) {
+      const unsigned off = (unsigned)((2 * wu + i) * 1024);
+      glds(srcA[i] + (size_t)s * BK, abase + off);
+      glds(srcB[i] + (size_t)s * BK, bbase + off);
     }
   };
-  // Schedule as gemm_dw.hip (see the hazard argument there): waves 4-7 run one
-  // barrier interval behind waves 0-3; per 16-k step R (6 row reads [+ DMA];
-  // lgkmcnt(0)) | barrier | M (8 MFMAs) | barrier; next tile's DMA in steps
-  // 0-1, drained in step 3's R.  (A 4-stage BK=32 ring with one barrier per
-  // 16 MFMAs and no ping-pong measured 4-10 % slower: 1.03-1.05 vs 1.10-1.14 PF.)
-  load_half(0, 0, 0);
-  load_half(0, 0, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // wait until this wave's DMA for stage `s` landed, given stages ≤ last issued
+  auto wait_stage = [](int after) {  // after = stages issued after it (0..STAGES-2)
+    static_assert(STAGES == 5, "wait_stage covers 0..3 stages in flight after the awaited one");
+    if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // Ping-pong over a STAGES-deep ring of 32-k stages: waves 4-7 run one barrier
+  // interval behind waves 0-3, so on every SIMD one wave issues its 32 MFMAs
+  // while the other issues the next stage's 12 row reads.  Per stage s:
+  // R (12 reads; DMA of stage s+STAGES-1 into the buffer of s-1, whose last reads
+  // retired before the previous barrier; wait for this wave's DMA of stage
+  // s+1; lgkmcnt(0)) | barrier | M (32 MFMAs) | barrier.  Stage s+1 is read
+  // two barriers after every wave waited for its share of it.
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (t < nk) load_stage(t);
+  wait_stage(min(nk - 1, STAGES - 2));
   __builtin_amdgcn_s_barrier();
   const bool g1 = wu >= 4;
   if (g1) __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const bool more = kt + 1 < nk;
-    const bf16* As = smem + buf * 2 * TILE + wm * 128 * BK;
-    const bf16* Bs = smem + buf * 2 * TILE + TILE + wn * 64 * BK;
-#define PDO_NT_PP(KS, PRE)                                                                         \
-    {                                                                                              \
-      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(As + 0 * 32 * BK + fo[KS]);              \
-      const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(As + 1 * 32 * BK + fo[KS]);              \
-      const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(As + 2 * 32 * BK + fo[KS]);              \
-      const bf16x8 x3 = *reinterpret_cast<const bf16x8*>(As + 3 * 32 * BK + fo[KS]);              \
-      const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(Bs + 0 * 32 * BK + fo[KS]);              \
-      const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(Bs + 1 * 32 * BK + fo[KS]);              \
-      PRE                                                                                          \
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
-      __builtin_amdgcn_s_barrier();                                                                \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
-      __builtin_amdgcn_s_setprio(1);                                                               \
-      acc[0][0] = mfma(w0, x0, acc[0][0]);                                                         \
-      acc[0][1] = mfma(w1, x0, acc[0][1]);                                                         \
-      acc[1][0] = mfma(w0, x1, acc[1][0]);                                                         \
-      acc[1][1] = mfma(w1, x1, acc[1][1]);                                                         \
-      acc[2][0] = mfma(w0, x2, acc[2][0]);                                                         \
-      acc[2][1] = mfma(w1, x2, acc[2][1]);                                                         \
-      acc[3][0] = mfma(w0, x3, acc[3][0]);                                                         \
-      acc[3][1] = mfma(w1, x3, acc[3][1]);                                                         \
-      __builtin_amdgcn_s_setprio(0);                                                               \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
-      __builtin_amdgcn_s_barrier();                                                                \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
-    }
-    PDO_NT_PP(0, if (more) load_half(kt + 1, buf ^ 1, 0);)
-    PDO_NT_PP(1, if (more) load_half(kt + 1, buf ^ 1, 1);)
-    PDO_NT_PP(2, )
-    PDO_NT_PP(3, asm volatile("s_waitcnt vmcnt(0)" ::: "memory");)
-#undef PDO_NT_PP
+  for (int s = 0; s < nk; ++s) {
+    const bf16* As = smem + (s % STAGES) * 2 * TILE + wm * 128 * BK + fo;
+    const bf16* Bs = smem + (s % STAGES) * 2 * TILE + TILE + wn * 64 * BK + fo;
+    bf16x8 xf[8], wf[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * BK);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = *reinterpret_cast<const bf16x8*>(Bs + j * 16 * BK);
+    if (s + STAGES - 1 < nk) load_stage(s + STAGES - 1);
+    if (s + 1 < nk) wait_stage(min(nk - 1, s + STAGES - 1) - (s + 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (!g1) __builtin_amdgcn_s_barrier();  // balance the stagger
 
   // ---- epilogue ----
-  // acc[i][j][4g + e] = C[m][n], m = wm·128 + 32i + li, n = wn·64 + 32j + 8g + 4hh + e
+  // acc[i][j][e] = C[m][n], m = wm·128 + 16i + (l&15), n = wn·64 + 16j + 4(l>>4) + e
   // (tile-relative).  Stage the bf16 tile through LDS — [256][256] = 128 KiB,
   // the whole array, free once every wave passed the loop's last barrier — and
   // write it back as 512-B rows, 16 B per lane (the accumulator layout would
-  // scatter 8-B pieces over 32 rows per instruction).  LDS image: 16-B chunk
+  // scatter 8-B pieces over 16 rows per instruction).  LDS image: 16-B chunk
   // c of row m at chunk c ^ (m & 31), so the 8-B writes (16 rows per lane
   // group) and the 16-B row reads are both conflict-free.
   __syncthreads();
   unsigned char* lds = reinterpret_cast<unsigned char*>(smem);
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == 1) {  // bias before the rounding, as a library bias epilogue
-        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * 64 + 32 * j + 8 * g + 4 * hh);
-        bv = f32x4{(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
-      }
-      const int c = wn * 8 + 4 * j + g;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = wm * 128 + 32 * i + li;
-        const f32x16& a = acc[i][j];
-        const bf16x4 o = {(bf16)(a[4 * g] + bv[0]), (bf16)(a[4 * g + 1] + bv[1]), (bf16)(a[4 * g + 2] + bv[2]),
-                          (bf16)(a[4 * g + 3] + bv[3])};
-        *reinterpret_cast<bf16x4*>(lds + m * 512 + ((c ^ (m & 31)) << 4) + 8 * hh) = o;
-      }
+  for (int j = 0; j < 4; ++j) {
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == 1) {  // bias before the rounding, as a library bias epilogue
+      const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * 64 + 16 * j + 4 * (lane >> 4));
+      bv = f32x4{(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
     }
+    const int c = wn * 8 + 2 * j + (lane >> 5);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = wm * 128 + 16 * i + (lane & 15);
+      const f32x4 a = acc[i][j] + bv;
+      const bf16x4 o = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+      *reinterpret_cast<bf16x4*>(lds + m * 512 + ((c ^ (m & 31)) << 4) + 8 * ((lane >> 4) & 1)) = o;
+    }
+  }
   __syncthreads();
   // row phase: thread t owns 16-B column chunk t & 31 of rows 16·it + (t >> 5)
   const int c = tid & 31, r0 = tid >> 5;
@@ -242,7 +226,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 }  // namespace
 
 int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
-  return M > 0 && N > 0 && K >= BK && M % BM == 0 && N % BN == 0 && K % BK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+  return M > 0 && N > 0 && K >= 64 && M % BM == 0 && N % BN == 0 && K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          ldc % 4 == 0 && lda >= K && ldb >= K && ldc >= N;
 }
 

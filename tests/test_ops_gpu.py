@@ -435,6 +435,30 @@ def test_fused_mlp_epilogues(cuda, T, C):
 
 
 @pytest.mark.gpu
+def test_mlp_nt_dgelu_matches_unfused(cuda):
+    """fc2 input gradient with the fused GELU' epilogue (gemm_nt) == hipBLASLt + bias-GELU kernel."""
+    ops = _ops()
+    T, C = 4096, 512
+    g = torch.Generator(device=cuda).manual_seed(5)
+    base = [(0.05 * torch.randn(T, C, device=cuda, generator=g)).bfloat16() * 20,
+            (0.05 * torch.randn(4 * C, C, device=cuda, generator=g)).bfloat16(),
+            (0.1 * torch.randn(4 * C, device=cuda, generator=g)).bfloat16(),
+            (0.05 * torch.randn(C, 4 * C, device=cuda, generator=g)).bfloat16()]
+    dy = torch.randn(T, C, device=cuda, generator=g).bfloat16()
+    grads = []
+    for fused in (True, False):
+        ops._NT_DGELU[0] = fused
+        try:
+            ts = [t.clone().requires_grad_() for t in base]
+            ops.mlp(*ts).backward(dy)
+        finally:
+            ops._NT_DGELU[0] = True
+        grads.append([t.grad.float() for t in ts])
+    for a, b, name in zip(grads[0], grads[1], ("dx", "dw1", "db1", "dw2")):
+        assert rel_err(a, b) < 1e-2, name
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N,C,H,relu,res", [(8, 64, 28, True, False), (4, 256, 14, True, True),
                                               (16, 128, 7, False, False), (2, 2048, 7, True, True),
                                               (4, 24, 9, True, False), (3, 40, 5, True, True)])
