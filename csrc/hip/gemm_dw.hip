@@ -23,7 +23,10 @@
 // round; workgroup ids remapped so the workgroups sharing an A or B panel run
 // on one XCD (shared L2).  Measured: 1.05-1.21 PF vs hipBLASLt's 0.86-1.15 PF
 // on the same shapes (tools/dw_probe.py --pdo-only); the register-staged and
-// plain LDS-DMA 2-barrier versions of this tiling ran 0.92-0.95 PF.
+// plain LDS-DMA 2-barrier versions of this tiling ran 0.92-0.95 PF, and a
+// 16x16x32 version over a 5-deep ring of 32-token stages (gemm_nt.hip's
+// schedule, which gained 5 % there) ran 8-20 % slower here: qkv 445, proj
+// 165, fc1 546, fc2 523 µs (tools/gpu_dw.sh).
 #include "common.h"
 #include "kernels.h"
 
