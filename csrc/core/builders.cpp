@@ -256,14 +256,20 @@ static bool is_ipv4_like(const std::string& ip) {
   return dots == 3;  // strings.Split(ip, ".") has 4 parts (paddlejob_helper.go:226)
 }
 
-Value construct_configmap(const PaddleJob& job, const std::vector<Value>& pods) {
+Value construct_configmap(const PaddleJob& job, const std::vector<Value>& pods, bool host_port_endpoints) {
   std::map<std::string, std::vector<std::string>> eps;
   for (auto& r : api::role_order()) {
     const api::ResourceSpec* rs = job.spec.role(r);
     if (rs) eps[r] = std::vector<std::string>(rs->replicas > 0 ? rs->replicas : 0);
   }
   const bool svc = job.spec.intranet == api::intranet::Service;
-  const std::string port = std::to_string(api::kPaddlePort);
+  // D-5: the reference writes :2379 into every endpoint even in Host mode,
+  // where the ranks listen on the allocated block (PADDLE_PORT); fast mode
+  // advertises the block's base port, compat mode keeps the reference value
+  const bool host = job.spec.intranet == api::intranet::Host;
+  const std::string hp = host ? job.annotation(api::kAnnotationHostPort) : std::string();
+  const int base = host_port_endpoints && !hp.empty() ? std::atoi(hp.c_str()) : api::kPaddlePort;
+  const std::string port = std::to_string(base);
   for (auto& pod : pods) {
     const std::string& ip = pod.at_path("status.podIP").as_string();
     if (!is_ipv4_like(ip)) return Value();
@@ -283,7 +289,7 @@ Value construct_configmap(const PaddleJob& job, const std::vector<Value>& pods) 
   md["annotations"] = Value::object();
   Value& data = cm["data"];
   data["TRAINER_PORTS_NUM"] = std::to_string(api::kPortsPerPod);
-  data["PADDLE_PORT"] = job.spec.intranet == api::intranet::Host ? job.annotation(api::kAnnotationHostPort) : port;
+  data["PADDLE_PORT"] = host ? hp : port;
   if (job.spec.role(api::kRolePS)) data["PADDLE_PSERVERS_IP_PORT_LIST"] = join(eps[api::kRolePS], ",");
   if (const api::ResourceSpec* w = job.spec.role(api::kRoleWorker)) {
     data["PADDLE_TRAINER_ENDPOINTS"] = join(eps[api::kRoleWorker], ",");
@@ -296,7 +302,7 @@ Value construct_configmap(const PaddleJob& job, const std::vector<Value>& pods) 
     data["PADDLE_WITH_GLOO"] = std::to_string(*job.spec.with_gloo);
     data["PADDLE_GLOO_RENDEZVOUS"] = "3";
     std::string ep = ps->second[0];
-    const std::string from = ":" + port, to = ":" + std::to_string(api::kPaddlePort + api::kPortsPerPod - 2);
+    const std::string from = ":" + port, to = ":" + std::to_string(base + api::kPortsPerPod - 2);
     size_t at = ep.find(from);
     if (at != std::string::npos) ep.replace(at, from.size(), to);
     data["PADDLE_GLOO_HTTP_ENDPOINT"] = ep;

@@ -63,8 +63,11 @@ bool without_volcano(const api::PaddleJob& job);
 
 // full pod as the reconciler creates it (constructPod + createPod additions)
 Value construct_pod(const api::PaddleJob& job, const std::string& role, int idx, const Options& opt);
-// nullptr-equivalent (Null value) when some pod has no IPv4 yet
-Value construct_configmap(const api::PaddleJob& job, const std::vector<Value>& pods);
+// nullptr-equivalent (Null value) when some pod has no IPv4 yet.
+// host_port_endpoints: Host-mode endpoints carry the job's allocated host port
+// (fast mode) instead of the reference's fixed :2379 (SURVEY D-5, compat mode)
+Value construct_configmap(const api::PaddleJob& job, const std::vector<Value>& pods,
+                          bool host_port_endpoints = false);
 Value construct_service_for_pod(const Value& pod);
 Value construct_podgroup(const api::PaddleJob& job, bool rewrite_gpu = true);
 Value pg_min_resources(const api::PaddleJob& job, bool rewrite_gpu = true);

@@ -286,7 +286,7 @@ Plan reconcile(const Observed& obs, const Options& opt, HostPorts* ports, double
 
   // ---------------------------------------------------------- 13. configmap
   if (!job.spec.elastic && fsm::all_pods_ready(job, obs.pods) && !obs.configmap_exists) {
-    Value cm = build::construct_configmap(job, obs.pods);
+    Value cm = build::construct_configmap(job, obs.pods, /*host_port_endpoints=*/!compat);
     if (cm.is_null()) {
       p.requeue = true;
       p.step = "configmap/wait-ipv4";

@@ -182,6 +182,8 @@ def test_collective_hostnetwork_volcano_lifecycle():
     assert 40000 <= port < 40100
     cm = cl.get("ConfigMap", "coll")["data"]
     assert cm["PADDLE_PORT"] == str(port)
+    # fast mode fixes D-5: Host-mode endpoints carry the allocated port, not :2379
+    assert all(ep.endswith(f":{port}") for ep in cm["PADDLE_TRAINER_ENDPOINTS"].split(","))
     p = cl.get("Pod", "coll-worker-1")
     assert p["spec"]["hostNetwork"] is True and p["spec"]["schedulerName"] == "volcano"
     pg = cl.get("PodGroup", "coll")
