@@ -124,6 +124,54 @@ __device__ __forceinline__ void store_acc_rows(bf16* dst_row, const f32x16& acc,
   }
 }
 
+// Column sums over the workgroup's 128 token rows (the QKV bias gradient,
+// fused into the backward kernels).  Lane (li, hh) holds row li, columns
+// 32a + 8g + 4hh + e in pair member a, register 4g + e — per half-wave 32
+// values for 32 distinct columns.  A butterfly reduce-scatter (send one half
+// of the vector to the xor partner, add the partner's other half) needs 16
+// shuffles per accumulator instead of 16 × 5.  The 4 waves then add through LDS
+// (free at the call: after the loop's last barrier).
+// one 32x32 accumulator (columns c0 + 8g + 4hh + e in register 4g + e) →
+// this wave's 32 column sums in red[c0 + …].  Butterfly over lane bits 3..0
+// (16 live values at most), then one xor-16 add joins the two 16-row groups.
+template <int O>
+__device__ __forceinline__ void bfly_step(float (&v)[16], int li) {
+  // compile-time O: every v[] index is a constant (a runtime step count would
+  // turn them into 16-way select chains)
+  const bool hi = li & O;
+#pragma unroll
+  for (int k = 0; k < O; ++k) {
+    const float send = hi ? v[k] : v[k + O];
+    const float keep = hi ? v[k + O] : v[k];
+    v[k] = keep + __shfl_xor(send, O, 64);
+  }
+}
+
+__device__ __forceinline__ void colsum_acc(const f32x16& acc, int c0, float sc, float* red, int lane) {
+  const int hh = lane >> 5, li = lane & 31;
+  float v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = acc[r];
+  bfly_step<8>(v, li);
+  bfly_step<4>(v, li);
+  bfly_step<2>(v, li);
+  bfly_step<1>(v, li);
+  const float t = v[0] + __shfl_xor(v[0], 16, 64);
+  // lane li (< 16) holds register index li = 4g + e → column c0 + 8g + 4hh + e
+  if (li < 16) red[c0 + 8 * (li >> 2) + 4 * hh + (li & 3)] = t * sc;
+}
+
+// after colsum_acc of NP 64-column slots by every wave (red = [4 waves][NP·64]): add the
+// 4 waves and write slot p's 64 sums to out[p]
+template <int NP>
+__device__ __forceinline__ void colsum_finish(const float* red, float* const (&out)[NP], int tid) {
+  __syncthreads();
+  for (int c = tid; c < 64 * NP; c += 256) {
+    const float t = red[c] + red[64 * NP + c] + red[2 * 64 * NP + c] + red[3 * 64 * NP + c];
+    out[c >> 6][c & 63] = t;
+  }
+}
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -279,7 +327,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                          const float* __restrict__ lse, const float* __restrict__ delta,
                                                          bf16* __restrict__ dqkv, int B, int S, int H, float c2,
-                                                         float scale) {
+                                                         float scale, float* __restrict__ dbias_part) {
   // [buf][Q|dO][64][64] bf16 + [buf][lse2|delta][64] f32
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD + 2 * 2 * TROWS * 2];
   float* sstat = reinterpret_cast<float*>(smem + 2 * 2 * TROWS * HD);
@@ -390,6 +438,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
   store_acc_rows(krow, dk1, 32, hh, scale);
   store_acc_rows(vrow, dv0, 0, hh, 1.f);
   store_acc_rows(vrow, dv1, 32, hh, 1.f);
+  if (dbias_part) {  // fp32 partial row b·(S/128) + kb of the QKV bias gradient, k and v slots
+    float* prow = dbias_part + (size_t)(b * (S / 128) + kb) * (3 * H * HD) + (size_t)h * HD;
+    float* red = reinterpret_cast<float*>(smem);
+    colsum_acc(dk0, 0, scale, red + w * 128, lane);
+    colsum_acc(dk1, 32, scale, red + w * 128, lane);
+    colsum_acc(dv0, 0, 1.f, red + w * 128 + 64, lane);
+    colsum_acc(dv1, 32, 1.f, red + w * 128 + 64, lane);
+    float* const out[2] = {prow + (size_t)H * HD, prow + (size_t)2 * H * HD};
+    colsum_finish<2>(red, out, tid);
+  }
 }
 
 // ============================================================================
@@ -398,7 +456,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
 __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
-                                                       int H, float c2, float scale) {
+                                                       int H, float c2, float scale, float* __restrict__ dbias_part) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
@@ -493,6 +551,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ 
   bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
   store_acc_rows(qrow, a0, 0, hh, scale);
   store_acc_rows(qrow, a1, 32, hh, scale);
+  if (dbias_part) {  // q slot of the QKV bias-gradient partial row b·(S/128) + qb
+    float* prow = dbias_part + (size_t)(b * (S / 128) + qb) * (3 * H * HD) + (size_t)h * HD;
+    float* red = reinterpret_cast<float*>(smem);
+    colsum_acc(a0, 0, scale, red + w * 64, lane);
+    colsum_acc(a1, 32, scale, red + w * 64, lane);
+    float* const out[1] = {prow};
+    colsum_finish<1>(red, out, tid);
+  }
 }
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
@@ -503,12 +569,12 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
 }
 
 int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse, float* delta, bf16* dqkv, int B,
-             int S, int H, int D, float scale, hipStream_t st) {
+             int S, int H, int D, float scale, hipStream_t st, float* dbias_part) {
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
-  attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale);
+  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part);
+  attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part);
   return 0;
 }
 

@@ -481,7 +481,10 @@ std::vector<at::Tensor> attn_fwd(at::Tensor qkv, int64_t n_head) {
   return {o, lse};
 }
 
-at::Tensor attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, at::Tensor lse, int64_t n_head) {
+// dqkv, plus (with_bias_grad) the QKV bias gradient reduced from the kernels'
+// fp32 column partials — accumulated into db_out when given, else returned
+std::vector<at::Tensor> attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, at::Tensor lse, int64_t n_head,
+                                 bool with_bias_grad, c10::optional<at::Tensor> db_out) {
   CHECK_IN(dout); CHECK_IN(qkv); CHECK_IN(o); CHECK_IN(lse);
   CHECK_BF16(dout); CHECK_BF16(qkv); CHECK_BF16(o); CHECK_F32(lse);
   const int B = qkv.size(0), S = qkv.size(1), C = qkv.size(2) / 3, H = n_head, D = C / H;
@@ -489,9 +492,27 @@ at::Tensor attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, at::Tensor ls
   TORCH_CHECK(D == 64 && S % 128 == 0);
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  const int G = B * (S / 128), NC = 3 * C;
+  at::Tensor part;
+  if (with_bias_grad)
+    part = at::empty({(int64_t)G * NC + pdo::colsum_scratch_floats(G, NC)}, qkv.options().dtype(at::kFloat));
   CHECK_RC(pdo::attn_bwd(bp(dout), bp(qkv), bp(o), fp(lse), fp(delta), bp(dqkv), B, S, H, D,
-                         1.f / std::sqrt((float)D), cur_stream()), "attn_bwd");
-  return dqkv;
+                         1.f / std::sqrt((float)D), cur_stream(), with_bias_grad ? fp(part) : nullptr), "attn_bwd");
+  if (!with_bias_grad) return {dqkv};
+  at::Tensor db;
+  pdo::ColOut co;
+  if (db_out.has_value()) {
+    db = *db_out;
+    CHECK_IN(db); CHECK_BF16(db); TORCH_CHECK(db.numel() == NC);
+    co = pdo::ColOut::one(bp(db), NC);
+    co.acc = 1;
+  } else {
+    db = at::empty({NC}, qkv.options());
+    co = pdo::ColOut::one(bp(db), NC);
+  }
+  pdo::colsum(fp(part), G, NC, NC, co, fp(part) + (size_t)G * NC, cur_stream());
+  if (db_out.has_value()) return {dqkv};
+  return {dqkv, db};
 }
 
 // ---------------------------------------------------------------- bucket helpers
@@ -647,7 +668,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
   });
   m.def("matmul_dgelu", &matmul_dgelu);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("n_head"),
+        py::arg("with_bias_grad") = false, py::arg("db_out") = py::none());
   m.def("scale_", &scale_);
   m.def("flatten_scale", &flatten_scale);
   m.def("device_info", &device_info);

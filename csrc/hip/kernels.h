@@ -99,8 +99,10 @@ int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, cons
 
 // attention.hip  (qkv: [B, S, 3, H, D] bf16; o: [B, S, H, D]; lse: [B, H, S] f32)
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st);
+// dbias_part (optional): fp32 [B·S/128][3·H·64] column partial sums of dqkv
+// (the QKV bias gradient before its final reduction)
 int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse, float* delta, bf16* dqkv, int B,
-             int S, int H, int D, float scale, hipStream_t st);
+             int S, int H, int D, float scale, hipStream_t st, float* dbias_part = nullptr);
 
 // bucket.hip (DDP helpers: multi-tensor flatten with fused scale / unflatten)
 int flatten_scale(const void* const* srcs, const long long* sizes, const long long* offsets, int n, bf16* dst,

@@ -105,7 +105,7 @@ class Block(nn.Module):
         its bias — the caller fuses ``x_mid + m + bias`` with the next LayerNorm.
         """
         cfg = self.cfg
-        a = ops.attention(self.qkv(h), cfg.n_head)
+        a = ops.qkv_attention(h, self.qkv.weight, self.qkv.bias, cfg.n_head)
         a = self.proj.forward_nobias(a)
         x, h2 = ops.add_layer_norm(x, a, self.ln2_w, self.ln2_b, cfg.ln_eps, rbias=self.proj.bias)
         m = ops.mlp(h2, self.fc.weight, self.fc.bias, self.fc_proj.weight)

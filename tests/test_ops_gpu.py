@@ -435,6 +435,36 @@ def test_fused_mlp_epilogues(cuda, T, C):
 
 
 @pytest.mark.gpu
+def test_qkv_attention_fused_bias_grad(cuda):
+    """QKV projection + attention node (bias gradient from the attention kernels'
+    column partials) == separate linear + attention nodes, and ≈ fp32."""
+    ops = _ops()
+    B, S, H, C = 2, 256, 4, 256
+    g = torch.Generator(device=cuda).manual_seed(21)
+    base = [torch.randn(B, S, C, device=cuda, generator=g).bfloat16(),
+            (0.05 * torch.randn(3 * C, C, device=cuda, generator=g)).bfloat16(),
+            (0.1 * torch.randn(3 * C, device=cuda, generator=g)).bfloat16()]
+    do = torch.randn(B, S, C, device=cuda, generator=g).bfloat16()
+    grads = []
+    for fused in (True, False):
+        ops._QKV_FUSED[0] = fused
+        try:
+            ts = [t.clone().requires_grad_() for t in base]
+            ops.qkv_attention(ts[0], ts[1], ts[2], H).backward(do)
+        finally:
+            ops._QKV_FUSED[0] = True
+        grads.append([t.grad.float() for t in ts])
+    for a, b, name in zip(grads[0], grads[1], ("dh", "dw", "db")):
+        assert rel_err(a, b) < 1e-2, name
+    ref = [t.detach().float().requires_grad_() for t in base]
+    qkv = ref[0] @ ref[1].t() + ref[2]
+    q, k, v = qkv.view(B, S, 3, H, C // H).permute(2, 0, 3, 1, 4).unbind(0)
+    o = ops.ref_attention(q, k, v, causal=True).transpose(1, 2).reshape(B, S, C)
+    o.backward(do.float())
+    assert rel_err(grads[0][2], ref[2].grad) < 3e-2
+
+
+@pytest.mark.gpu
 def test_mlp_nt_dgelu_matches_unfused(cuda):
     """fc2 input gradient with the fused GELU' epilogue (gemm_nt) == hipBLASLt + bias-GELU kernel."""
     ops = _ops()
