@@ -141,6 +141,8 @@ def report_ready(b: Bootstrapped, job_key: str, kv_endpoints: str = "", extra: O
     b.t_ready = time.time()
     rec = {"rank": b.rank, "world": b.world, "t_start": b.t_start, "t_pg": b.t_pg, "t_ready": b.t_ready,
            "host": socket.gethostname(), "pid": os.getpid(), "backend": b.backend}
+    if os.environ.get("PDO_ELASTIC_GEN"):
+        rec["gen"] = os.environ["PDO_ELASTIC_GEN"]
     if b.ipc_gbps is not None:
         rec["ipc_gbps"] = b.ipc_gbps
     if extra:

@@ -11,21 +11,27 @@ KV layout under ``/paddle/<job-id>/`` (pdo-kv, etcd-v3 JSON gateway):
 
 * ``np``                — desired world size; the agent creates it from
   PADDLE_ELASTIC_NP if absent (the controller never creates it, only updates).
-* ``nodes/<id>``        — membership, value ``{"id","host","port"}``, bound to a
-  lease of ``ttl`` seconds kept alive by the agent: a killed pod drops out
-  after ``ttl`` without anyone deleting it.
+* ``nodes/<id>``        — membership, value ``{"id","host","port","lease","inc"}``,
+  bound to a lease of ``ttl`` seconds kept alive by the agent: a killed pod
+  drops out after ``ttl`` without anyone deleting it.
 * ``rdzv/<gen>/<id>``   — per-generation arrival barrier.  ``gen`` is a digest
-  of (np, the first np member ids), so every agent that sees the same
-  membership computes the same generation, the same rank order and the same
-  TCPStore port (``PADDLE_PORT + 2 + gen % 16`` on rank 0's host; each pod owns
-  20 ports, paddlejob_helper.go:215-279).
+  of (np, the first np members' (id, lease, inc)), so every agent that sees
+  the same membership computes the same generation, the same rank order and
+  the same TCPStore port (``PADDLE_PORT + 2 + gen % 16`` on rank 0's host;
+  each pod owns 20 ports, paddlejob_helper.go:215-279).  A pod that was killed
+  and restarted in place (OnFailure, paddlejob_helper.go:366-374) comes back
+  with a new lease, and an agent whose worker crashed bumps ``inc``: either
+  way the generation id changes, so no stale arrival key or still-bound
+  TCPStore port of the previous generation can be mistaken for the new one.
 * ``done/<id>``         — written when a worker finished all steps.
 
 Loop: register → wait for ≥ np live members (``PADDLE_ELASTIC_TIMEOUT``) →
 barrier on ``rdzv/<gen>`` → spawn ``pdo-launch --worker`` with RANK/WORLD_SIZE/
 MASTER_* → watch np + membership every ``poll`` s; on change SIGTERM the
 worker (rank 0 checkpoints in its SIGTERM handler) and rendezvous again; on
-worker failure with unchanged membership restart it (``max_restarts``).
+worker failure, wait up to one lease TTL for the membership to change (a
+dead peer is the usual cause: its lease expires), otherwise count a restart
+(``max_restarts``) and bump ``inc`` so every peer re-forms the world.
 Workers resume from the newest checkpoint, whose flat-arena layout does not
 depend on the world size.
 """
@@ -64,6 +70,7 @@ class ElasticAgent:
         self.max_restarts = max_restarts
         self.prefix = f"/paddle/{job_id}/"
         self.lease = 0
+        self.inc = 0
         self._ka = None
         self.proc: Optional[subprocess.Popen] = None
         self.history: List[dict] = []
@@ -72,9 +79,18 @@ class ElasticAgent:
     def register(self):
         self.kv.put_if_absent(self.prefix + "np", str(self.np_default))
         self.lease = self.kv.lease_grant(self.ttl)
-        self.kv.put(self.prefix + f"nodes/{self.id:06d}",
-                    json.dumps({"id": self.id, "host": self.host, "port": self.port}), lease=self.lease)
+        self._announce()
         self._ka = self.kv.keepalive_thread(self.lease, self.ttl)
+
+    def _announce(self):
+        self.kv.put(self.prefix + f"nodes/{self.id:06d}",
+                    json.dumps({"id": self.id, "host": self.host, "port": self.port, "lease": self.lease,
+                                "inc": self.inc}), lease=self.lease)
+
+    def bump(self):
+        """This member's worker failed on its own: force a fresh generation."""
+        self.inc += 1
+        self._announce()
 
     def deregister(self):
         if self._ka is not None:
@@ -101,7 +117,8 @@ class ElasticAgent:
     def plan(np_: int, members: List[dict]) -> Tuple[int, List[dict]]:
         """Deterministic generation id + rank order for (np, membership)."""
         chosen = members[:np_]
-        h = hashlib.sha1(json.dumps([np_, [m["id"] for m in chosen]]).encode()).hexdigest()
+        ident = [[m["id"], m.get("lease", 0), m.get("inc", 0)] for m in chosen]
+        h = hashlib.sha1(json.dumps([np_, ident]).encode()).hexdigest()
         return int(h[:8], 16), chosen
 
     # ------------------------------------------------------------ rendezvous
@@ -160,7 +177,10 @@ class ElasticAgent:
                     "LOCAL_WORLD_SIZE": "1", "MASTER_ADDR": world["master_addr"],
                     "MASTER_PORT": str(world["master_port"]), "PDO_ELASTIC_GEN": f"{world['gen']:08x}"})
         cmd = [sys.executable, "-m", "paddle_operator_amd.launch", "--worker"] + worker_argv
-        return subprocess.Popen(cmd, env=env, start_new_session=True)
+        # own session so stop_worker() can signal the worker's whole group; but
+        # a pod kill (SIGKILL to the agent's group, as a container runtime
+        # would kill the container) must take the worker down too
+        return subprocess.Popen(cmd, env=env, start_new_session=True, preexec_fn=_die_with_parent)
 
     def stop_worker(self, grace: float = 20.0):
         p = self.proc
@@ -208,15 +228,31 @@ class ElasticAgent:
                 if rc == 0:
                     self.kv.put(self.prefix + f"done/{self.id:06d}", json.dumps({"gen": world["gen"]}))
                     return 0
+                # a dead peer usually takes this worker down with it before
+                # its lease has expired: give the membership one TTL to move
+                t_end = time.time() + self.ttl + 2 * self.poll
+                while not self.changed(world) and time.time() < t_end:
+                    time.sleep(self.poll)
                 if self.changed(world):
+                    _log(f"worker exited rc={rc} after a membership change → re-rendezvous")
                     continue  # a peer left: not this worker's fault
                 restarts += 1
                 _log(f"worker exited rc={rc}; restart {restarts}/{self.max_restarts}")
                 if restarts > self.max_restarts:
                     return rc
+                self.bump()
         finally:
             self.stop_worker(5.0)
             self.deregister()
+
+
+def _die_with_parent():
+    """Child side of spawn(): SIGKILL this worker when the agent dies."""
+    try:
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
 
 
 def _strip(argv: List[str]) -> List[str]:

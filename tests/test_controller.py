@@ -386,6 +386,65 @@ def test_exec_agent_elastic_scale_out(tmp_path):
         cl.stop()
 
 
+def _ready_rec(cl, job, rank):
+    v = cl.kv_get(f"/pdo/default-{job}/ready/{rank}")
+    return json.loads(v) if v else None
+
+
+def test_exec_agent_elastic_scale_kill_scale_in(tmp_path):
+    """Config 5 in full (scaled to CPU): elastic 2 → 3, pod kill of a rank
+    (agent restarts it in place, OnFailure), scale-in 3 → 2 (controller deletes
+    the surplus pod, paddlejob_controller.go:161-168), job completes.
+
+    Each re-formed world resumes from the newest checkpoint."""
+    port = _free_port()
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), elastic_kv=True,
+                      kv_endpoint=f"127.0.0.1:{port}")
+    cl.serve(f"127.0.0.1:{port}")
+    args = ["--workload", "resnet50", "--tiny", "--steps", "90", "--throttle-ms", "60",
+            "--ckpt-dir", str(tmp_path / "ckpt"), "--ckpt-every", "5"]
+    cont = _launcher_container(args)
+    cont["env"].append({"name": "PDO_ELASTIC_TTL", "value": "2"})
+    cl.create(T.paddlejob("ek", worker={"replicas": 2, "template": {"spec": {"containers": [cont]}}}, elastic=1,
+                          clean_pod_policy="Never"))
+
+    def log(i):
+        d = cl.sandbox(f"ek-worker-{i}")
+        p = os.path.join(d, "paddle.log") if d else ""
+        return open(p).read() if p and os.path.exists(p) else ""
+
+    try:
+        assert cl.wait(lambda: _ready_rec(cl, "ek", 1) is not None, timeout=120)
+        assert cl.wait(lambda: list((tmp_path / "ckpt").glob("ckpt-*.pt")), timeout=120)
+        cl.scale("ek", "worker", 3)
+        def world3():  # every rank of one 3-rank generation reported ready
+            recs = [_ready_rec(cl, "ek", r) or {} for r in range(3)]
+            return recs[0]["gen"] if all(r.get("world") == 3 for r in recs) and \
+                len({r.get("gen") for r in recs}) == 1 else None
+
+        assert cl.wait(lambda: world3() is not None, timeout=120), log(0)[-3000:]
+        gen_before = world3()
+        # pod kill: SIGKILL to worker-1's process group (agent + its worker)
+        assert cl.kill("ek-worker-1", 9)
+        assert cl.wait(lambda: world3() not in (None, gen_before), timeout=150), log(0)[-3000:]
+        pod1 = cl.get("Pod", "ek-worker-1")
+        assert pod1["status"]["containerStatuses"][0]["restartCount"] >= 1
+        # scale-in: np 3 → 2, the controller deletes ek-worker-2
+        cl.scale("ek", "worker", 2)
+        ok = cl.wait_phase("ek", T.Phase.Completed, timeout=240)
+        assert ok, (cl.job("ek")["status"], log(0)[-3000:], log(1)[-3000:])
+        assert cl.kv_get("/paddle/default-ek/np") == "2"
+        assert cl.get("Pod", "ek-worker-2") is None
+        readies = [json.loads(l[10:]) for i in range(2) for l in log(i).splitlines()
+                   if l.startswith("PDO_READY ")]
+        worlds = [r["world"] for r in readies if r["rank"] == 0]
+        # 2-rank, 3-rank, 3-rank again after the kill, 2-rank after scale-in
+        assert worlds[0] == 2 and worlds[-1] == 2 and worlds.count(3) >= 2, worlds
+        assert readies[-1]["resume_step"] >= 5
+    finally:
+        cl.stop()
+
+
 def test_zygote_warm_launch_and_kill(tmp_path):
     """bin/pdo-launch forks ranks from the per-node zygote; a pod kill reaches the rank."""
     pdo_launch = os.path.join(REPO, "bin", "pdo-launch")
