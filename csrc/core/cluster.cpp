@@ -102,11 +102,11 @@ bool Cluster::tick() {
   auto evs = store_->drain();
   if (!evs.empty()) progress = true;
   for (auto& e : evs) {
-    ctrl_->on_event(e);
+    if (opt_.controller) ctrl_->on_event(e);
     if (tap_) tap_(e);
   }
   // reconcile every ready key once (workers run in start() mode instead)
-  if (!running_) {
+  if (!running_ && opt_.controller) {
     ctrl_->queue().promote_due();
     int guard = 0;
     while (guard++ < 256 && ctrl_->process_one(0)) progress = true;
@@ -155,7 +155,7 @@ int Cluster::run_for(double s, double step) {
 
 void Cluster::start() {
   if (running_.exchange(true)) return;
-  ctrl_->start();
+  if (opt_.controller) ctrl_->start();
   loop_ = std::thread([this] {
     while (running_) {
       bool p = tick();
@@ -167,7 +167,7 @@ void Cluster::start() {
 void Cluster::stop() {
   if (!running_.exchange(false)) return;
   if (loop_.joinable()) loop_.join();
-  ctrl_->stop();
+  if (opt_.controller) ctrl_->stop();
 }
 
 Value Cluster::apply(const std::string& kind, Value obj) {

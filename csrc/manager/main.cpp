@@ -12,6 +12,9 @@
 //   --agent=exec|sim --gpus N --sandbox-root DIR --workers N
 //   --kubeconfig / --master  (k8s backend)
 //   --apply FILE.json        create/update objects at start (local backend)
+//   --controller=false       local backend as a bare single-node cluster (API
+//                            server, scheduler, kubelet-lite, KV) for an external
+//                            operator such as a second pdo-manager --backend=k8s
 #include <signal.h>
 #include <unistd.h>
 
@@ -57,6 +60,7 @@ struct Flags {
   int workers = 1;
   std::string kubeconfig, master;
   std::vector<std::string> apply;
+  bool controller = true;  // --controller=false: local backend without its PaddleJob controller
 };
 
 static int detect_gpus() {
@@ -97,6 +101,7 @@ static void usage() {
       "  --initImage IMAGE             coordinator init image ('' disables)\n"
       "  --backend local|k8s  --mode fast|compat  --api-bind-address ADDR  --agent exec|sim\n"
       "  --gpus N  --sandbox-root DIR  --workers N  --kubeconfig F  --master URL  --apply FILE\n"
+      "  --controller=false            local backend without its PaddleJob controller\n"
       "  --zap-log-level L  --zap-encoder json|console  --zap-devel\n");
 }
 
@@ -143,6 +148,7 @@ int main(int argc, char** argv) {
     else if (flag == "--kubeconfig") f.kubeconfig = next();
     else if (flag == "--master") f.master = next();
     else if (flag == "--apply") f.apply.push_back(next());
+    else if (flag == "--controller") f.controller = boolean();
     else if (flag == "--zap-log-level") {
       if (!pdo::log::parse_level(next(), &lc.level)) return 2;
     } else if (flag == "--zap-encoder") lc.json = next() == "json";
@@ -227,6 +233,7 @@ int main(int argc, char** argv) {
   co.port_start = ps;
   co.port_end = pe;
   co.namespace_ = f.ns;
+  co.controller = f.controller;
   pdo::NodeInfo node;
   node.name = "local";
   node.gpus = f.gpus >= 0 ? f.gpus : detect_gpus();
