@@ -209,7 +209,10 @@ def _splitk(tokens: int, m: int, n: int) -> int:
     """Token-slice count for dW = dY^T X: aim for ≥256 output tiles of 256² (one per CU).
 
     The LM-head dW (50304×1024 → 786 tiles, K = 65536) is past that target but
-    still runs 6-8 % faster as 4 token slices (tools/dw_probe.py, tuned)."""
+    still runs 6-8 % faster as 4 token slices (tools/dw_probe.py, tuned).
+    Padding the vocabulary to 50432 so gemm_dw takes it measured 6.10 ms (4
+    slices) vs 6.35 ms here (tools/lm_dw_probe.py): not worth untuned
+    forward / dX shapes for 0.16 % of the step."""
     if tokens < 8192 or os.environ.get("PDO_SPLITK", "1") == "0":
         return 1
     tiles = max(1, (m * n) // 65536)
