@@ -245,6 +245,23 @@ static void test_cluster_sim_multiworker() {
   CHECK(running == 8);
 }
 
+// controller=false: API objects are stored and watched, but nothing reconciles
+// them — no pods, no status (the bare cluster an external operator drives)
+static void test_cluster_without_controller() {
+  pdo::ClusterOptions o;
+  o.agent_mode = pdo::AgentOptions::Sim;
+  o.controller = false;
+  pdo::Cluster c(o);
+  c.apply("PaddleJob", job("bare", 1, 2));
+  c.start();
+  usleep(200000);
+  c.stop();
+  for (int i = 0; i < 20; ++i) c.tick();
+  CHECK(c.store().list("PaddleJob").size() == 1);
+  CHECK(c.store().list("Pod").empty());
+  CHECK(c.store().list("PaddleJob")[0].at_path("status.phase").as_string().empty());
+}
+
 int main() {
   test_json();
   test_quantity();
@@ -255,6 +272,7 @@ int main() {
   test_kv_and_http();
   test_yaml();
   test_cluster_sim_multiworker();
+  test_cluster_without_controller();
   printf("core_tests: %d passed, %d failed\n", g_pass, g_fail);
   return g_fail ? 1 : 0;
 }
