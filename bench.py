@@ -1,137 +1,315 @@
 #!/usr/bin/env python3
-"""Headline benchmark: launched GPT-2-medium training throughput on MI355X.
+"""Headline benchmark: a *launched* GPT-2-medium PaddleJob on N MI355X.
 
 BASELINE.json metric: "job-start->all-ranks-ready p50 (s); launched tokens/sec
-at 1/2/4/8 MI355X".  This script measures the flagship *training step* of a
-launched collective-mode job (config 4: GPT-2-medium, seq 1024, bf16, data
-parallel over RCCL/xGMI, one rank per GPU) and reports the whole-job
-tokens/s.  The time from process start until every rank is ready (RCCL
-communicator up, weights broadcast, first barrier passed) is reported as
-``ready_s`` alongside.  The operator-level launch latency (PaddleJob →
-all-ranks-ready through the control plane) is measured by
-``python bench_launch.py``.
+at 1/2/4/8 MI355X".  Both halves are measured here, through the operator:
 
-Per-GPU micro-batch 64 × 1024 tokens (weak scaling): at 8 GPUs the global
-batch is 512 sequences = 0.5 M tokens, GPT-2's own batch size; GEMM shapes
-are pre-tuned for it (paddle_operator_amd/tuning/*_b64_gfx950.csv).
+1. this process starts the native local backend in-process (object store +
+   PaddleJob controller in ``fast`` mode + gang scheduler + kubelet-lite exec
+   agent with its per-node warm launcher + pdo-kv) — the same C++ code as
+   ``pdo-manager --backend=local`` (csrc/core);
+2. **ready p50**: ``--ready-trials`` PaddleJobs of N ``noop`` ranks (one
+   ``amd.com/gpu`` each) are created one after the other; a trial's latency is
+   PaddleJob create → the last rank's readiness record in pdo-kv, where a rank
+   is ready once its RCCL communicator is up (eager ``device_id`` init, even at
+   one rank) and a warm-up all-reduce has completed (launch/bootstrap.py);
+3. **throughput**: one PaddleJob with ``worker.replicas=N`` whose ranks run
+   ``pdo-launch --workload gpt2 --model gpt2-medium --batch 64 --seq 1024
+   --bench``: W untimed steps, then exactly K timed steps bracketed by barrier +
+   device synchronize; each rank publishes its elapsed time to pdo-kv and the
+   MAX over ranks gives the whole-job tokens/s.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-it runs under ``torch.distributed.run`` one rank per GPU.  W untimed steps,
-then exactly K timed steps bracketed by barrier + device synchronize; the max
-over ranks is reported by rank 0 as one JSON line.
+The reference's launch path being emulated is
+controllers/paddlejob_controller.go:277-330 (pod creation → ConfigMap →
+ordered release); its data plane is the launched job
+(deploy/examples/resnet.yaml:14-25).  ``--compat-trials`` adds ready trials of
+the reference-equivalent ``compat`` sequencing (cold interpreters, one mutation
+per reconcile, busybox-style coordinator released by exec) for comparison.
+
+Rank processes are spawned by the agent, never by torchrun: ``python bench.py
+--gpus 8`` is a complete 8-GPU run.  Under the driver's
+``torch.distributed.run --nproc-per-node N bench.py --gpus N`` the torchrun
+rank 0 is the launcher and the other torchrun processes wait on a CPU (gloo)
+barrier without touching the GPU.  This process never initialises HIP: GPUs are
+counted from KFD sysfs, so the agent may fork+exec ranks from it.
 
 Data: synthetic tokens generated on device each step; weights: random init.
 """
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import socket
+import statistics
+import sys
+import tempfile
 import time
 
-_T0 = time.time()  # process start (before torch import) for ready_s
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
 
-import argparse  # noqa: E402
-import json  # noqa: E402
-import os  # noqa: E402
-import sys  # noqa: E402
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+BASELINE_METRIC = "job-start->all-ranks-ready p50 (s); launched tokens/sec at 1/2/4/8 MI355X"
+# torchrun's contract variables: never inherited by the ranks this process launches
+TORCHRUN_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                 "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
 
 
-def main():
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks to launch (one MI355X each)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="gpt2-medium")
     ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("PDO_MICRO_BATCH", "64")))
     ap.add_argument("--seq", type=int, default=1024)
-    ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--ready-trials", type=int, default=10)
+    ap.add_argument("--compat-trials", type=int, default=0,
+                    help="extra ready trials in the reference-equivalent compat mode")
+    ap.add_argument("--mode", default="fast", choices=["fast", "compat"])
+    ap.add_argument("--no-zygote", action="store_true", help="cold interpreter per rank")
+    ap.add_argument("--cpu", action="store_true", help="ranks on CPU (gloo) even if GPUs are present")
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
-    ap.add_argument("--quiet", action="store_true")
-    args = ap.parse_args()
-    os.environ["PDO_OPS"] = args.ops
+    ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
+    ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
+    return ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
+
+class Launcher:
+    """One in-process local backend; launches PaddleJobs and reads pdo-kv."""
+
+    def __init__(self, mode, zygote, gpus, sandbox):
+        from paddle_operator_amd.controller import LocalCluster
+        from paddle_operator_amd.kv.client import KVClient
+
+        self.port = _free_port()
+        self.gpus = gpus
+        self.sandbox = sandbox
+        self.cl = LocalCluster(mode=mode, agent="exec", sandbox_root=sandbox,
+                               nodes=[{"name": "node0", "gpus": gpus}],
+                               kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote)
+        self.cl.serve(f"127.0.0.1:{self.port}")
+        self.cl.start()
+        self.kv = KVClient(f"127.0.0.1:{self.port}")
+        if zygote:
+            t0 = time.time()
+            # node warm-up (the zygote imports torch once), not part of any job's launch
+            while not self.cl.zygotes_ready():
+                if time.time() - t0 > 600:
+                    raise RuntimeError("zygote not ready after 600 s; see " + os.path.join(sandbox, "zygote.log"))
+                time.sleep(0.05)
+            log(f"zygote ready in {time.time() - t0:.1f}s")
+
+    def container(self, args, ops):
+        from paddle_operator_amd.api import types as T
+        env = [{"name": "PYTHONPATH", "value": REPO}, {"name": "PDO_KV", "value": f"127.0.0.1:{self.port}"},
+               {"name": "PDO_PYTHON", "value": sys.executable}, {"name": "PDO_OPS", "value": ops}]
+        if not self.gpus:
+            env.append({"name": "OMP_NUM_THREADS", "value": "2"})
+        c = {"name": "paddle", "image": "pdo/launcher:rocm",
+             "command": [os.path.join(REPO, "bin", "pdo-launch")] + list(args), "env": env}
+        if self.gpus:
+            c["resources"] = {"limits": {T.AMD_GPU: 1}}
+        return c
+
+    def launch(self, name, ranks, args, ops):
+        from paddle_operator_amd.api import types as T
+        job = T.paddlejob(name, worker={"replicas": ranks,
+                                        "template": {"spec": {"containers": [self.container(args, ops)]}}},
+                          clean_pod_policy="Always")
+        t0 = time.time()
+        self.cl.create(job)
+        return t0
+
+    def wait_records(self, name, kind, n, timeout):
+        prefix = f"/pdo/default-{name}/{kind}/"
+        deadline = time.time() + timeout
+        recs = {}
+        while time.time() < deadline:
+            recs = self.kv.get_prefix(prefix)
+            if len(recs) >= n:
+                return [json.loads(v) for v in recs.values()]
+            phase = ((self.cl.job(name) or {}).get("status") or {}).get("phase")
+            if phase == "Failed":
+                break
+            time.sleep(0.005)
+        self.dump_logs(name)
+        raise RuntimeError(f"{name}: {len(recs)}/{n} {kind} records (phase "
+                           f"{((self.cl.job(name) or {}).get('status') or {}).get('phase')})")
+
+    def dump_logs(self, name, tail=4000):
+        import glob
+        for path in sorted(glob.glob(os.path.join(self.sandbox, f"default_{name}-*", "*.log"))):
+            try:
+                with open(path) as f:
+                    log(f"--- {os.path.relpath(path, self.sandbox)} (tail) ---\n{f.read()[-tail:]}")
+            except OSError:
+                pass
+
+    def finish(self, name, timeout=120):
+        from paddle_operator_amd.api import types as T
+        ok = self.cl.wait_phase(name, "Completed", timeout=timeout)
+        if not ok:
+            self.dump_logs(name)
+            raise RuntimeError(f"{name}: not Completed "
+                               f"({((self.cl.job(name) or {}).get('status') or {}).get('phase')})")
+        self.cl.delete(T.KIND, name)
+        self.cl.wait(lambda: self.cl.job(name) is None and not self.cl.pods(name), timeout=60)
+
+    def ready_trial(self, name, ranks, timeout):
+        t0 = self.launch(name, ranks, ["--workload", "noop", "--exit-after-ready"], "torch")
+        rs = self.wait_records(name, "ready", ranks, timeout)
+        self.finish(name)
+        return {"ready_s": max(r["t_ready"] for r in rs) - t0,
+                "pg_s": max(r["t_pg"] - r["t_start"] for r in rs),
+                "proc_start_s": min(r["t_start"] for r in rs) - t0}
+
+    def stop(self):
+        self.cl.stop()
+
+
+def ready_stats(trials):
+    v = [t["ready_s"] for t in trials]
+    return {"p50": round(statistics.median(v), 4), "min": round(min(v), 4), "max": round(max(v), 4),
+            "trials": len(v), "pg_init_p50": round(statistics.median(t["pg_s"] for t in trials), 4)}
+
+
+def orchestrate(a):
     from paddle_operator_amd.models.gpt2 import GPT2Config
-    from paddle_operator_amd.train import GPT2Trainer, init_distributed
+    from paddle_operator_amd.utils.topology import gpu_count
 
-    info = init_distributed()
-    world = info.world
-    if world != args.gpus and info.is_main:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = torch.device("cuda", info.local_rank) if torch.cuda.is_available() else torch.device("cpu")
-    cfg = GPT2Config.named(args.model)
-    tr = GPT2Trainer(cfg, args.micro_batch, args.seq, dev, bucket_mb=args.bucket_mb)
-    tr.sync_initial_weights()
+    N = a.gpus
+    detected = 0 if a.cpu else gpu_count()
+    if detected and detected < N:
+        log(f"--gpus {N} but only {detected} GPU(s) visible")
+        return 2
+    gpus = N if detected else 0  # the job asks for N amd.com/gpu; the node offers exactly those
+    sandbox = tempfile.mkdtemp(prefix="pdo-bench-")
+    out = {}
+    try:
+        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode))
+        try:
+            trials = []
+            for t in range(a.ready_trials):
+                trials.append(L.ready_trial(f"ready-{t}", N, a.timeout))
+            out["ready"] = ready_stats(trials) if trials else None
+            if trials:
+                log(f"ready p50 {out['ready']['p50']}s over {len(trials)} trials ({N} ranks)")
+            name = "gpt2-bench"
+            wl = ["--workload", "gpt2", "--model", a.model, "--batch", str(a.micro_batch), "--seq", str(a.seq),
+                  "--steps", str(a.steps), "--warmup", str(a.warmup), "--bench", "--timeout", "600"]
+            t0 = L.launch(name, N, wl, a.ops)
+            rs = L.wait_records(name, "bench", N, a.timeout)
+            L.finish(name)
+            out["bench"] = rs
+            out["bench_ready_s"] = max(r["t_ready"] for r in rs) - t0
+        finally:
+            L.stop()
+        if a.compat_trials:
+            C = Launcher("compat", False, gpus, os.path.join(sandbox, "compat"))
+            try:
+                ct = [C.ready_trial(f"compat-{t}", N, a.timeout) for t in range(a.compat_trials)]
+            finally:
+                C.stop()
+            out["compat_ready"] = ready_stats(ct)
+    finally:
+        if a.keep:
+            log(f"sandbox kept: {sandbox}")
+        else:
+            shutil.rmtree(sandbox, ignore_errors=True)
 
-    def sync():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-
-    def barrier():
-        if dist.is_initialized():
-            dist.barrier()
-
-    sync()
-    barrier()
-    t_ready = time.time()
-
-    for _ in range(args.warmup):
-        loss = tr.step()
-    sync()
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = tr.step()
-    sync()
-    barrier()
-    sync()
-    dt = time.perf_counter() - t0
-    loss_v = float(loss.detach().float().item())
-
-    # max over ranks of elapsed time; ready = latest ready minus earliest start
-    vals = torch.tensor([dt, t_ready, -_T0], dtype=torch.float64, device=dev)
-    if dist.is_initialized():
-        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-    dt = float(vals[0])
-    ready_s = float(vals[1]) + float(vals[2])
-
-    tokens = tr.tokens_per_step() * world * args.steps
+    rs = out["bench"]
+    dt = max(r["seconds"] for r in rs)  # max over ranks
+    tokens = sum(r["tokens_per_step_rank"] for r in rs) * a.steps
     tps = tokens / dt
-    ms = dt / args.steps * 1e3
-    flops = cfg.flops_per_token(args.seq) * tps / world
-    if info.is_main:
-        rec = {
-            "metric": "launched tokens/sec (GPT-2-medium collective DP, bf16)",
-            "value": round(tps, 1),
-            "unit": "tokens/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (on-device random tokens), random-init weights",
-            "config": {
-                "model": args.model,
-                "global_batch": args.micro_batch * world,
-                "micro_batch_per_gpu": args.micro_batch,
-                "seq_len": args.seq,
-                "parallelism": f"dp{world}",
-                "bucket_mb": args.bucket_mb,
-                "ops": args.ops,
-            },
-            "ready_s": round(ready_s, 3),
-            "model_tflops_per_gpu": round(flops / 1e12, 1),
-            "mfu_vs_2.5PF_dense": round(flops / 2.5e15, 4),
-            "final_loss": round(loss_v, 4),
-        }
-        print(json.dumps(rec), flush=True)
-    if dist.is_initialized():
-        dist.barrier()
+    cfg = GPT2Config.named(a.model)
+    flops_gpu = cfg.flops_per_token(a.seq) * tps / N
+    rec = {
+        "metric": "launched tokens/sec (GPT-2-medium PaddleJob through the pdo operator, collective DP over RCCL)",
+        "value": round(tps, 1),
+        "unit": "tokens/s",
+        "n_gpus": N,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,  # BASELINE.json publishes no number ("published": {})
+        "dtype": "bf16",
+        "data": "synthetic (on-device random tokens), random-init weights",
+        "config": {
+            "model": a.model,
+            "global_batch": a.micro_batch * N,
+            "micro_batch_per_gpu": a.micro_batch,
+            "seq_len": a.seq,
+            "parallelism": f"dp{N}",
+            "launch": f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}",
+            "grad_reduce": rs[0].get("grad_reduce"),
+            "buckets": rs[0].get("buckets"),
+            "ops": a.ops,
+            "device": "cpu/gloo" if not gpus else rs[0].get("gpu_name", "gpu"),
+        },
+        "baseline_metric": BASELINE_METRIC,
+        "ready_p50_s": out["ready"]["p50"] if out.get("ready") else None,
+        "ready": out.get("ready"),
+        "compat_ready": out.get("compat_ready"),
+        "gpt2_job_ready_s": round(out["bench_ready_s"], 3),
+        "model_tflops_per_gpu": round(flops_gpu / 1e12, 1),
+        "mfu_vs_2.5PF_dense": round(flops_gpu / 2.5e15, 4),
+        "final_loss": rs[0].get("loss"),
+        "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in rs),
+    }
+    print(json.dumps(rec), flush=True)
+    return 0
+
+
+def main(argv=None):
+    a = parse_args(argv)
+    tr_world = int(os.environ.get("WORLD_SIZE", "1"))
+    tr_rank = int(os.environ.get("RANK", "0"))
+    if tr_world > 1:
+        # the driver's torchrun wrapper: rank 0 launches the job, the others
+        # only keep torchrun's world alive (CPU gloo barrier, no GPU)
+        import datetime
+
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=tr_rank, world_size=tr_world,
+                                timeout=datetime.timedelta(seconds=7200))
+        rc = 0
+        if tr_rank == 0:
+            for k in TORCHRUN_VARS:
+                os.environ.pop(k, None)
+            for k in [k for k in os.environ if k.startswith("TORCHELASTIC_")]:
+                os.environ.pop(k, None)
+            try:
+                rc = orchestrate(a)
+            except Exception as e:
+                log(f"failed: {e}")
+                rc = 1
+        import torch
+        t = torch.tensor([rc], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.destroy_process_group()
+        return int(t.item())
+    try:
+        return orchestrate(a)
+    except Exception as e:
+        log(f"failed: {e}")
+        return 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -50,9 +50,9 @@ def _free_port():
 
 
 def _gpu_count():
-    # device_count() does not initialise HIP on this image (the agent forks ranks)
-    import torch
-    return torch.cuda.device_count()
+    # KFD sysfs, never HIP: this process's agent fork+execs every rank
+    from paddle_operator_amd.utils.topology import gpu_count
+    return gpu_count()
 
 
 def run(mode, ranks, trials, workload, gpus, sandbox, timeout=180.0, extra_args=()):

@@ -521,33 +521,52 @@ void scale_(at::Tensor x, double s) {
   CHECK_RC(pdo::scale_bf16(bp(x), x.numel(), (float)s, cur_stream()), "scale_bf16");
 }
 
-// flat[off_i : off_i + n_i] = scale * t_i for every tensor (one launch)
+// flat[off_i : off_i + n_i] = scale * t_i for every tensor (one launch);
+// reverse: t_i = flat[off_i : off_i + n_i].  bf16 or f32, all one dtype.
 void flatten_scale(std::vector<at::Tensor> ts, at::Tensor flat, std::vector<int64_t> offsets, double scale,
                    bool reverse) {
-  CHECK_IN(flat); CHECK_BF16(flat);
+  CHECK_IN(flat);
+  const auto dt = flat.scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kFloat, "flat must be bf16 or float32");
   TORCH_CHECK(ts.size() == offsets.size());
   const int n = ts.size();
   if (n == 0) return;
   auto meta = at::empty({n, 3}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
   int64_t* mp = meta.data_ptr<int64_t>();
-  std::vector<long long> sizes(n), offs(n);
-  int64_t prev = -1;
+  int64_t prev = -1, total = 0;
   for (int i = 0; i < n; ++i) {
-    CHECK_IN(ts[i]); CHECK_BF16(ts[i]);
-    TORCH_CHECK(offsets[i] > prev, "offsets must be increasing");
+    CHECK_IN(ts[i]);
+    TORCH_CHECK(ts[i].scalar_type() == dt, "every tensor must have the flat buffer's dtype");
+    TORCH_CHECK(ts[i].device() == flat.device(), "tensors must live on the flat buffer's device");
+    TORCH_CHECK(offsets[i] >= 0 && offsets[i] >= prev, "offsets must be non-negative and increasing");
     TORCH_CHECK(offsets[i] + ts[i].numel() <= flat.numel(), "tensor overruns the flat buffer");
+    TORCH_CHECK(i == 0 || offsets[i] >= offsets[i - 1] + ts[i - 1].numel(), "tensors overlap in the flat buffer");
     prev = offsets[i];
     mp[3 * i] = reinterpret_cast<int64_t>(ts[i].data_ptr());
     mp[3 * i + 1] = ts[i].numel();
     mp[3 * i + 2] = offsets[i];
-    sizes[i] = ts[i].numel();
-    offs[i] = offsets[i];
+    total = offsets[i] + ts[i].numel();
   }
   auto dmeta = meta.to(flat.device(), /*non_blocking=*/true);
-  int rc = reverse ? pdo::unflatten(bp(flat), nullptr, sizes.data(), offs.data(), n, dmeta.data_ptr(), cur_stream())
-                   : pdo::flatten_scale(nullptr, sizes.data(), offs.data(), n, bp(flat), (float)scale,
-                                        dmeta.data_ptr(), cur_stream());
-  CHECK_RC(rc, "flatten/unflatten");
+  CHECK_RC(pdo::bucket_copy(dt == at::kFloat ? 1 : 0, !reverse, flat.data_ptr(), total, n, dmeta.data_ptr(),
+                            (float)scale, cur_stream()),
+           "flatten/unflatten");
+  // the pinned meta must outlive the async H2D copy
+  c10::hip::getCurrentHIPStream().synchronize();
+}
+
+// dst (f32) = scale * src (bf16), elementwise; numel % 8 == 0
+void cast_scale_bf16_f32(at::Tensor src, at::Tensor dst, double scale) {
+  CHECK_IN(src); CHECK_IN(dst); CHECK_BF16(src); CHECK_F32(dst);
+  TORCH_CHECK(src.numel() == dst.numel() && src.numel() % 8 == 0, "cast: numel mismatch or not a multiple of 8");
+  CHECK_RC(pdo::cast_scale_bf16_f32(bp(src), fp(dst), src.numel(), (float)scale, cur_stream()), "cast_scale_bf16_f32");
+}
+
+// dst (bf16) = src (f32); numel % 8 == 0
+void cast_f32_bf16(at::Tensor src, at::Tensor dst) {
+  CHECK_IN(src); CHECK_IN(dst); CHECK_F32(src); CHECK_BF16(dst);
+  TORCH_CHECK(src.numel() == dst.numel() && src.numel() % 8 == 0, "cast: numel mismatch or not a multiple of 8");
+  CHECK_RC(pdo::cast_f32_bf16(fp(src), bp(dst), src.numel(), cur_stream()), "cast_f32_bf16");
 }
 
 // ---------------------------------------------------------------- device / IPC bootstrap
@@ -584,23 +603,34 @@ int set_device(int dev) {
   return cur;
 }
 
-py::bytes ipc_get_handle(at::Tensor t) {
+// export a tensor for another process: (handle of the allocation that holds
+// it, byte offset of the tensor inside that allocation) — the caching
+// allocator sub-allocates, so the tensor need not start at the allocation base
+py::tuple ipc_get_handle(at::Tensor t) {
   CHECK_DEV(t);
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HIP_OK(hipMemGetAddressRange(&base, &size, t.data_ptr()));
   hipIpcMemHandle_t h;
-  HIP_OK(hipIpcGetMemHandle(&h, t.data_ptr()));
-  return py::bytes(reinterpret_cast<const char*>(&h), sizeof h);
+  HIP_OK(hipIpcGetMemHandle(&h, base));
+  const int64_t off = reinterpret_cast<char*>(t.data_ptr()) - reinterpret_cast<char*>(base);
+  return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&h), sizeof h), off);
 }
 
-// map a peer's exported buffer into this process as a uint8 tensor
-at::Tensor ipc_open_handle(py::bytes handle, int64_t nbytes, int64_t device) {
+// map a peer's exported buffer into this process as a uint8 tensor of
+// `nbytes` starting `offset` bytes into the peer's allocation
+at::Tensor ipc_open_handle(py::bytes handle, int64_t nbytes, int64_t device, int64_t offset) {
   std::string hs = handle;
   TORCH_CHECK(hs.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
+  TORCH_CHECK(offset >= 0 && nbytes >= 0, "bad IPC offset/size");
   hipIpcMemHandle_t h;
   memcpy(&h, hs.data(), sizeof h);
   void* p = nullptr;
   HIP_OK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
   auto opts = at::TensorOptions().dtype(at::kByte).device(at::Device(at::kCUDA, (c10::DeviceIndex)device));
-  return at::from_blob(p, {nbytes}, [](void* ptr) { (void)hipIpcCloseMemHandle(ptr); }, opts);
+  void* base = p;
+  return at::from_blob(static_cast<char*>(p) + offset, {nbytes}, [base](void*) { (void)hipIpcCloseMemHandle(base); },
+                       opts);
 }
 
 bool can_access_peer(int dev, int peer) {
@@ -672,10 +702,13 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("with_bias_grad") = false, py::arg("db_out") = py::none());
   m.def("scale_", &scale_);
   m.def("flatten_scale", &flatten_scale);
+  m.def("cast_scale_bf16_f32", &cast_scale_bf16_f32);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("device_info", &device_info);
   m.def("set_device", &set_device);
   m.def("ipc_get_handle", &ipc_get_handle);
-  m.def("ipc_open_handle", &ipc_open_handle);
+  m.def("ipc_open_handle", &ipc_open_handle, py::arg("handle"), py::arg("nbytes"), py::arg("device"),
+        py::arg("offset") = 0);
   m.def("can_access_peer", &can_access_peer);
   m.def("enable_peer_access", &enable_peer_access);
   m.attr("arch") = "gfx950";

@@ -1,12 +1,21 @@
 // SPDX-License-Identifier: Apache-2.0
 // Multi-tensor bucket kernels for the RCCL data-parallel path (gfx950).
-// The flat-arena DDP needs no copies for its own gradients; these kernels
-// serve everything else that must travel through a bucket (parameter
-// broadcast of non-arena modules, PS pushes, checkpoint packing):
+//
+// The flat-arena DDP needs no copies for its own gradients (a bucket is a
+// slice of the arena).  These kernels serve what must still travel through a
+// bucket:
 //   flatten_scale: dst[off_i : off_i + n_i] = scale * src_i  (one launch for N tensors)
 //   unflatten:     dst_i = src[off_i : off_i + n_i]
-// Work split: one 2048-element span of the flat buffer per workgroup; the
-// owning tensor is found by binary search over the (device-resident) offsets.
+//     → one RCCL broadcast of all non-arena module buffers (BatchNorm running
+//       statistics, workloads/resnet.py) instead of one collective per buffer;
+//   cast_scale_bf16_f32: fp32 staging copy of a bf16 gradient bucket with the
+//     1/world average folded in (parallel/ddp.py grad_reduce="fp32": the
+//     all-reduce then accumulates in fp32 on the wire);
+//   (the averaged fp32 gradients go back into the bf16 arena with
+//   embed.hip's cast_f32_bf16).
+// Work split of the multi-tensor kernels: one 2048-element span of the flat
+// buffer per workgroup; the owning tensor is found by binary search over the
+// (device-resident) offsets.  Cast kernels move 16 B of bf16 per lane.
 #include "common.h"
 #include "kernels.h"
 
@@ -26,16 +35,16 @@ __device__ __forceinline__ int find_tensor(const Meta* meta, int n, long long e)
   return lo;
 }
 
-template <bool FLATTEN>
-__global__ __launch_bounds__(256) void bucket_kernel(const Meta* __restrict__ meta, int n, bf16* __restrict__ flat,
+template <typename T, bool FLATTEN>
+__global__ __launch_bounds__(256) void bucket_kernel(const Meta* __restrict__ meta, int n, T* __restrict__ flat,
                                                      long long total, float scale) {
   const long long span0 = (long long)blockIdx.x * 2048;
   for (long long e = span0 + threadIdx.x; e < span0 + 2048 && e < total; e += 256) {
     const int i = find_tensor(meta, n, e);
     const long long k = e - meta[i].offset;
     if (k >= meta[i].size) continue;  // alignment padding between tensors
-    bf16* t = reinterpret_cast<bf16*>(meta[i].ptr);
-    if (FLATTEN) flat[e] = (bf16)((float)t[k] * scale);
+    T* t = reinterpret_cast<T*>(meta[i].ptr);
+    if (FLATTEN) flat[e] = (T)((float)t[k] * scale);
     else t[k] = flat[e];
   }
 }
@@ -47,32 +56,44 @@ __global__ __launch_bounds__(256) void scale_kernel(bf16* __restrict__ x, long l
   }
 }
 
-static long long total_of(const long long* sizes, const long long* offsets, int n) {
-  return n ? offsets[n - 1] + sizes[n - 1] : 0;
+__global__ __launch_bounds__(256) void cast_scale_bf16_f32_kernel(const bf16* __restrict__ src,
+                                                                  float* __restrict__ dst, long long nvec, float s) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    const f32x8 v = to_f32(reinterpret_cast<const bf16x8*>(src)[i]) * s;
+    f32x4* d = reinterpret_cast<f32x4*>(dst) + 2 * i;
+    d[0] = f32x4{v[0], v[1], v[2], v[3]};
+    d[1] = f32x4{v[4], v[5], v[6], v[7]};
+  }
 }
 
-int flatten_scale(const void* const* srcs, const long long* sizes, const long long* offsets, int n, bf16* dst,
-                  float scale, void* dev_meta, hipStream_t st) {
-  (void)srcs;
-  const long long total = total_of(sizes, offsets, n);
-  if (total == 0) return 0;
-  bucket_kernel<true><<<(unsigned)((total + 2047) / 2048), 256, 0, st>>>((const Meta*)dev_meta, n, dst, total, scale);
+template <typename T>
+static int multi_tensor(bool flatten, T* flat, long long total, int n, void* dev_meta, float scale, hipStream_t st) {
+  if (total <= 0 || n <= 0) return 0;
+  const unsigned grid = (unsigned)((total + 2047) / 2048);
+  if (flatten) bucket_kernel<T, true><<<grid, 256, 0, st>>>((const Meta*)dev_meta, n, flat, total, scale);
+  else bucket_kernel<T, false><<<grid, 256, 0, st>>>((const Meta*)dev_meta, n, flat, total, 1.f);
   return 0;
 }
 
-int unflatten(const bf16* src, void* const* dsts, const long long* sizes, const long long* offsets, int n,
-              void* dev_meta, hipStream_t st) {
-  (void)dsts;
-  const long long total = total_of(sizes, offsets, n);
-  if (total == 0) return 0;
-  bucket_kernel<false><<<(unsigned)((total + 2047) / 2048), 256, 0, st>>>((const Meta*)dev_meta, n,
-                                                                          const_cast<bf16*>(src), total, 1.f);
-  return 0;
+int bucket_copy(int dtype, bool flatten, void* flat, long long total, int n, void* dev_meta, float scale,
+                hipStream_t st) {
+  switch (dtype) {
+    case 0: return multi_tensor<bf16>(flatten, (bf16*)flat, total, n, dev_meta, scale, st);
+    case 1: return multi_tensor<float>(flatten, (float*)flat, total, n, dev_meta, scale, st);
+    default: return -3;
+  }
 }
 
 int scale_bf16(bf16* x, long long n, float s, hipStream_t st) {
   if (n % 8) return -2;
   scale_kernel<<<stream_grid(n / 8, 256), 256, 0, st>>>(x, n / 8, s);
+  return 0;
+}
+
+int cast_scale_bf16_f32(const bf16* src, float* dst, long long n, float s, hipStream_t st) {
+  if (n % 8) return -2;
+  if (n == 0) return 0;
+  cast_scale_bf16_f32_kernel<<<stream_grid(n / 8, 256), 256, 0, st>>>(src, dst, n / 8, s);
   return 0;
 }
 

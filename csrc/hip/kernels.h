@@ -104,11 +104,12 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
 int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse, float* delta, bf16* dqkv, int B,
              int S, int H, int D, float scale, hipStream_t st, float* dbias_part = nullptr);
 
-// bucket.hip (DDP helpers: multi-tensor flatten with fused scale / unflatten)
-int flatten_scale(const void* const* srcs, const long long* sizes, const long long* offsets, int n, bf16* dst,
-                  float scale, void* dev_meta, hipStream_t st);
-int unflatten(const bf16* src, void* const* dsts, const long long* sizes, const long long* offsets, int n,
-              void* dev_meta, hipStream_t st);
+// bucket.hip (DDP helpers).  bucket_copy: dtype 0 = bf16, 1 = f32; dev_meta is
+// n × {ptr, numel, offset} (int64) in device memory; flatten: flat[off+k] = scale·t[k],
+// else t[k] = flat[off+k]
+int bucket_copy(int dtype, bool flatten, void* flat, long long total, int n, void* dev_meta, float scale,
+                hipStream_t st);
+int cast_scale_bf16_f32(const bf16* src, float* dst, long long n, float s, hipStream_t st);
 int scale_bf16(bf16* x, long long n, float s, hipStream_t st);
 
 }  // namespace pdo

@@ -77,12 +77,17 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
     else:
         dev = torch.device("cpu")
     b = Bootstrapped(rank, world, local, dev, backend, t_start)
-    if world > 1 and not dist.is_initialized():
+    # RCCL is brought up even for a 1-rank job: "ready" then always includes
+    # communicator init, and the DDP code path is the one that runs at scale.
+    # A CPU (gloo) world of 1 has nothing to rendezvous with.
+    if (world > 1 or backend == "nccl") and not dist.is_initialized():
         kw = {}
         if backend == "nccl":
             kw["device_id"] = dev
         if store is not None:
             kw["store"] = store
+        elif world == 1:
+            kw["store"] = dist.HashStore()
         else:
             host, port = os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"])
             if rank != 0:
@@ -110,7 +115,8 @@ def ipc_probe_run(dev: torch.device, nbytes: int = 64 << 20) -> dict:
     node = os.environ.get("PDO_NODE_NAME") or socket.gethostname()
     buf = torch.full((nbytes,), rank % 251, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
-    rec = {"node": node, "pid": os.getpid(), "handle": m.ipc_get_handle(buf).hex(),
+    handle, off = m.ipc_get_handle(buf)
+    rec = {"node": node, "pid": os.getpid(), "handle": handle.hex(), "offset": off,
            "device": torch.cuda.current_device(), "bdf": m.device_info(torch.cuda.current_device())["pci_bus_id"]}
     allrec = [None] * world
     dist.all_gather_object(allrec, rec)
@@ -119,8 +125,8 @@ def ipc_probe_run(dev: torch.device, nbytes: int = 64 << 20) -> dict:
     local_dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     for r in peers:
         try:
-            peer = m.ipc_open_handle(bytes.fromhex(allrec[r]["handle"]), nbytes, dev.index)
-        except RuntimeError as e:  # same GPU / no peer access
+            peer = m.ipc_open_handle(bytes.fromhex(allrec[r]["handle"]), nbytes, dev.index, allrec[r]["offset"])
+        except RuntimeError as e:  # no peer access between the two GPUs
             out[r] = f"unavailable: {e}"
             continue
         torch.cuda.synchronize(dev)

@@ -27,6 +27,10 @@ def parse_args(argv=None):
     ap.add_argument("--workload", default="noop", choices=["gpt2", "resnet50", "wide_deep", "deepfm", "noop"])
     ap.add_argument("--model", default="gpt2-medium")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=0, help="untimed steps before the timed ones (--bench)")
+    ap.add_argument("--bench", action="store_true",
+                    help="benchmark protocol: --warmup untimed steps, then exactly --steps timed steps bracketed by "
+                         "barrier + device synchronize; the record goes to pdo-kv /pdo/<job>/bench/<rank>")
     ap.add_argument("--batch", type=int, default=0, help="per-rank micro batch (0 = workload default)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--tiny", action="store_true", help="tiny model variant (CPU tests)")
@@ -104,6 +108,9 @@ def run_collective(args, jenv) -> int:
             dist.destroy_process_group()
         return 0
 
+    if args.bench:
+        return _bench(args, b, jenv, trainer, tokens_per_step, rec)
+
     def state():
         if args.workload == "gpt2":
             return {"params": trainer.flat.params, "opt": trainer.opt.state_dict()}
@@ -149,6 +156,55 @@ def run_collective(args, jenv) -> int:
                "throughput": tokens_per_step * b.world * done / max(dt, 1e-9), "final_step": step,
                "ready_s": rec["t_ready"] - T_START}
     print("PDO_DONE " + json.dumps(summary), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def _bench(args, b, jenv, trainer, tokens_per_step, ready_rec) -> int:
+    """The bench.py contract inside a launched rank: W untimed steps, then
+    exactly K timed steps bracketed by barrier + device synchronize on both
+    sides.  Every rank publishes its own elapsed time; the launcher parent
+    (bench.py) takes the max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    dev = b.device
+
+    def fence():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if dist.is_initialized():
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    loss = None
+    for _ in range(args.warmup):
+        loss = trainer.step()
+    fence()
+    t_wall0 = time.time()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step()
+    fence()
+    dt = time.perf_counter() - t0
+    res = {"rank": b.rank, "world": b.world, "steps": args.steps, "warmup": args.warmup, "seconds": dt,
+           "t_timed_start": t_wall0, "tokens_per_step_rank": tokens_per_step,
+           "loss": float(loss.detach().float()) if loss is not None else None,
+           "ready_s": ready_rec["t_ready"] - T_START, "t_ready": ready_rec["t_ready"],
+           "backend": b.backend, "device": str(dev),
+           "grad_reduce": getattr(getattr(trainer, "ddp", None), "grad_reduce", None),
+           "buckets": len(trainer.flat.buckets) if hasattr(trainer, "flat") else None}
+    if dev.type == "cuda":
+        res["gpu_name"] = torch.cuda.get_device_name(dev)
+        res["max_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 2)
+    print("PDO_BENCH " + json.dumps(res), flush=True)
+    kv = jenv.kv_endpoints()
+    if kv:
+        from ..kv.client import KVClient
+        KVClient(kv).put(f"/pdo/{jenv.job_key()}/bench/{b.rank}", json.dumps(res))
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

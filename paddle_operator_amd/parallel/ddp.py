@@ -9,14 +9,29 @@ NCCL all-reduce to the Paddle image).  Design for MI355X:
 * a post-accumulate-grad hook counts ready parameters per bucket and launches
   ``all_reduce(SUM)`` on the bucket as soon as it is complete — RCCL runs on
   its own HIP stream, overlapping the backward GEMMs of the earlier layers;
-* the 1/world average is NOT a separate scale kernel: it is folded into the
-  fused AdamW step (``grad_scale``);
-* bucket size defaults to 64 MiB: on 8×MI355X each ring step moves
-  bucket/8 per link and 7 xGMI links run concurrent channels, so buckets below
-  ~16 MiB fall off the bandwidth plateau while buckets above ~128 MiB delay the
-  first overlap (see ``tools/allreduce_sweep.py`` / ``profiles/``).
+* bucket size: ``utils.topology.bucket_bytes_for`` (a link-model heuristic,
+  see its docstring; the callers pass it in);
+* reduction precision (``grad_reduce``):
+
+  - ``"bf16"`` (default for a bf16 arena): RCCL sums the bf16 bucket in
+    place; the 1/world average is folded into the fused AdamW step
+    (``grad_scale``).  Half the xGMI bytes of fp32.  The gradients are already
+    bf16-rounded by the dW GEMM epilogue; the ring adds at most ``world − 1``
+    more roundings of partial sums.  tests/test_ddp.py::
+    test_grad_reduce_precision_4_ranks pins the effect at 4 ranks: the bf16-wire
+    DDP gradient is within 1.5× of a single process's full-batch bf16 error
+    against the fp32 reference.
+  - ``"fp32"``: each bucket is cast to an fp32 staging arena with the 1/world
+    average folded in (``cast_scale_bf16_f32``, csrc/hip/bucket.hip), reduced
+    in fp32, and cast back into the bf16 arena once after the drain — one
+    rounding of the exact average.  2× wire bytes + ~0.35 ms of HBM passes per
+    GPT-2-medium step.  Select with ``PDO_GRAD_REDUCE=fp32``.
+
+  An fp32 arena (ResNet-50) always reduces in fp32.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -25,11 +40,22 @@ from .flat import FlatParams
 
 
 class BucketedDDP:
-    def __init__(self, flat: FlatParams, group=None, enabled: bool | None = None):
+    def __init__(self, flat: FlatParams, group=None, enabled: bool | None = None, grad_reduce: str | None = None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.enabled = (self.world > 1) if enabled is None else enabled
+        if enabled is None:
+            # PDO_DDP_ALWAYS=1: reduce even at world 1 (RCCL overlap traces on one GPU)
+            enabled = self.world > 1 or (os.environ.get("PDO_DDP_ALWAYS") == "1" and dist.is_initialized())
+        self.enabled = enabled
+        mode = grad_reduce or os.environ.get("PDO_GRAD_REDUCE") or "bf16"
+        if mode not in ("bf16", "fp32"):
+            raise ValueError(f"grad_reduce must be bf16 or fp32, not {mode!r}")
+        # an fp32 arena is reduced in fp32 either way (no staging needed)
+        self.stage = None
+        if mode == "fp32" and flat.dtype != torch.float32 and self.enabled:
+            self.stage = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
+        self.grad_reduce = "fp32" if (mode == "fp32" or flat.dtype == torch.float32) else "bf16"
         self._pending = [0] * len(flat.buckets)
         self._sizes = [len(b.slots) for b in flat.buckets]
         self._works = []
@@ -39,6 +65,7 @@ class BucketedDDP:
         self._bucket_of = flat.bucket_of()
         self._seen = set()
         self._hooks = []
+        self._staged = False
         if self.enabled:
             for s in flat.slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._hook))
@@ -69,6 +96,7 @@ class BucketedDDP:
         self._works = []
         self._next = 0
         self._seen = set()
+        self._staged = False
 
     def finish(self):
         """Call after backward: launch stragglers, make the compute stream wait."""
@@ -79,10 +107,16 @@ class BucketedDDP:
         for w in self._works:
             w.wait()
         self._works = []
+        if self._staged:
+            self._cast_back()
 
     @property
     def grad_scale(self) -> float:
-        return 1.0 / self.world if self.enabled else 1.0
+        """Factor the optimizer applies to the arena gradients (1/world unless
+        the average was already folded into the fp32 staging cast)."""
+        if not self.enabled or self.stage is not None:
+            return 1.0
+        return 1.0 / self.world
 
     # -- internals ----------------------------------------------------------
     def _hook(self, p):
@@ -113,6 +147,29 @@ class BucketedDDP:
         b = self.flat.buckets[i]
         self._launched[i] = True
         self._next = i + 1
-        w = dist.all_reduce(self.flat.grads[b.start:b.end], op=dist.ReduceOp.SUM,
-                            group=self.group, async_op=True)
+        buf = self.flat.grads[b.start:b.end]
+        if self.stage is not None:
+            # fp32 wire: stage = grad / world on the compute stream (RCCL's
+            # stream waits on it), reduce the staging slice
+            st = self.stage[b.start:b.end]
+            _cast_scale(buf, st, 1.0 / self.world)
+            buf = st
+            self._staged = True
+        w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._works.append(w)
+
+    def _cast_back(self):
+        g, st = self.flat.grads, self.stage
+        if g.is_cuda:
+            from .. import _native
+            _native.require_hip().cast_f32_bf16(st, g)
+        else:
+            g.copy_(st)
+
+
+def _cast_scale(src: torch.Tensor, dst: torch.Tensor, scale: float):
+    if src.is_cuda:
+        from .. import _native
+        _native.require_hip().cast_scale_bf16_f32(src, dst, scale)
+    else:
+        torch.mul(src.float(), scale, out=dst)

@@ -19,6 +19,7 @@ from .ops.optim import FlatAdamW
 from .parallel.ddp import BucketedDDP
 from .parallel.flat import FlatParams
 from .utils import trace
+from .utils.topology import bucket_bytes_for
 
 
 @dataclass
@@ -51,13 +52,18 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistIn
             local = local % ndev
             info.local_rank = local
         torch.cuda.set_device(local)
-    if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    # RCCL comes up eagerly even at world 1 (device_id → communicator built
+    # now, so "ready" includes comm init and the DDP path is the one that runs
+    # at scale); a CPU world of 1 needs no process group
+    if (world > 1 or backend == "nccl") and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {}
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            kw["store"] = dist.HashStore()  # single rank: no rendezvous port
         import datetime
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
@@ -66,7 +72,7 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistIn
 
 class GPT2Trainer:
     def __init__(self, cfg: GPT2Config, micro_batch: int, seq_len: int, device,
-                 dtype=torch.bfloat16, lr=3e-4, bucket_mb: int = 64, seed: int = 0):
+                 dtype=torch.bfloat16, lr=3e-4, bucket_mb: int | None = None, seed: int = 0):
         self.cfg = cfg
         self.B = micro_batch
         self.S = seq_len
@@ -78,8 +84,13 @@ class GPT2Trainer:
         model = GPT2(cfg)
         model.to(device=self.device, dtype=dtype)
         self.model = model
-        self.flat = FlatParams(model, dtype=dtype, device=self.device,
-                               bucket_bytes=bucket_mb << 20, late=("wte",))
+        if bucket_mb is None:
+            world = dist.get_world_size() if dist.is_initialized() else 1
+            nbytes = sum(p.numel() for p in model.parameters()) * torch.empty((), dtype=dtype).element_size()
+            bucket_bytes = bucket_bytes_for(world, nbytes)
+        else:
+            bucket_bytes = bucket_mb << 20
+        self.flat = FlatParams(model, dtype=dtype, device=self.device, bucket_bytes=bucket_bytes, late=("wte",))
         self.ddp = BucketedDDP(self.flat)
         self.opt = FlatAdamW(self.flat, lr=lr)
         self.gen = torch.Generator(device=self.device)

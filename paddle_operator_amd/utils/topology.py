@@ -11,6 +11,7 @@
 * ``bucket_bytes_for(...)`` — all-reduce bucket size policy for xGMI (see
   parallel/ddp.py): large enough for a ring step per link to be
   bandwidth-bound, small enough to start overlapping early.
+* ``gpu_count()`` — usable GPUs from KFD sysfs (no HIP init).
 
 Nothing here touches the GPU runtime, so the manager / agent can call it
 without initialising HIP (forking after HIP init is unsafe).
@@ -203,13 +204,45 @@ def pin_to_gpu(local_rank: int, topo: Optional[Topology] = None) -> List[int]:
     return cpus
 
 
-# measured RCCL all-reduce knee on 8×MI355X is tens of MB (profiles/); the
-# policy keeps ≥ 1 MiB per (ring step × channel) and caps at 256 MiB
+def gpu_count() -> int:
+    """GPUs this process may use, from KFD sysfs — never initialises HIP.
+
+    Same rule as ``pdo-manager``'s ``detect_gpus`` (csrc/manager/main.cpp): count
+    KFD topology nodes with SIMDs, then cap by any visible-devices list.  Safe
+    in a process that later fork+execs rank processes (the agent)."""
+    n = 0
+    for d in glob.glob("/sys/class/kfd/kfd/topology/nodes/*"):
+        try:
+            with open(os.path.join(d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count":
+                        n += int(v) > 0
+                        break
+        except (OSError, ValueError):
+            continue
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def bucket_bytes_for(world: int, grad_bytes: int, links_per_gpu: int = 7) -> int:
+    """All-reduce bucket size for the flat-arena DDP (parallel/ddp.py).
+
+    A heuristic from the xGMI link model, NOT a measured knee:
+    a ring all-reduce splits each bucket into ``world`` chunks per channel and
+    RCCL runs up to ``links_per_gpu`` channels, so ``world × links × 1 MiB``
+    keeps ≥ 1 MiB per (ring step × channel) — the regime where a step is
+    bandwidth- rather than latency-bound.  Clamped to [16, 256] MiB, and to a
+    quarter of the gradient so at least four buckets overlap the backward.
+    At world 1 there is nothing to reduce: one bucket.  Pinned by
+    tests/test_ddp.py::test_bucket_policy; the 1-GPU RCCL size sweep is
+    ``bin/pdo-allreduce-bench`` (profiles/rccl_allreduce_1gpu_r2.md)."""
     if world <= 1:
         return max(grad_bytes, 1 << 20)
-    per_step_chunk = 1 << 20
-    b = per_step_chunk * world * links_per_gpu
+    b = (1 << 20) * world * links_per_gpu
     b = max(b, 16 << 20)
     b = min(b, 256 << 20, max(grad_bytes // 4, 16 << 20))
     return int(b)
