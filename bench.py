@@ -85,6 +85,7 @@ def parse_args(argv=None):
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
+    ap.add_argument("--ready-only", action="store_true", help="only the ready trials (prints their record)")
     return ap.parse_args(argv)
 
 
@@ -173,9 +174,11 @@ class Launcher:
         t0 = self.launch(name, ranks, ["--workload", "noop", "--exit-after-ready"], "torch")
         rs = self.wait_records(name, "ready", ranks, timeout)
         self.finish(name)
-        return {"ready_s": max(r["t_ready"] for r in rs) - t0,
+        slow = max(rs, key=lambda r: r["t_ready"])
+        return {"ready_s": slow["t_ready"] - t0,
                 "pg_s": max(r["t_pg"] - r["t_start"] for r in rs),
-                "proc_start_s": min(r["t_start"] for r in rs) - t0}
+                "proc_start_s": min(r["t_start"] for r in rs) - t0,
+                "phases": slow.get("phases") or {}}
 
     def stop(self):
         self.cl.stop()
@@ -183,8 +186,15 @@ class Launcher:
 
 def ready_stats(trials):
     v = [t["ready_s"] for t in trials]
-    return {"p50": round(statistics.median(v), 4), "min": round(min(v), 4), "max": round(max(v), 4),
-            "trials": len(v), "pg_init_p50": round(statistics.median(t["pg_s"] for t in trials), 4)}
+    med = lambda xs: round(statistics.median(xs), 4)  # noqa: E731
+    out = {"p50": med(v), "min": round(min(v), 4), "max": round(max(v), 4), "trials": len(v),
+           "pg_init_p50": med([t["pg_s"] for t in trials]),
+           "proc_start_p50": med([t["proc_start_s"] for t in trials])}
+    # where the slowest rank's time went (medians over trials): create → process start
+    # is the control plane + warm launcher; the rest is inside the rank
+    keys = set().union(*(t["phases"].keys() for t in trials))
+    out["rank_phases_p50"] = {k: med([t["phases"].get(k, 0.0) for t in trials]) for k in sorted(keys)}
+    return out
 
 
 def orchestrate(a):
@@ -208,6 +218,13 @@ def orchestrate(a):
             out["ready"] = ready_stats(trials) if trials else None
             if trials:
                 log(f"ready p50 {out['ready']['p50']}s over {len(trials)} trials ({N} ranks)")
+            if a.ready_only:
+                print(json.dumps({"metric": "job-start->all-ranks-ready p50", "unit": "s", "n_gpus": N,
+                                  "mode": a.mode, "zygote": not a.no_zygote, "ready": out.get("ready"),
+                                  "env": {k: v for k, v in os.environ.items()
+                                          if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "PDO_"))}}),
+                      flush=True)
+                return 0
             name = "gpt2-bench"
             wl = ["--workload", "gpt2", "--model", a.model, "--batch", str(a.micro_batch), "--seq", str(a.seq),
                   "--steps", str(a.steps), "--warmup", str(a.warmup), "--bench", "--timeout", "600"]

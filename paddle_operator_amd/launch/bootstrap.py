@@ -45,6 +45,10 @@ class Bootstrapped:
     t_pg: float = 0.0
     t_ready: float = 0.0
     ipc_gbps: Optional[dict] = None
+    # wall-clock split of bootstrap (s): entry = process start → init() call
+    # (interpreter + imports), hip = device init, comm = communicator init,
+    # warm = warm-up all-reduce
+    phases: Optional[dict] = None
 
 
 def _wait_port(host: str, port: int, timeout_s: float, poll: float = 0.002) -> bool:
@@ -64,19 +68,23 @@ def _env_int(k, d):
 
 def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ipc_probe: bool = False,
          store=None) -> Bootstrapped:
+    t_entry = time.time()
     rank = _env_int("RANK", 0)
     world = _env_int("WORLD_SIZE", 1)
     local = _env_int("LOCAL_RANK", 0)
+    topology.pin_to_gpu(local)  # before HIP init: uses sysfs only
     gpu = torch.cuda.is_available()
     if backend is None:
         backend = "nccl" if gpu else "gloo"
-    topology.pin_to_gpu(local)  # before HIP init: uses sysfs only
     if gpu:
         torch.cuda.set_device(local)  # hipSetDevice
+        torch.cuda.init()
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    t_dev = time.time()
     b = Bootstrapped(rank, world, local, dev, backend, t_start)
+    t_comm = t_dev
     # RCCL is brought up even for a 1-rank job: "ready" then always includes
     # communicator init, and the DDP code path is the one that runs at scale.
     # A CPU (gloo) world of 1 has nothing to rendezvous with.
@@ -97,6 +105,7 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
             kw["init_method"] = f"tcp://{host}:{port}"
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        t_comm = time.time()
         if ipc_probe and gpu:
             b.ipc_gbps = ipc_probe_run(dev)
         # warm-up: forces the communicator + first ring setup before "ready"
@@ -105,6 +114,8 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
         if gpu:
             torch.cuda.synchronize(dev)
     b.t_pg = time.time()
+    b.phases = {"entry": round(t_entry - t_start, 4), "hip": round(t_dev - t_entry, 4),
+                "comm": round(t_comm - t_dev, 4), "warm": round(b.t_pg - t_comm, 4)}
     return b
 
 
@@ -151,6 +162,8 @@ def report_ready(b: Bootstrapped, job_key: str, kv_endpoints: str = "", extra: O
         rec["gen"] = os.environ["PDO_ELASTIC_GEN"]
     if b.ipc_gbps is not None:
         rec["ipc_gbps"] = b.ipc_gbps
+    if b.phases:
+        rec["phases"] = b.phases
     if extra:
         rec.update(extra)
     line = "PDO_READY " + json.dumps(rec)
