@@ -81,6 +81,11 @@ static http::Response status_resp(int code, const std::string& reason, const std
   return r;
 }
 
+static std::string lower_ascii(std::string s) {
+  for (auto& c : s) c = (char)tolower((unsigned char)c);
+  return s;
+}
+
 static http::Response api_error(const store::ApiError& e) {
   switch (e.code) {
     case store::ApiError::NotFound: return status_resp(404, "NotFound", e.what());
@@ -207,6 +212,56 @@ void mount_apiserver(http::Server& srv, store::Store& st, WatchHub& hub, Cluster
         list["items"] = items;
         http::Response r;
         r.body = list.dump();
+        return r;
+      }
+      if ((q.method == "GET" || q.method == "POST") && sub == "exec" && k->kind == "Pod") {
+        // kubectl exec / the k8s-backend coordinator: WebSocket upgrade with the
+        // channel.k8s.io protocols (kube-apiserver also accepts SPDY; pdo speaks
+        // only WebSocket).  Frames: [channel byte][data]; channel 3 = Status.
+        st.get(k->kind, ns, name);  // 404 if the pod does not exist
+        if (lower_ascii(q.headers.count("upgrade") ? q.headers.at("upgrade") : "") != "websocket" ||
+            !q.headers.count("sec-websocket-key"))
+          return status_resp(400, "BadRequest", "pods/exec requires a WebSocket upgrade (v4/v5.channel.k8s.io)");
+        std::string proto;
+        const std::string offered = q.headers.count("sec-websocket-protocol") ? q.headers.at("sec-websocket-protocol") : "";
+        for (const char* p : {"v5.channel.k8s.io", "v4.channel.k8s.io", "channel.k8s.io"})
+          if (offered.find(p) != std::string::npos) {
+            proto = p;
+            break;
+          }
+        if (proto.empty()) return status_resp(400, "BadRequest", "no supported exec subprotocol offered");
+        const std::vector<std::string> argv = q.params("command");
+        if (argv.empty()) return status_resp(400, "BadRequest", "you must specify at least 1 command");
+        const std::string container = q.param("container");
+        http::Response r;
+        r.status = 101;
+        r.headers["Upgrade"] = "websocket";
+        r.headers["Connection"] = "Upgrade";
+        r.headers["Sec-WebSocket-Accept"] = http::ws_accept_key(q.headers.at("sec-websocket-key"));
+        r.headers["Sec-WebSocket-Protocol"] = proto;
+        r.upgrade = [cluster, ns, name, container, argv](int fd) {
+          http::WsConn ws(fd);
+          const bool ok = cluster && cluster->exec(ns, name, container, argv);
+          Value s = Value::object();
+          s["metadata"] = Value::object();
+          if (ok) {
+            s["status"] = "Success";
+          } else {
+            s["status"] = "Failure";
+            s["message"] = "command terminated with non-zero exit code";
+            s["reason"] = "NonZeroExitCode";
+            Value cause = Value::object();
+            cause["reason"] = "ExitCode";
+            cause["message"] = "1";
+            s["details"]["causes"] = Value::array();
+            s["details"]["causes"].push_back(cause);
+          }
+          ws.send(http::kWsBinary, std::string(1, '\x03') + s.dump());
+          ws.send(http::kWsClose, std::string("\x03\xe8", 2));
+          int op;
+          std::string msg;
+          ws.recv(&op, &msg, 1.0);  // the client's close, if it sends one
+        };
         return r;
       }
       if (q.method == "GET" && sub == "log" && k->kind == "Pod") {

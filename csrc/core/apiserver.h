@@ -13,6 +13,8 @@
 //   /apis/coordination.k8s.io/v1/namespaces/{ns}/leases[/{name}]
 //   ?watch=true streams {"type":"ADDED|MODIFIED|DELETED","object":{…}} lines
 //   ?labelSelector=a=b,c=d
+//   GET|POST /api/v1/namespaces/{ns}/pods/{name}/exec?container=c&command=…  (WebSocket,
+//     v5/v4.channel.k8s.io — what the k8s backend's coordinator and kubectl use)
 // plus local-backend extras (no kubelet API exists here):
 //   POST /pdo/v1/namespaces/{ns}/pods/{name}/exec   {"container": "...", "command": [...]}
 //   POST /pdo/v1/namespaces/{ns}/pods/{name}/kill   {"signal": 9}

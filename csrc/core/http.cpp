@@ -10,14 +10,25 @@
 #include <sys/time.h>
 #include <unistd.h>
 
+#include <fcntl.h>
+#include <poll.h>
+
 #include <algorithm>
 #include <cctype>
+#include <chrono>
 #include <cstring>
+#include <deque>
+#include <random>
 #include <sstream>
+
+#include "base64.h"
+#include "json.h"
 
 #ifdef PDO_WITH_TLS
 #include <openssl/err.h>
+#include <openssl/pem.h>
 #include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #endif
 
 namespace pdo {
@@ -57,10 +68,40 @@ std::string Request::param(const std::string& k, const std::string& def) const {
   return def;
 }
 
+std::vector<std::string> Request::params(const std::string& k) const {
+  std::vector<std::string> out;
+  size_t pos = 0;
+  while (pos <= query.size()) {
+    size_t amp = query.find('&', pos);
+    std::string kv = query.substr(pos, amp == std::string::npos ? std::string::npos : amp - pos);
+    size_t eq = kv.find('=');
+    if (url_decode(kv.substr(0, eq)) == k) out.push_back(eq == std::string::npos ? "" : url_decode(kv.substr(eq + 1)));
+    if (amp == std::string::npos) break;
+    pos = amp + 1;
+  }
+  return out;
+}
+
+std::string url_encode(const std::string& s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string out;
+  for (unsigned char c : s) {
+    if (isalnum(c) || c == '-' || c == '_' || c == '.' || c == '~') {
+      out.push_back((char)c);
+    } else {
+      out.push_back('%');
+      out.push_back(hex[c >> 4]);
+      out.push_back(hex[c & 15]);
+    }
+  }
+  return out;
+}
+
 static const char* reason(int code) {
   switch (code) {
     case 200: return "OK";
     case 201: return "Created";
+    case 101: return "Switching Protocols";
     case 204: return "No Content";
     case 400: return "Bad Request";
     case 404: return "Not Found";
@@ -119,7 +160,7 @@ int Server::listen(const std::string& addr) {
     port_s = addr.substr(c + 1);
   }
   if (addr == "0" || port_s.empty()) port_s = "0";
-  fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+  fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (fd_ < 0) return -1;
   int one = 1;
   setsockopt(fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
@@ -168,7 +209,7 @@ void Server::accept_loop() {
   while (running_) {
     sockaddr_in sa{};
     socklen_t len = sizeof sa;
-    int cfd = ::accept(fd_, (sockaddr*)&sa, &len);
+    int cfd = ::accept4(fd_, (sockaddr*)&sa, &len, SOCK_CLOEXEC);
     if (cfd < 0) {
       if (!running_) break;
       if (errno == EINTR) continue;
@@ -272,6 +313,13 @@ void Server::serve(int fd) {
           resp.body = e.what();
         }
       }
+      if (resp.upgrade) {
+        std::string head = "HTTP/1.1 101 Switching Protocols\r\n";
+        for (auto& kv : resp.headers) head += kv.first + ": " + kv.second + "\r\n";
+        head += "\r\n";
+        if (send_all(fd, head.data(), head.size())) resp.upgrade(fd);
+        goto done;
+      }
       std::string head = "HTTP/1.1 " + std::to_string(resp.status) + " " + reason(resp.status) + "\r\n";
       head += "Content-Type: " + resp.content_type + "\r\n";
       for (auto& kv : resp.headers) head += kv.first + ": " + kv.second + "\r\n";
@@ -321,21 +369,134 @@ bool parse_url(const std::string& url, std::string* scheme, std::string* host, i
 }
 
 namespace {
+
+#ifdef PDO_WITH_TLS
+// PEM text → certificates / key through memory BIOs: kubeconfig *-data
+// material is never written to a file
+bool load_pem_ca(SSL_CTX* ctx, const std::string& pem) {
+  BIO* bio = BIO_new_mem_buf(pem.data(), (int)pem.size());
+  if (!bio) return false;
+  X509_STORE* store = SSL_CTX_get_cert_store(ctx);
+  int n = 0;
+  while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
+    if (X509_STORE_add_cert(store, x) == 1) ++n;
+    X509_free(x);
+  }
+  ERR_clear_error();  // the read loop ends on a "no start line" error
+  BIO_free(bio);
+  return n > 0;
+}
+
+bool load_pem_cert(SSL_CTX* ctx, const std::string& pem) {
+  BIO* bio = BIO_new_mem_buf(pem.data(), (int)pem.size());
+  if (!bio) return false;
+  X509* leaf = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+  bool ok = leaf && SSL_CTX_use_certificate(ctx, leaf) == 1;
+  while (ok) {  // intermediates after the leaf
+    X509* extra = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+    if (!extra) break;
+    if (SSL_CTX_add_extra_chain_cert(ctx, extra) != 1) {  // takes ownership on success
+      X509_free(extra);
+      ok = false;
+    }
+  }
+  ERR_clear_error();
+  if (leaf) X509_free(leaf);
+  BIO_free(bio);
+  return ok;
+}
+
+bool load_pem_key(SSL_CTX* ctx, const std::string& pem) {
+  BIO* bio = BIO_new_mem_buf(pem.data(), (int)pem.size());
+  if (!bio) return false;
+  EVP_PKEY* k = PEM_read_bio_PrivateKey(bio, nullptr, nullptr, nullptr);
+  const bool ok = k && SSL_CTX_use_PrivateKey(ctx, k) == 1;
+  if (k) EVP_PKEY_free(k);
+  BIO_free(bio);
+  return ok;
+}
+#endif
+
+std::string tls_identity(const ClientOptions& o) {
+  return o.ca_file + '\n' + o.cert_file + '\n' + o.key_file + '\n' + o.ca_pem + '\n' + o.cert_pem + '\n' + o.key_pem +
+         (o.insecure_skip_verify ? "\ninsecure" : "\nverify");
+}
+
+#ifdef PDO_WITH_TLS
+// one SSL_CTX per distinct trust/identity configuration, shared by every
+// connection that uses it (handshakes reuse the loaded chain and key)
+SSL_CTX* tls_context(const ClientOptions& opt, std::string* err) {
+  static std::mutex mu;
+  static std::map<std::string, SSL_CTX*> cache;  // process lifetime
+  const std::string key = tls_identity(opt);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  if (!ctx) {
+    *err = "SSL_CTX_new failed";
+    return nullptr;
+  }
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  bool ok = true;
+  if (!opt.ca_pem.empty()) {
+    ok = load_pem_ca(ctx, opt.ca_pem);
+    if (!ok) *err = "cannot load the CA certificate (PEM data)";
+  } else if (!opt.ca_file.empty()) {
+    ok = SSL_CTX_load_verify_locations(ctx, opt.ca_file.c_str(), nullptr) == 1;
+    if (!ok) *err = "cannot load the CA certificate " + opt.ca_file;
+  } else {
+    SSL_CTX_set_default_verify_paths(ctx);
+  }
+  const bool has_cert = !opt.cert_pem.empty() || !opt.cert_file.empty();
+  const bool has_key = !opt.key_pem.empty() || !opt.key_file.empty();
+  if (ok && has_cert) {
+    ok = !opt.cert_pem.empty() ? load_pem_cert(ctx, opt.cert_pem)
+                               : SSL_CTX_use_certificate_chain_file(ctx, opt.cert_file.c_str()) == 1;
+    if (!ok) *err = "cannot load the client certificate";
+  }
+  if (ok && has_key) {
+    ok = !opt.key_pem.empty() ? load_pem_key(ctx, opt.key_pem)
+                              : SSL_CTX_use_PrivateKey_file(ctx, opt.key_file.c_str(), SSL_FILETYPE_PEM) == 1;
+    if (!ok) *err = "cannot load the client key";
+  }
+  if (ok && (has_cert || has_key)) {
+    ok = has_cert && has_key && SSL_CTX_check_private_key(ctx) == 1;
+    if (!ok) *err = "client certificate and key do not match (or one is missing)";
+  }
+  if (!ok) {
+    ERR_clear_error();
+    SSL_CTX_free(ctx);
+    return nullptr;
+  }
+  SSL_CTX_set_verify(ctx, opt.insecure_skip_verify ? SSL_VERIFY_NONE : SSL_VERIFY_PEER, nullptr);
+  cache[key] = ctx;
+  return ctx;
+}
+#endif
+
 struct Conn {
   int fd = -1;
+  std::string pool_key;
 #ifdef PDO_WITH_TLS
-  SSL_CTX* ctx = nullptr;
   SSL* ssl = nullptr;
 #endif
-  ~Conn() {
+  Conn() = default;
+  Conn(const Conn&) = delete;
+  Conn& operator=(const Conn&) = delete;
+  ~Conn() { close(); }
+  void close() {
 #ifdef PDO_WITH_TLS
     if (ssl) {
       SSL_shutdown(ssl);
       SSL_free(ssl);
+      ssl = nullptr;
     }
-    if (ctx) SSL_CTX_free(ctx);
 #endif
-    if (fd >= 0) ::close(fd);
+    if (fd >= 0) {
+      ::close(fd);
+      fd = -1;
+    }
   }
   ssize_t rd(char* b, size_t n) {
 #ifdef PDO_WITH_TLS
@@ -349,7 +510,72 @@ struct Conn {
 #endif
     return send_all(fd, s.data(), s.size());
   }
+  void set_timeout(double t) {
+    timeval tv;
+    tv.tv_sec = (long)t;
+    tv.tv_usec = (long)((t - (long)t) * 1e6);
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+  }
+  // an idle pooled connection is reusable only if nothing is readable on it:
+  // readable = the server closed it (EOF) or sent stray bytes
+  bool idle_ok() const {
+    if (fd < 0) return false;
+#ifdef PDO_WITH_TLS
+    if (ssl && SSL_pending(ssl) > 0) return false;
+#endif
+    pollfd p{fd, POLLIN, 0};
+    return ::poll(&p, 1, 0) == 0;
+  }
 };
+
+// idle keep-alive connections per (server, TLS identity); bounded per key
+std::mutex g_pool_mu;
+std::map<std::string, std::deque<std::unique_ptr<Conn>>> g_pool;
+constexpr size_t kPoolPerKey = 8;
+
+std::unique_ptr<Conn> pool_take(const std::string& key) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  auto it = g_pool.find(key);
+  if (it == g_pool.end()) return nullptr;
+  while (!it->second.empty()) {
+    std::unique_ptr<Conn> c = std::move(it->second.back());
+    it->second.pop_back();
+    if (c->idle_ok()) return c;
+  }
+  return nullptr;
+}
+
+void pool_put(std::unique_ptr<Conn> c) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  auto& q = g_pool[c->pool_key];
+  if (q.size() < kPoolPerKey) q.push_back(std::move(c));
+}
+
+bool is_ip_literal(const std::string& host) {
+  unsigned char buf[sizeof(in6_addr)];
+  return inet_pton(AF_INET, host.c_str(), buf) == 1 || inet_pton(AF_INET6, host.c_str(), buf) == 1;
+}
+
+// connect with a deadline (non-blocking connect + poll), close-on-exec socket
+int connect_timeout(const addrinfo* a, double timeout_s) {
+  int fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, a->ai_protocol);
+  if (fd < 0) return -1;
+  int rc = ::connect(fd, a->ai_addr, a->ai_addrlen);
+  if (rc != 0 && errno == EINPROGRESS) {
+    pollfd p{fd, POLLOUT, 0};
+    rc = ::poll(&p, 1, (int)(timeout_s * 1000)) == 1 ? 0 : -1;
+    int soerr = 0;
+    socklen_t sl = sizeof soerr;
+    if (rc == 0 && (getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl) != 0 || soerr != 0)) rc = -1;
+  }
+  if (rc != 0) {
+    ::close(fd);
+    return -1;
+  }
+  fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) & ~O_NONBLOCK);
+  return fd;
+}
 
 bool dial(Conn& c, const std::string& scheme, const std::string& host, int port, const ClientOptions& opt,
           std::string* err) {
@@ -360,38 +586,43 @@ bool dial(Conn& c, const std::string& scheme, const std::string& host, int port,
     *err = "resolve " + host + " failed";
     return false;
   }
-  for (addrinfo* a = res; a; a = a->ai_next) {
-    c.fd = ::socket(a->ai_family, a->ai_socktype, a->ai_protocol);
-    if (c.fd < 0) continue;
-    timeval tv;
-    tv.tv_sec = (long)opt.timeout_s;
-    tv.tv_usec = (long)((opt.timeout_s - (long)opt.timeout_s) * 1e6);
-    setsockopt(c.fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
-    setsockopt(c.fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
-    if (::connect(c.fd, a->ai_addr, a->ai_addrlen) == 0) break;
-    ::close(c.fd);
-    c.fd = -1;
-  }
+  for (addrinfo* a = res; a && c.fd < 0; a = a->ai_next) c.fd = connect_timeout(a, opt.timeout_s);
   freeaddrinfo(res);
   if (c.fd < 0) {
     *err = "connect " + host + ":" + std::to_string(port) + " failed";
     return false;
   }
+  c.set_timeout(opt.timeout_s);
   int one = 1;
   setsockopt(c.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
   if (scheme == "https") {
 #ifdef PDO_WITH_TLS
-    c.ctx = SSL_CTX_new(TLS_client_method());
-    if (!opt.ca_file.empty()) SSL_CTX_load_verify_locations(c.ctx, opt.ca_file.c_str(), nullptr);
-    else SSL_CTX_set_default_verify_paths(c.ctx);
-    SSL_CTX_set_verify(c.ctx, opt.insecure_skip_verify ? SSL_VERIFY_NONE : SSL_VERIFY_PEER, nullptr);
-    if (!opt.cert_file.empty()) SSL_CTX_use_certificate_file(c.ctx, opt.cert_file.c_str(), SSL_FILETYPE_PEM);
-    if (!opt.key_file.empty()) SSL_CTX_use_PrivateKey_file(c.ctx, opt.key_file.c_str(), SSL_FILETYPE_PEM);
-    c.ssl = SSL_new(c.ctx);
+    SSL_CTX* ctx = tls_context(opt, err);
+    if (!ctx) return false;
+    c.ssl = SSL_new(ctx);
+    if (!c.ssl) {
+      *err = "SSL_new failed";
+      return false;
+    }
     SSL_set_fd(c.ssl, c.fd);
-    SSL_set_tlsext_host_name(c.ssl, host.c_str());
+    const bool ip = is_ip_literal(host);
+    if (!ip) SSL_set_tlsext_host_name(c.ssl, host.c_str());
+    if (!opt.insecure_skip_verify) {
+      // the chain must be valid AND issued for this server: its DNS name
+      // (SAN / CN) or, for an IP master, its IP SAN
+      X509_VERIFY_PARAM* vp = SSL_get0_param(c.ssl);
+      X509_VERIFY_PARAM_set_hostflags(vp, X509_CHECK_FLAG_NO_PARTIAL_WILDCARDS);
+      const int set = ip ? X509_VERIFY_PARAM_set1_ip_asc(vp, host.c_str()) : SSL_set1_host(c.ssl, host.c_str());
+      if (set != 1) {
+        *err = "cannot set the expected TLS peer name " + host;
+        return false;
+      }
+    }
     if (SSL_connect(c.ssl) != 1) {
-      *err = "TLS handshake with " + host + " failed";
+      const long vr = SSL_get_verify_result(c.ssl);
+      *err = "TLS handshake with " + host + " failed" +
+             (vr != X509_V_OK ? std::string(": ") + X509_verify_cert_error_string(vr) : std::string());
+      ERR_clear_error();
       return false;
     }
 #else
@@ -402,27 +633,37 @@ bool dial(Conn& c, const std::string& scheme, const std::string& host, int port,
   return true;
 }
 
-// reads a full response; if on_line is set, streams the body line by line
-ClientResponse do_request(const std::string& method, const std::string& url, const std::string& body,
-                          const ClientOptions& opt, const std::function<bool(const std::string&)>* on_line) {
+struct Head {
+  int status = 0;
+  std::map<std::string, std::string> headers;
+};
+
+void parse_head(const std::string& text, Head* h) {
+  std::istringstream hs(text);
+  std::string line;
+  std::getline(hs, line);
+  std::istringstream sl(line);
+  std::string ver;
+  sl >> ver >> h->status;
+  while (std::getline(hs, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    size_t colon = line.find(':');
+    if (colon == std::string::npos) continue;
+    std::string v = line.substr(colon + 1);
+    v.erase(0, v.find_first_not_of(' '));
+    h->headers[lower(line.substr(0, colon))] = v;
+  }
+}
+
+// one attempt on connection `c`; *sent_nothing = the server answered nothing
+// at all (a stale keep-alive connection: safe to retry on a fresh one)
+ClientResponse exchange(Conn& c, const std::string& req, const std::function<bool(const std::string&)>* on_line,
+                        bool* sent_nothing, bool* reusable) {
   ClientResponse out;
-  std::string scheme, host, path;
-  int port;
-  if (!parse_url(url, &scheme, &host, &port, &path)) {
-    out.error = "bad url " + url;
-    return out;
-  }
-  Conn c;
-  if (!dial(c, scheme, host, port, opt, &out.error)) return out;
-  std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + host + ":" + std::to_string(port) + "\r\n";
-  bool has_ct = false;
-  for (auto& kv : opt.headers) {
-    req += kv.first + ": " + kv.second + "\r\n";
-    if (lower(kv.first) == "content-type") has_ct = true;
-  }
-  if (!has_ct && !body.empty()) req += "Content-Type: application/json\r\n";
-  req += "Content-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body;
+  *sent_nothing = false;
+  *reusable = false;
   if (!c.wr(req)) {
+    *sent_nothing = true;
     out.error = "send failed";
     return out;
   }
@@ -432,33 +673,22 @@ ClientResponse do_request(const std::string& method, const std::string& url, con
   while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos) {
     ssize_t r = c.rd(tmp, sizeof tmp);
     if (r <= 0) {
+      *sent_nothing = buf.empty();
       out.error = "no response";
       return out;
     }
     buf.append(tmp, (size_t)r);
   }
-  {
-    std::istringstream hs(buf.substr(0, hdr_end));
-    std::string line;
-    std::getline(hs, line);
-    std::istringstream sl(line);
-    std::string ver;
-    sl >> ver >> out.status;
-    while (std::getline(hs, line)) {
-      if (!line.empty() && line.back() == '\r') line.pop_back();
-      size_t colon = line.find(':');
-      if (colon == std::string::npos) continue;
-      std::string v = line.substr(colon + 1);
-      v.erase(0, v.find_first_not_of(' '));
-      out.headers[lower(line.substr(0, colon))] = v;
-    }
-  }
+  Head h;
+  parse_head(buf.substr(0, hdr_end), &h);
+  out.status = h.status;
+  out.headers = std::move(h.headers);
   buf.erase(0, hdr_end + 4);
   const bool chunked = lower(out.headers["transfer-encoding"]).find("chunked") != std::string::npos;
   const bool has_len = out.headers.count("content-length") > 0;
   const size_t clen = has_len ? (size_t)atol(out.headers["content-length"].c_str()) : 0;
   std::string linebuf;
-  bool stop = false;
+  bool stop = false, complete = false;
   auto deliver = [&](const std::string& data) {
     if (!on_line) {
       out.body += data;
@@ -486,7 +716,13 @@ ClientResponse do_request(const std::string& method, const std::string& url, con
         if (!fill()) goto end;
       size_t n = strtoul(buf.substr(0, crlf).c_str(), nullptr, 16);
       buf.erase(0, crlf + 2);
-      if (n == 0) break;
+      if (n == 0) {
+        // trailer section ends with an empty line
+        while (buf.find("\r\n") == std::string::npos)
+          if (!fill()) goto end;
+        complete = buf.compare(0, 2, "\r\n") == 0;
+        break;
+      }
       while (buf.size() < n + 2)
         if (!fill()) goto end;
       deliver(buf.substr(0, n));
@@ -496,6 +732,9 @@ ClientResponse do_request(const std::string& method, const std::string& url, con
     while (buf.size() < clen)
       if (!fill()) break;
     deliver(buf.substr(0, std::min(clen, buf.size())));
+    complete = buf.size() == clen;
+  } else if (out.status == 204 || out.status == 304) {
+    complete = buf.empty();
   } else {
     deliver(buf);
     buf.clear();
@@ -506,8 +745,173 @@ ClientResponse do_request(const std::string& method, const std::string& url, con
   }
 end:
   if (on_line && !linebuf.empty() && !stop) (*on_line)(linebuf);
+  *reusable = complete && lower(out.headers["connection"]) != "close";
   return out;
 }
+
+ClientResponse do_request(const std::string& method, const std::string& url, const std::string& body,
+                          const ClientOptions& opt, const std::function<bool(const std::string&)>* on_line) {
+  ClientResponse out;
+  std::string scheme, host, path;
+  int port;
+  if (!parse_url(url, &scheme, &host, &port, &path)) {
+    out.error = "bad url " + url;
+    return out;
+  }
+  const bool pooled = opt.keep_alive && !on_line;
+  std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + host + ":" + std::to_string(port) + "\r\n";
+  bool has_ct = false;
+  for (auto& kv : opt.headers) {
+    req += kv.first + ": " + kv.second + "\r\n";
+    if (lower(kv.first) == "content-type") has_ct = true;
+  }
+  if (!has_ct && !body.empty()) req += "Content-Type: application/json\r\n";
+  req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
+  req += pooled ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+  req += body;
+  const std::string key = scheme + "://" + host + ":" + std::to_string(port) + "#" +
+                          std::to_string(std::hash<std::string>{}(tls_identity(opt)));
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    std::unique_ptr<Conn> c = pooled ? pool_take(key) : nullptr;
+    const bool reused = c != nullptr;
+    if (!c) {
+      c.reset(new Conn);
+      if (!dial(*c, scheme, host, port, opt, &out.error)) return out;
+      c->pool_key = key;
+    } else {
+      c->set_timeout(opt.timeout_s);
+    }
+    bool nothing = false, reusable = false;
+    out = exchange(*c, req, on_line, &nothing, &reusable);
+    if (out.status == 0 && reused && nothing) continue;  // the server dropped an idle connection
+    if (pooled && reusable) pool_put(std::move(c));
+    return out;
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ SHA-1 (RFC 3174; WebSocket handshake only)
+std::string sha1(const std::string& msg) {
+  uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  std::string m = msg;
+  const uint64_t bits = (uint64_t)msg.size() * 8;
+  m.push_back((char)0x80);
+  while (m.size() % 64 != 56) m.push_back(0);
+  for (int i = 7; i >= 0; --i) m.push_back((char)(bits >> (8 * i)));
+  auto rol = [](uint32_t x, int n) { return (x << n) | (x >> (32 - n)); };
+  for (size_t off = 0; off < m.size(); off += 64) {
+    uint32_t w[80];
+    for (int i = 0; i < 16; ++i)
+      w[i] = (uint32_t)(uint8_t)m[off + 4 * i] << 24 | (uint32_t)(uint8_t)m[off + 4 * i + 1] << 16 |
+             (uint32_t)(uint8_t)m[off + 4 * i + 2] << 8 | (uint32_t)(uint8_t)m[off + 4 * i + 3];
+    for (int i = 16; i < 80; ++i) w[i] = rol(w[i - 3] ^ w[i - 8] ^ w[i - 14] ^ w[i - 16], 1);
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+    for (int i = 0; i < 80; ++i) {
+      uint32_t f, k;
+      if (i < 20) f = (b & c) | (~b & d), k = 0x5A827999u;
+      else if (i < 40) f = b ^ c ^ d, k = 0x6ED9EBA1u;
+      else if (i < 60) f = (b & c) | (b & d) | (c & d), k = 0x8F1BBCDCu;
+      else f = b ^ c ^ d, k = 0xCA62C1D6u;
+      const uint32_t t = rol(a, 5) + f + e + k + w[i];
+      e = d, d = c, c = rol(b, 30), b = a, a = t;
+    }
+    h[0] += a, h[1] += b, h[2] += c, h[3] += d, h[4] += e;
+  }
+  std::string out;
+  for (uint32_t x : h)
+    for (int i = 3; i >= 0; --i) out.push_back((char)(x >> (8 * i)));
+  return out;
+}
+
+// ------------------------------------------------------------------ WebSocket framing (RFC 6455 §5)
+std::string make_frame(int opcode, const std::string& pl, bool mask) {
+  std::string f;
+  f.push_back((char)(0x80 | (opcode & 0x0f)));
+  const unsigned char mbit = mask ? 0x80 : 0;
+  const uint64_t n = pl.size();
+  if (n < 126) {
+    f.push_back((char)(mbit | n));
+  } else if (n < 65536) {
+    f.push_back((char)(mbit | 126));
+    f.push_back((char)(n >> 8));
+    f.push_back((char)(n & 0xff));
+  } else {
+    f.push_back((char)(mbit | 127));
+    for (int i = 7; i >= 0; --i) f.push_back((char)(n >> (8 * i)));
+  }
+  if (!mask) return f + pl;
+  static thread_local std::mt19937 rng{std::random_device{}()};
+  const uint32_t k = rng();
+  const char key[4] = {(char)(k >> 24), (char)(k >> 16), (char)(k >> 8), (char)k};
+  f.append(key, 4);
+  for (size_t i = 0; i < pl.size(); ++i) f.push_back((char)(pl[i] ^ key[i & 3]));
+  return f;
+}
+
+// one frame out of `buf`, refilled by fill(); payload unmasked
+bool parse_frame(std::string& buf, const std::function<bool()>& fill, bool* fin, int* opcode, std::string* pl) {
+  auto need = [&](size_t n) {
+    while (buf.size() < n)
+      if (!fill()) return false;
+    return true;
+  };
+  if (!need(2)) return false;
+  const unsigned char b0 = (unsigned char)buf[0], b1 = (unsigned char)buf[1];
+  *fin = (b0 & 0x80) != 0;
+  *opcode = b0 & 0x0f;
+  const bool masked = (b1 & 0x80) != 0;
+  uint64_t len = b1 & 0x7f;
+  size_t hdr = 2;
+  if (len == 126) {
+    if (!need(4)) return false;
+    len = (uint64_t)(unsigned char)buf[2] << 8 | (unsigned char)buf[3];
+    hdr = 4;
+  } else if (len == 127) {
+    if (!need(10)) return false;
+    len = 0;
+    for (int i = 0; i < 8; ++i) len = len << 8 | (unsigned char)buf[2 + i];
+    hdr = 10;
+  }
+  if (len > (64ull << 20)) return false;  // 64 MiB per frame is far beyond any exec stream chunk
+  const size_t mk = hdr;
+  if (masked) hdr += 4;
+  if (!need(hdr + (size_t)len)) return false;
+  pl->assign(buf, hdr, (size_t)len);
+  if (masked)
+    for (size_t i = 0; i < pl->size(); ++i) (*pl)[i] = (char)((*pl)[i] ^ buf[mk + (i & 3)]);
+  buf.erase(0, hdr + (size_t)len);
+  return true;
+}
+
+// one message: continuation frames reassembled, pings answered through pong()
+bool read_message(std::string& buf, const std::function<bool()>& fill, const std::function<bool(const std::string&)>& pong,
+                  int* opcode, std::string* msg) {
+  msg->clear();
+  int first = -1;
+  while (true) {
+    bool fin;
+    int op;
+    std::string pl;
+    if (!parse_frame(buf, fill, &fin, &op, &pl)) return false;
+    if (op == kWsPing) {
+      if (!pong(pl)) return false;
+      continue;
+    }
+    if (op == kWsPong) continue;
+    if (op == kWsClose) {
+      *opcode = kWsClose;
+      *msg = pl;
+      return true;
+    }
+    if (first < 0) first = op;
+    *msg += pl;
+    if (fin) {
+      *opcode = first;
+      return true;
+    }
+  }
+}
+
 }  // namespace
 
 ClientResponse request(const std::string& method, const std::string& url, const std::string& body,
@@ -518,6 +922,124 @@ ClientResponse request(const std::string& method, const std::string& url, const 
 ClientResponse stream_lines(const std::string& method, const std::string& url, const std::string& body,
                             const std::function<bool(const std::string&)>& on_line, const ClientOptions& opt) {
   return do_request(method, url, body, opt, &on_line);
+}
+
+std::string ws_accept_key(const std::string& client_key) {
+  return b64encode(sha1(client_key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11"));
+}
+
+bool WsConn::send(int opcode, const std::string& payload) {
+  const std::string f = make_frame(opcode, payload, false);
+  return send_all(fd_, f.data(), f.size());
+}
+
+bool WsConn::recv(int* opcode, std::string* payload, double timeout_s) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  auto fill = [&]() -> bool {
+    const double left =
+        std::chrono::duration<double>(deadline - std::chrono::steady_clock::now()).count();
+    if (left <= 0) return false;
+    pollfd p{fd_, POLLIN, 0};
+    if (::poll(&p, 1, (int)(left * 1000) + 1) != 1) return false;
+    char tmp[16384];
+    ssize_t r = ::recv(fd_, tmp, sizeof tmp, 0);
+    if (r <= 0) return false;
+    buf_.append(tmp, (size_t)r);
+    return true;
+  };
+  auto pong = [&](const std::string& pl) { return send(kWsPong, pl); };
+  return read_message(buf_, fill, pong, opcode, payload);
+}
+
+ExecResult ws_exec(const std::string& url, const ClientOptions& opt) {
+  ExecResult r;
+  std::string scheme, host, path;
+  int port;
+  if (!parse_url(url, &scheme, &host, &port, &path)) {
+    r.error = "bad url " + url;
+    return r;
+  }
+  if (scheme == "ws") scheme = "http";
+  if (scheme == "wss") scheme = "https";
+  Conn c;
+  if (!dial(c, scheme, host, port, opt, &r.error)) return r;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(opt.timeout_s);
+  std::string nonce(16, '\0');
+  {
+    static thread_local std::mt19937 rng{std::random_device{}()};
+    for (auto& ch : nonce) ch = (char)(rng() & 0xff);
+  }
+  const std::string key = b64encode(nonce);
+  std::string req = "GET " + path + " HTTP/1.1\r\nHost: " + host + ":" + std::to_string(port) + "\r\n";
+  for (auto& kv : opt.headers) req += kv.first + ": " + kv.second + "\r\n";
+  req += "Connection: Upgrade\r\nUpgrade: websocket\r\nSec-WebSocket-Version: 13\r\nSec-WebSocket-Key: " + key +
+         "\r\nSec-WebSocket-Protocol: v5.channel.k8s.io, v4.channel.k8s.io\r\n\r\n";
+  if (!c.wr(req)) {
+    r.error = "send failed";
+    return r;
+  }
+  std::string buf;
+  char tmp[16384];
+  auto fill = [&]() -> bool {
+    if (std::chrono::steady_clock::now() > deadline) return false;
+    ssize_t n = c.rd(tmp, sizeof tmp);
+    if (n <= 0) return false;
+    buf.append(tmp, (size_t)n);
+    return true;
+  };
+  size_t hdr_end;
+  while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos)
+    if (!fill()) {
+      r.error = "no upgrade response";
+      return r;
+    }
+  Head h;
+  parse_head(buf.substr(0, hdr_end), &h);
+  buf.erase(0, hdr_end + 4);
+  if (h.status != 101) {
+    r.error = "exec upgrade refused: HTTP " + std::to_string(h.status) + " " + buf.substr(0, 300);
+    return r;
+  }
+  if (lower(h.headers["upgrade"]) != "websocket" || h.headers["sec-websocket-accept"] != ws_accept_key(key)) {
+    r.error = "bad WebSocket handshake (Upgrade / Sec-WebSocket-Accept)";
+    return r;
+  }
+  r.protocol = h.headers["sec-websocket-protocol"];
+  auto pong = [&](const std::string& pl) { return c.wr(make_frame(kWsPong, pl, true)); };
+  while (true) {
+    int op;
+    std::string msg;
+    if (!read_message(buf, fill, pong, &op, &msg)) break;  // EOF / timeout
+    if (op == kWsClose) break;
+    if (msg.empty()) continue;
+    const unsigned char ch = (unsigned char)msg[0];
+    if (ch == 1) r.out.append(msg, 1, std::string::npos);
+    else if (ch == 2) r.err.append(msg, 1, std::string::npos);
+    else if (ch == 3) r.status.append(msg, 1, std::string::npos);
+  }
+  std::string code = "\x03\xe8";  // 1000 normal closure
+  c.wr(make_frame(kWsClose, code, true));
+  if (r.status.empty()) {
+    r.error = std::chrono::steady_clock::now() > deadline ? "exec timed out" : "exec stream ended without a Status";
+    return r;
+  }
+  // metav1.Status on the error channel: Success, or Failure with an ExitCode cause
+  json::Value st;
+  try {
+    st = json::Value::parse(r.status);
+  } catch (const std::exception& e) {
+    r.error = std::string("bad exec Status: ") + e.what();
+    return r;
+  }
+  if (st.get("status").str() == "Success") {
+    r.ok = true;
+    r.exit_code = 0;
+    return r;
+  }
+  for (auto& cause : st.at_path("details.causes").arr())
+    if (cause.get("reason").str() == "ExitCode") r.exit_code = atoi(cause.get("message").str().c_str());
+  r.error = st.get("message").str("exec failed");
+  return r;
 }
 
 }  // namespace http

@@ -5,7 +5,14 @@
 // KV server and the local API server serve a handful of clients), keep-alive,
 // Content-Length bodies, chunked streaming responses for watches.
 // Client: http:// (and https:// when built with OpenSSL, for the Kubernetes
-// REST backend), Content-Length and chunked responses, line streaming.
+// REST backend), Content-Length and chunked responses, line streaming,
+// keep-alive connection reuse; TLS verifies the peer's chain AND host name.
+// WebSocket (RFC 6455) both ways: the server upgrades a request
+// (Response::upgrade) and ws_exec() speaks the Kubernetes pods/exec
+// channel protocol (v5/v4.channel.k8s.io) — the transport the reference's
+// start-order coordinator uses (controllers/paddlejob_controller.go:491-518,
+// there through SPDY).
+// Every socket is close-on-exec: the agent fork+execs ranks from this process.
 #pragma once
 
 #include <atomic>
@@ -27,6 +34,7 @@ struct Request {
   std::map<std::string, std::string> headers;  // lower-case keys
   std::string body;
   std::string param(const std::string& k, const std::string& def = "") const;
+  std::vector<std::string> params(const std::string& k) const;  // repeated keys (?command=a&command=b)
 };
 
 class StreamWriter {
@@ -43,6 +51,9 @@ struct Response {
   std::map<std::string, std::string> headers;
   // streaming: called after headers are sent (chunked); return when done
   std::function<void(StreamWriter&)> stream;
+  // protocol upgrade (status 101): called with the raw connection after the
+  // response head; the connection is closed when it returns
+  std::function<void(int fd)> upgrade;
 };
 
 using Handler = std::function<Response(const Request&)>;
@@ -89,8 +100,10 @@ struct ClientResponse {
 struct ClientOptions {
   double timeout_s = 10;
   std::map<std::string, std::string> headers;
-  std::string ca_file, cert_file, key_file;  // TLS (https)
+  std::string ca_file, cert_file, key_file;  // TLS (https), PEM files
+  std::string ca_pem, cert_pem, key_pem;     // or PEM text (kubeconfig *-data): never written to disk
   bool insecure_skip_verify = false;
+  bool keep_alive = true;  // reuse connections to the same server (not for streams)
 };
 
 ClientResponse request(const std::string& method, const std::string& url, const std::string& body = "",
@@ -101,6 +114,33 @@ ClientResponse stream_lines(const std::string& method, const std::string& url, c
 
 bool parse_url(const std::string& url, std::string* scheme, std::string* host, int* port, std::string* path);
 std::string url_decode(const std::string& s);
+std::string url_encode(const std::string& s);
+
+// ------------------------------------------------------------ WebSocket
+enum WsOpcode { kWsText = 1, kWsBinary = 2, kWsClose = 8, kWsPing = 9, kWsPong = 10 };
+std::string ws_accept_key(const std::string& client_key);  // base64(SHA-1(key + GUID))
+// server side of an upgraded connection (server frames are unmasked)
+class WsConn {
+ public:
+  explicit WsConn(int fd) : fd_(fd) {}
+  bool send(int opcode, const std::string& payload);
+  // one message (fragments reassembled, pings answered); false on error / timeout / EOF
+  bool recv(int* opcode, std::string* payload, double timeout_s);
+
+ private:
+  int fd_;
+  std::string buf_;
+};
+
+struct ExecResult {
+  bool ok = false;     // upgraded, a Status arrived, and it says Success
+  int exit_code = -1;  // 0 on Success, the ExitCode cause otherwise
+  std::string protocol, out, err, status, error;
+};
+// Kubernetes pods/exec over WebSocket: GET `url` (…/pods/{name}/exec?container=…
+// &command=…) with an Upgrade to v5/v4.channel.k8s.io, demultiplex stdout (1) /
+// stderr (2), read the channel-3 metav1.Status.  Bounded by opt.timeout_s.
+ExecResult ws_exec(const std::string& url, const ClientOptions& opt);
 
 }  // namespace http
 }  // namespace pdo

@@ -25,13 +25,6 @@ static std::string read_file(const std::string& p) {
   return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
 }
 
-static std::string write_temp(const std::string& content, const std::string& tag) {
-  std::string path = "/tmp/pdo-k8s-" + tag + "-" + std::to_string(getpid()) + ".pem";
-  std::ofstream f(path);
-  f << content;
-  return path;
-}
-
 bool Config::load(const std::string& kubeconfig, const std::string& master, Config* out, std::string* err) {
   Config c;
   std::string kc = kubeconfig;
@@ -76,15 +69,16 @@ bool Config::load(const std::string& kubeconfig, const std::string& master, Conf
     c.insecure = cluster.get("insecure-skip-tls-verify").as_bool();
     c.ca_file = cluster.get("certificate-authority").str();
     std::string dec;
+    // *-data fields stay in memory (loaded through BIOs by the TLS client)
     if (c.ca_file.empty() && b64decode(cluster.get("certificate-authority-data").str(), &dec) && !dec.empty())
-      c.ca_file = write_temp(dec, "ca");
+      c.ca_pem = dec;
     c.token = user.get("token").str();
     c.cert_file = user.get("client-certificate").str();
     c.key_file = user.get("client-key").str();
     if (c.cert_file.empty() && b64decode(user.get("client-certificate-data").str(), &dec) && !dec.empty())
-      c.cert_file = write_temp(dec, "cert");
+      c.cert_pem = dec;
     if (c.key_file.empty() && b64decode(user.get("client-key-data").str(), &dec) && !dec.empty())
-      c.key_file = write_temp(dec, "key");
+      c.key_pem = dec;
     if (!ctx.get("namespace").str().empty()) c.ns = ctx.get("namespace").str();
   }
   if (!master.empty()) c.server = master;
@@ -102,6 +96,9 @@ http::ClientOptions Config::client(double timeout_s) const {
   o.ca_file = ca_file;
   o.cert_file = cert_file;
   o.key_file = key_file;
+  o.ca_pem = ca_pem;
+  o.cert_pem = cert_pem;
+  o.key_pem = key_pem;
   o.insecure_skip_verify = insecure;
   if (!token.empty()) o.headers["Authorization"] = "Bearer " + token;
   o.headers["Accept"] = "application/json";
@@ -301,13 +298,22 @@ int run_manager(const std::string& kubeconfig, const std::string& master, const 
   co.watch_namespace = ns;
   co.workers = workers;
   co.graceful_pod_delete = false;  // the real kubelet handles termination
-  ExecFn ex = [](const std::string& pns, const std::string& pod, const std::string& c,
-                 const std::vector<std::string>&) {
-    // pods/exec needs the SPDY/websocket streaming protocol; the fast path's
-    // ConfigMap barrier needs no exec.  Run compat mode with --initImage "".
-    log::error("controller", "exec not supported on the k8s backend",
-               {{"pod", pns + "/" + pod}, {"container", c}});
-    return false;
+  // start-order coordinator release (compat / --initImage): `touch goon` in the
+  // coord-paddle container through pods/exec over WebSocket, 3 s bound
+  // (controllers/paddlejob_controller.go:491-518)
+  ExecFn ex = [&cfg](const std::string& pns, const std::string& pod, const std::string& c,
+                     const std::vector<std::string>& argv) {
+    std::string url = cfg.server + "/api/v1/namespaces/" + http::url_encode(pns) + "/pods/" + http::url_encode(pod) +
+                      "/exec?container=" + http::url_encode(c) + "&stdout=true&stderr=true";
+    for (auto& a : argv) url += "&command=" + http::url_encode(a);
+    http::ClientOptions o = cfg.client(3.0);
+    o.headers.erase("Accept");
+    const http::ExecResult r = http::ws_exec(url, o);
+    if (!r.ok)
+      log::error("controller", "exec in pod failed",
+                 {{"pod", pns + "/" + pod}, {"container", c}, {"error", r.error},
+                  {"exit_code", std::to_string(r.exit_code)}});
+    return r.ok;
   };
   Controller ctrl(&cache, &api, kvc.get(), &ports, ex, co);
 

@@ -30,6 +30,7 @@ struct Config {
   std::string server;  // https://host:6443
   std::string token;
   std::string ca_file, cert_file, key_file;
+  std::string ca_pem, cert_pem, key_pem;  // kubeconfig *-data: in memory only, never written to disk
   bool insecure = false;
   std::string ns = "default";  // namespace of the in-cluster pod (leases)
   static bool load(const std::string& kubeconfig, const std::string& master, Config* out, std::string* err);

@@ -206,6 +206,58 @@ static void test_kv_and_http() {
   srv.stop();
 }
 
+// WebSocket handshake key (RFC 6455 §1.3 example), keep-alive reuse, and a
+// pods/exec-style upgrade round trip between the server and ws_exec
+static void test_websocket_and_keepalive() {
+  CHECK(pdo::http::ws_accept_key("dGhlIHNhbXBsZSBub25jZQ==") == "s3pPLMBiTxaQ9kYGzzhZRbK+xOo=");
+  CHECK(pdo::http::url_encode("a b/c&d") == "a%20b%2Fc%26d");
+  pdo::http::Server srv;
+  std::atomic<int> hits{0};
+  srv.route("GET", "/ping", [&](const pdo::http::Request&) {
+    ++hits;
+    pdo::http::Response r;
+    r.body = "{\"ok\":true}";
+    return r;
+  });
+  srv.route("GET", "/exec", [](const pdo::http::Request& q) {
+    pdo::http::Response r;
+    r.status = 101;
+    r.headers["Upgrade"] = "websocket";
+    r.headers["Connection"] = "Upgrade";
+    r.headers["Sec-WebSocket-Accept"] = pdo::http::ws_accept_key(q.headers.at("sec-websocket-key"));
+    r.headers["Sec-WebSocket-Protocol"] = "v4.channel.k8s.io";
+    const auto cmd = q.params("command");
+    r.upgrade = [cmd](int fd) {
+      pdo::http::WsConn ws(fd);
+      std::string joined;
+      for (auto& c : cmd) joined += c + " ";
+      ws.send(pdo::http::kWsBinary, std::string(1, '\x01') + joined);
+      ws.send(pdo::http::kWsBinary, std::string(1, '\x02') + std::string(70000, 'e'));  // 64-bit length form
+      const std::string ok = "{\"status\":\"Success\"}";
+      const std::string bad =
+          "{\"status\":\"Failure\",\"message\":\"bad\",\"details\":{\"causes\":[{\"message\":\"7\","
+          "\"reason\":\"ExitCode\"}]}}";
+      ws.send(pdo::http::kWsBinary, std::string(1, '\x03') + (cmd.size() == 2 ? ok : bad));
+      ws.send(pdo::http::kWsClose, "");
+    };
+    return r;
+  });
+  int port = srv.listen("127.0.0.1:0");
+  CHECK(port > 0);
+  srv.start();
+  const std::string base = "http://127.0.0.1:" + std::to_string(port);
+  for (int i = 0; i < 5; ++i) CHECK(pdo::http::request("GET", base + "/ping").status == 200);
+  CHECK(hits == 5);
+  auto r = pdo::http::ws_exec(base + "/exec?command=touch&command=goon", {});
+  CHECK(r.ok && r.exit_code == 0 && r.out == "touch goon " && r.err.size() == 70000 &&
+        r.protocol == "v4.channel.k8s.io");
+  auto f = pdo::http::ws_exec(base + "/exec?command=false", {});
+  CHECK(!f.ok && f.exit_code == 7 && f.error == "bad");
+  auto n = pdo::http::ws_exec(base + "/ping", {});  // no upgrade → refused cleanly
+  CHECK(!n.ok && n.error.find("HTTP 200") != std::string::npos);
+  srv.stop();
+}
+
 static void test_yaml() {
   const char* y = R"(apiVersion: v1
 clusters:
@@ -270,6 +322,7 @@ int main() {
   test_store_and_gc();
   test_workqueue();
   test_kv_and_http();
+  test_websocket_and_keepalive();
   test_yaml();
   test_cluster_sim_multiworker();
   test_cluster_without_controller();

@@ -80,9 +80,9 @@ def _child(req, fds, listener):
         os.setsid()
         for target, fd in zip((0, 1, 2), fds):
             os.dup2(fd, target)
-        for fd in fds:
-            if fd > 2:
-                os.close(fd)
+        # nothing of the zygote's survives into the rank: its selector, the other
+        # clients' connections and the passed originals (0-2 now hold the client's)
+        os.closerange(3, 65536)
         signal.signal(signal.SIGTERM, signal.SIG_DFL)
         signal.signal(signal.SIGINT, signal.default_int_handler)
         signal.signal(signal.SIGCHLD, signal.SIG_DFL)

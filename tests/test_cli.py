@@ -95,6 +95,31 @@ spec:
     assert not any(j["metadata"]["name"] == "demo" for j in c.list())
 
 
+FD_PROBE = ("import os\n"
+            "def is_open(fd):\n"
+            "    try:\n"
+            "        os.fstat(fd)\n"
+            "        return True\n"
+            "    except OSError:\n"
+            "        return False\n"
+            "print('OPEN_FDS', [fd for fd in range(1024) if is_open(fd)], flush=True)\n")
+
+
+def test_rank_processes_inherit_no_manager_sockets(manager):
+    """Every rank the exec agent fork+execs from the multi-threaded manager sees
+    only stdin/stdout/stderr: the API / KV / metrics listeners and their
+    connections are close-on-exec (csrc/core/http.cpp), so a crashed manager's
+    ranks never keep its ports bound."""
+    url, c, tmp = manager
+    c.create({"apiVersion": "batch.paddlepaddle.org/v1", "kind": "PaddleJob", "metadata": {"name": "fds"},
+              "spec": {"cleanPodPolicy": "Never", "worker": {"replicas": 1, "template": {"spec": {"containers": [
+                  {"name": "paddle", "image": "x", "command": [sys.executable, "-c", FD_PROBE]}]}}}}})
+    c.wait("fds", "Completed", timeout=30)
+    log = c.logs("fds-worker-0")
+    line = [l for l in log.splitlines() if l.startswith("OPEN_FDS")]
+    assert line and line[0] == "OPEN_FDS [0, 1, 2]", log
+
+
 def test_pdoctl_validate_rejects_bad_schema(tmp_path, capsys):
     bad = tmp_path / "bad.yaml"
     bad.write_text("apiVersion: batch.paddlepaddle.org/v1\nkind: PaddleJob\nmetadata: {name: b}\n"
@@ -176,6 +201,60 @@ def test_k8s_backend_against_rest_apiserver(tmp_path):
         # leader election went through the Lease API of the cluster process
         lease = c._req("GET", "/apis/coordination.k8s.io/v1/namespaces/default/leases/b2a304f2.paddlepaddle.org")
         assert (lease.get("spec") or {}).get("holderIdentity")
+    finally:
+        for p in (op, cluster):
+            if p is not None and p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+        if op is not None:
+            print(open(tmp_path / "operator.log").read()[-3000:])
+
+
+def test_k8s_backend_compat_releases_coordinator_by_websocket_exec(tmp_path):
+    """Compat mode on the k8s backend: every pod gets the busybox-style
+    ``coord-paddle`` init container and the operator releases the role groups
+    in order by ``touch goon`` through pods/exec over WebSocket
+    (csrc/core/http.cpp ws_exec → the apiserver's exec upgrade), as the
+    reference does through SPDY (controllers/paddlejob_controller.go:308-330,
+    491-518).  Before this existed the shipped compat manifest deadlocked."""
+    if not os.path.exists(MANAGER):
+        pytest.skip("pdo-manager not built")
+    api = _port()
+    url = f"http://127.0.0.1:{api}"
+    cluster = _spawn(["--backend=local", "--controller=false", "--agent=exec", "--gpus=0",
+                      f"--api-bind-address=127.0.0.1:{api}", "--metrics-bind-address=0",
+                      "--health-probe-bind-address=0", f"--sandbox-root={tmp_path}/sb"], tmp_path / "cluster.log")
+    op = None
+    try:
+        c = PaddleJobClient(url)
+        assert _wait_api(c)
+        rank = {"name": "paddle", "image": "x", "command": [
+            sys.executable, "-c", "import os,time; print('started', os.environ['TRAINING_ROLE'], time.time(), flush=True)"]}
+        job = {"apiVersion": "batch.paddlepaddle.org/v1", "kind": "PaddleJob",
+               "metadata": {"name": "cj", "namespace": "default"},
+               "spec": {"cleanPodPolicy": "Never",
+                        "ps": {"replicas": 1, "template": {"spec": {"containers": [rank]}}},
+                        "worker": {"replicas": 2, "template": {"spec": {"containers": [rank]}}}}}
+        c.create(job)
+        op = _spawn(["--backend=k8s", f"--master={url}", "--mode=compat", "--initImage=docker.io/library/busybox:1",
+                     "--metrics-bind-address=0", "--health-probe-bind-address=0"], tmp_path / "operator.log")
+        done = c.wait("cj", "Completed", timeout=90)
+        assert done["status"]["mode"] == "PS"
+        pods = {p["metadata"]["name"]: p for p in c.pods("cj")}
+        assert set(pods) == {"cj-ps-0", "cj-worker-0", "cj-worker-1"}
+        for p in pods.values():
+            assert [ic["name"] for ic in p["spec"]["initContainers"]] == ["coord-paddle"]
+        # released in order: the pserver's main container started before any worker's
+        starts = {}
+        for n in pods:
+            log = c.logs(n)
+            assert "started" in log, (n, log)
+            starts[n] = float(log.split()[-1])
+        assert starts["cj-ps-0"] < min(starts["cj-worker-0"], starts["cj-worker-1"])
+        assert "exec in pod failed" not in open(tmp_path / "operator.log").read()
     finally:
         for p in (op, cluster):
             if p is not None and p.poll() is None:
