@@ -331,61 +331,6 @@ std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre
   return {dx, db};
 }
 
-// ---- persistent forward-layout GEMM (gemm_pnt.hip) ----
-bool gemm_pnt_supported(int64_t M, int64_t N, int64_t K) {
-  return M < (1LL << 31) && N < (1LL << 31) && pdo::gemm_pnt_ok((int)M, (int)N, (int)K, (int)K, (int)K, (int)N);
-}
-
-// epi 0: [a·bᵀ]; 1: [a·bᵀ + bias]; 2: [pre = a·bᵀ, y = gelu(pre + bias)];
-// 3: [dx = (a·bᵀ) ⊙ gelu'(pre + bias)] + db (accumulated into db_out when given, else returned)
-std::vector<at::Tensor> gemm_pnt(at::Tensor a, at::Tensor b, int64_t epi, c10::optional<at::Tensor> bias,
-                                 c10::optional<at::Tensor> pre, c10::optional<at::Tensor> db_out, int64_t grid) {
-  CHECK_IN(a); CHECK_IN(b); CHECK_BF16(a); CHECK_BF16(b);
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_pnt: a [M, K], b [N, K]");
-  TORCH_CHECK(gemm_pnt_supported(a.size(0), b.size(0), a.size(1)), "gemm_pnt: M, N % 256, K % 32, K >= 128 required");
-  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_pnt: epi 0..3");
-  const int M = a.size(0), N = b.size(0), K = a.size(1);
-  const bf16* bptr = nullptr;
-  if (epi >= 1) {
-    TORCH_CHECK(bias.has_value(), "gemm_pnt: this epilogue needs a bias");
-    CHECK_IN((*bias)); CHECK_BF16((*bias)); TORCH_CHECK(bias->numel() == N);
-    bptr = bp(*bias);
-  }
-  auto c = at::empty({M, N}, a.options());
-  if (epi <= 1) {
-    CHECK_RC(pdo::gemm_pnt(bp(a), bp(b), M, N, K, K, K, bp(c), N, (int)epi, bptr, nullptr, 0, nullptr, (int)grid,
-                           cur_stream()), "gemm_pnt");
-    return {c};
-  }
-  if (epi == 2) {
-    auto y = at::empty({M, N}, a.options());
-    CHECK_RC(pdo::gemm_pnt(bp(a), bp(b), M, N, K, K, K, bp(c), N, 2, bptr, bp(y), N, nullptr, (int)grid,
-                           cur_stream()), "gemm_pnt_gelu");
-    return {c, y};
-  }
-  TORCH_CHECK(pre.has_value(), "gemm_pnt: epi 3 needs the saved pre-activation");
-  CHECK_IN((*pre)); CHECK_BF16((*pre));
-  TORCH_CHECK(pre->dim() == 2 && pre->size(0) == M && pre->size(1) == N);
-  const int G = pdo::gemm_pnt_dbias_rows(M);
-  auto part = at::empty({(int64_t)G * N + pdo::colsum_scratch_floats(G, N)}, a.options().dtype(at::kFloat));
-  CHECK_RC(pdo::gemm_pnt(bp(a), bp(b), M, N, K, K, K, bp(c), N, 3, bptr, bp(*pre), N, fp(part), (int)grid,
-                         cur_stream()), "gemm_pnt_dgelu");
-  at::Tensor db;
-  pdo::ColOut co;
-  if (db_out.has_value()) {
-    db = *db_out;
-    CHECK_IN(db); CHECK_BF16(db); TORCH_CHECK(db.numel() == N);
-    co = pdo::ColOut::one(bp(db), N);
-    co.acc = 1;
-  } else {
-    db = at::empty_like(*bias);
-    co = pdo::ColOut::one(bp(db), N);
-  }
-  pdo::colsum(fp(part), G, N, N, co, fp(part) + (size_t)G * N, cur_stream());
-  if (db_out.has_value()) return {c};
-  return {c, db};
-}
-
 at::Tensor transpose(at::Tensor x) {
   CHECK_IN(x); CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R, C] with R, C % 64 == 0");
@@ -729,9 +674,6 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
   m.def("gemm_nt_supported", &gemm_nt_supported);
-  m.def("gemm_pnt_supported", &gemm_pnt_supported);
-  m.def("gemm_pnt", &gemm_pnt, py::arg("a"), py::arg("b"), py::arg("epi") = 0, py::arg("bias") = py::none(),
-        py::arg("pre") = py::none(), py::arg("db_out") = py::none(), py::arg("grid") = 0);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
   m.def("gemm_nt_gelu", &gemm_nt_gelu);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),

@@ -66,12 +66,6 @@ int gemm_dw(const bf16* A, const bf16* B, long long T, int M, int N, int lda, in
 // gemm_nt.hip: C[M][N] = A[M][K]·B[N][K]ᵀ with a fused epilogue
 // (0 plain, 1 +bias, 2 C = pre-activation & Y = gelu(C + bias),
 //  3 C = (A·Bᵀ)⊙gelu'(Y + bias) & fp32 column partials [gemm_nt_dbias_rows(M)][N])
-// gemm_pnt.hip: persistent variant (one workgroup per CU walks the tiles; same
-// epilogues; EPI 3 partials: gemm_pnt_dbias_rows(M) rows); grid 0 = 256
-int gemm_pnt_ok(int M, int N, int K, int lda, int ldb, int ldc);
-int gemm_pnt_dbias_rows(int M);
-int gemm_pnt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
-             const bf16* bias, bf16* Y, int ldy, float* dbias_part, int grid, hipStream_t st);
 int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc);
 int gemm_nt_dbias_rows(int M);
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
