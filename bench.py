@@ -12,7 +12,12 @@ at 1/2/4/8 MI355X".  Both halves are measured here, through the operator:
    ``amd.com/gpu`` each) are created one after the other; a trial's latency is
    PaddleJob create → the last rank's readiness record in pdo-kv, where a rank
    is ready once its RCCL communicator is up (eager ``device_id`` init, even at
-   one rank) and a warm-up all-reduce has completed (launch/bootstrap.py);
+   one rank) and a warm-up all-reduce has completed (launch/bootstrap.py).
+   Each trial starts on an idle node: the node's warm launcher has its
+   per-GPU warm slot up (HIP initialised and RCCL's device code loaded in a
+   process that then becomes the rank — launch/zygote.py); the job's own
+   communicator (world size, rendezvous, rings) is built inside the measured
+   interval.  ``--no-warm-slots`` measures without the slots;
 3. **throughput**: one PaddleJob with ``worker.replicas=N`` whose ranks run
    ``pdo-launch --workload gpt2 --model gpt2-medium --batch 64 --seq 1024
    --bench``: W untimed steps, then exactly K timed steps bracketed by barrier +
@@ -81,6 +86,8 @@ def parse_args(argv=None):
                     help="extra ready trials in the reference-equivalent compat mode")
     ap.add_argument("--mode", default="fast", choices=["fast", "compat"])
     ap.add_argument("--no-zygote", action="store_true", help="cold interpreter per rank")
+    ap.add_argument("--no-warm-slots", action="store_true",
+                    help="zygote without GPU-warm slots (every rank inits HIP + RCCL from scratch)")
     ap.add_argument("--cpu", action="store_true", help="ranks on CPU (gloo) even if GPUs are present")
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
@@ -99,6 +106,7 @@ class Launcher:
         self.port = _free_port()
         self.gpus = gpus
         self.sandbox = sandbox
+        self.zygote = zygote
         self.cl = LocalCluster(mode=mode, agent="exec", sandbox_root=sandbox,
                                nodes=[{"name": "node0", "gpus": gpus}],
                                kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote)
@@ -153,7 +161,8 @@ class Launcher:
 
     def dump_logs(self, name, tail=4000):
         import glob
-        for path in sorted(glob.glob(os.path.join(self.sandbox, f"default_{name}-*", "*.log"))):
+        for path in sorted(glob.glob(os.path.join(self.sandbox, "*", f"default_{name}-*", "*.log")) +
+                           glob.glob(os.path.join(self.sandbox, "*", "zygote.log"))):
             try:
                 with open(path) as f:
                     log(f"--- {os.path.relpath(path, self.sandbox)} (tail) ---\n{f.read()[-tail:]}")
@@ -171,6 +180,8 @@ class Launcher:
         self.cl.wait(lambda: self.cl.job(name) is None and not self.cl.pods(name), timeout=60)
 
     def ready_trial(self, name, ranks, timeout):
+        if self.zygote and self.gpus and not self.cl.wait_warm(timeout=120):
+            log("warm slots not all up after 120 s; trial runs with what is there")
         t0 = self.launch(name, ranks, ["--workload", "noop", "--exit-after-ready"], "torch")
         rs = self.wait_records(name, "ready", ranks, timeout)
         self.finish(name)
@@ -178,6 +189,7 @@ class Launcher:
         return {"ready_s": slow["t_ready"] - t0,
                 "pg_s": max(r["t_pg"] - r["t_start"] for r in rs),
                 "proc_start_s": min(r["t_start"] for r in rs) - t0,
+                "warm": sum(bool(r.get("warm_slot")) for r in rs) / len(rs),
                 "phases": slow.get("phases") or {}}
 
     def stop(self):
@@ -189,7 +201,8 @@ def ready_stats(trials):
     med = lambda xs: round(statistics.median(xs), 4)  # noqa: E731
     out = {"p50": med(v), "min": round(min(v), 4), "max": round(max(v), 4), "trials": len(v),
            "pg_init_p50": med([t["pg_s"] for t in trials]),
-           "proc_start_p50": med([t["proc_start_s"] for t in trials])}
+           "proc_start_p50": med([t["proc_start_s"] for t in trials]),
+           "warm_slot_fraction": round(sum(t["warm"] for t in trials) / len(trials), 3)}
     # where the slowest rank's time went (medians over trials): create → process start
     # is the control plane + warm launcher; the rest is inside the rank
     keys = set().union(*(t["phases"].keys() for t in trials))
@@ -208,6 +221,8 @@ def orchestrate(a):
         return 2
     gpus = N if detected else 0  # the job asks for N amd.com/gpu; the node offers exactly those
     sandbox = tempfile.mkdtemp(prefix="pdo-bench-")
+    if a.no_warm_slots:
+        os.environ["PDO_WARM_SLOTS"] = "0"  # read by the agent when it starts the zygote
     out = {}
     try:
         L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode))
@@ -273,7 +288,8 @@ def orchestrate(a):
             "micro_batch_per_gpu": a.micro_batch,
             "seq_len": a.seq,
             "parallelism": f"dp{N}",
-            "launch": f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}",
+            "launch": f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}, "
+                      f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}",
             "grad_reduce": rs[0].get("grad_reduce"),
             "buckets": rs[0].get("buckets"),
             "ops": a.ops,

@@ -66,12 +66,47 @@ Agent::~Agent() {
   stop_zygote();
 }
 
+// agent GPU indices -> HIP_VISIBLE_DEVICES values: if the agent itself was
+// restricted (HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES), map through it;
+// ROCR_VISIBLE_DEVICES is inherited untouched (applied below HIP's list)
+static std::string visible_ids(const std::vector<int>& gpus) {
+  std::vector<std::string> parent;
+  const char* pv = getenv("HIP_VISIBLE_DEVICES");
+  if (!pv || !*pv) pv = getenv("CUDA_VISIBLE_DEVICES");
+  if (pv && *pv) {
+    std::string cur;
+    for (const char* q = pv;; ++q) {
+      if (*q == ',' || *q == 0) {
+        if (!cur.empty()) parent.push_back(cur);
+        cur.clear();
+        if (!*q) break;
+      } else {
+        cur += *q;
+      }
+    }
+  }
+  std::string ids;
+  for (size_t i = 0; i < gpus.size(); ++i) {
+    const int g = gpus[i];
+    ids += (i ? "," : "") + (g < (int)parent.size() ? parent[g] : std::to_string(g));
+  }
+  return ids;
+}
+
 void Agent::start_zygote() {
   zygote_sock_ = opt_.sandbox_root + "/zygote.sock";
   ::unlink(zygote_sock_.c_str());
   std::vector<std::string> argv = opt_.zygote_cmd;
   argv.push_back("--socket");
   argv.push_back(zygote_sock_);
+  // one GPU-warm slot per node GPU (launch/zygote.py); PDO_WARM_SLOTS=0 turns them off
+  const char* ws = getenv("PDO_WARM_SLOTS");
+  if (opt_.node.gpus > 0 && !(ws && std::string(ws) == "0")) {
+    std::vector<int> all;
+    for (int i = 0; i < opt_.node.gpus; ++i) all.push_back(i);
+    argv.push_back("--warm-devices");
+    argv.push_back(visible_ids(all));
+  }
   std::vector<char*> av;
   for (auto& a : argv) av.push_back(const_cast<char*>(a.c_str()));
   av.push_back(nullptr);
@@ -222,32 +257,7 @@ bool Agent::build_env(const Rt& rt, const Value& pod, const Value& c, std::vecto
     set(name, "");
   }
   // device + sandbox env (the device plugin's job on a real node)
-  if (!rt.gpus.empty()) {
-    // indices are into the agent's own visible set: if the agent itself was
-    // restricted (HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES), map through it;
-    // ROCR_VISIBLE_DEVICES is inherited untouched (applied below HIP's list)
-    std::vector<std::string> parent;
-    const char* pv = getenv("HIP_VISIBLE_DEVICES");
-    if (!pv || !*pv) pv = getenv("CUDA_VISIBLE_DEVICES");
-    if (pv && *pv) {
-      std::string cur;
-      for (const char* q = pv;; ++q) {
-        if (*q == ',' || *q == 0) {
-          if (!cur.empty()) parent.push_back(cur);
-          cur.clear();
-          if (!*q) break;
-        } else {
-          cur += *q;
-        }
-      }
-    }
-    std::string ids;
-    for (size_t i = 0; i < rt.gpus.size(); ++i) {
-      const int g = rt.gpus[i];
-      ids += (i ? "," : "") + (g < (int)parent.size() ? parent[g] : std::to_string(g));
-    }
-    set("HIP_VISIBLE_DEVICES", ids);
-  }
+  if (!rt.gpus.empty()) set("HIP_VISIBLE_DEVICES", visible_ids(rt.gpus));
   set("PDO_POD_IP", rt.ip);
   set("PDO_NODE_NAME", opt_.node.name);
   set("PDO_SANDBOX", rt.sandbox);

@@ -165,6 +165,28 @@ class LocalCluster:
     def zygotes_ready(self) -> bool:
         return self._c.zygotes_ready()
 
+    def zygote_status(self) -> Dict[str, Optional[dict]]:
+        """Per node: the warm launcher's slot table (launch/zygote.py ``status``)."""
+        import glob
+        import os
+
+        from ..launch.zygote import query_status
+        root = self.opts.get("sandbox_root") or ""
+        return {os.path.basename(os.path.dirname(p)): query_status(p)
+                for p in sorted(glob.glob(os.path.join(root, "*", "zygote.sock")))}
+
+    def wait_warm(self, timeout: float = 120.0) -> bool:
+        """Block until every node's GPU-warm slots are up (node idle)."""
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            st = self.zygote_status()
+            if st and all(z is not None and all(s["ready"] for s in z["slots"].values())
+                          and (len(z["slots"]) + len(z.get("failed") or {})) >= len(z["devices"])
+                          for z in st.values()):
+                return True
+            time.sleep(0.02)
+        return False
+
     def stop(self):
         self._c.stop()
 

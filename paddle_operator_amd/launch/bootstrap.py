@@ -164,6 +164,8 @@ def report_ready(b: Bootstrapped, job_key: str, kv_endpoints: str = "", extra: O
         rec["ipc_gbps"] = b.ipc_gbps
     if b.phases:
         rec["phases"] = b.phases
+    # served by a GPU-warm slot of the node's zygote (HIP + RCCL code already loaded)
+    rec["warm_slot"] = os.environ.get("PDO_WARM_SLOT_USED") == "1"
     if extra:
         rec.update(extra)
     line = "PDO_READY " + json.dumps(rec)

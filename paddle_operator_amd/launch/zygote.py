@@ -19,6 +19,23 @@ server → ``PID <pid>\\n`` then ``EXIT <status>\\n`` (status = exit code, or
 128+signal).  EOF from the client (it was SIGKILLed) kills the child's
 process group.  The server is single-threaded (selector loop + WNOHANG
 reaping) so ``fork`` never happens with other Python threads alive.
+
+GPU-warm slots (``--warm-devices 0,1,…``, one per node GPU, passed by the
+agent): the import saving leaves HIP init (≈0.15 s) and RCCL communicator
+init (≈1.1 s, almost all of it RCCL loading its device code objects into the
+new process — profiles/r2_launched_bench_1gpu.md) inside every rank.  A slot is
+forked from the zygote BEFORE any HIP call, binds one GPU
+(``HIP_VISIBLE_DEVICES``), initialises HIP, builds and destroys a 1-rank RCCL
+communicator (kernels now resident) and then blocks on its socketpair.  A
+request for exactly that GPU, whose runtime-relevant environment (HIP_/HSA_/
+ROCR_/GPU_/NCCL_/RCCL_/PYTORCH_/TORCH_/AMD_/LD_ variables — read once per
+process by HIP/RCCL/torch) equals the slot's, is handed to the slot (request +
+client fds over the socketpair) instead of forking: the slot BECOMES the rank
+and builds the job's real communicator (world size, rendezvous, rings) from
+scratch — only the process-level warm-up is reused.  A replacement slot for
+that GPU is forked at once and warms while the job runs.  Requests that could
+exec (elastic agents spawn their workers) or that differ in those variables
+take the cold fork.  ``PDO_WARM_SLOT=0`` in a pod's env opts it out.
 """
 from __future__ import annotations
 
@@ -31,6 +48,7 @@ import socket
 import struct
 import sys
 import time
+from typing import Dict, List, Optional
 
 PRELOAD = (
     "torch", "torch.distributed", "torch.nn.functional", "numpy",
@@ -54,6 +72,37 @@ def preload():
     return time.time() - t0
 
 
+# variables HIP / RCCL / torch read once per process: a warm slot initialised
+# under one set of them cannot serve a request asking for another
+WARM_PREFIXES = ("HIP_", "HSA_", "ROCR_", "GPU_", "NCCL_", "RCCL_", "PYTORCH_", "TORCH_", "AMD_", "LD_", "CUDA_")
+WARM_IGNORE = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+SLOT_RETRIES = 3
+
+
+def runtime_key(env: Dict[str, str]) -> tuple:
+    return tuple(sorted((k, v) for k, v in env.items() if k.startswith(WARM_PREFIXES) and k not in WARM_IGNORE))
+
+
+def warm_device_of(req: dict, key: tuple) -> Optional[str]:
+    """The GPU id a request may take a warm slot for, or None (cold fork)."""
+    env = req.get("env") or {}
+    argv = req.get("argv") or []
+    dev = env.get("HIP_VISIBLE_DEVICES", "")
+    if not dev or "," in dev or env.get("PDO_WARM_SLOT", "1") == "0":
+        return None
+    # elastic agents fork+exec their workers: never from a HIP-initialised process
+    if "--elastic" in argv or "--worker" in argv or env.get("PADDLE_ELASTIC_JOB_ID") or env.get("PADDLE_ELASTIC_NP"):
+        return None
+    return dev if runtime_key(env) == key else None
+
+
+def _send_request(sock: socket.socket, req: dict, fds: List[int]):
+    body = json.dumps(req).encode()
+    anc = [(socket.SOL_SOCKET, socket.SCM_RIGHTS, array.array("i", fds).tobytes())] if fds else []
+    sock.sendmsg([struct.pack("<I", len(body))], anc)
+    sock.sendall(body)
+
+
 def _recv_request(conn: socket.socket):
     fds = array.array("i")
     hdr, anc, _, _ = conn.recvmsg(4, socket.CMSG_SPACE(8 * fds.itemsize))
@@ -74,15 +123,29 @@ def _recv_request(conn: socket.socket):
 
 def _child(req, fds, listener):
     """In the forked child: become the rank process and never return."""
-    rc = 1
     try:
         listener.close()
         os.setsid()
+    except BaseException:
+        os._exit(1)
+    _become_rank(req, fds)
+
+
+def _become_rank(req, fds, warm=False):
+    rc = 1
+    try:
         for target, fd in zip((0, 1, 2), fds):
             os.dup2(fd, target)
-        # nothing of the zygote's survives into the rank: its selector, the other
-        # clients' connections and the passed originals (0-2 now hold the client's)
-        os.closerange(3, 65536)
+        if warm:
+            # a warm slot closed the zygote's descriptors before HIP init; what it
+            # holds now is the HIP runtime's (/dev/kfd, render node, ...)
+            for fd in fds:
+                if fd > 2:
+                    os.close(fd)
+        else:
+            # nothing of the zygote's survives into the rank: its selector, the other
+            # clients' connections and the passed originals (0-2 now hold the client's)
+            os.closerange(3, 65536)
         signal.signal(signal.SIGTERM, signal.SIG_DFL)
         signal.signal(signal.SIGINT, signal.default_int_handler)
         signal.signal(signal.SIGCHLD, signal.SIG_DFL)
@@ -111,7 +174,69 @@ def _child(req, fds, listener):
         os._exit(rc)
 
 
-def serve(path: str, idle_exit_s: float = 0.0):
+def _warm_gpu() -> dict:
+    """HIP init + a 1-rank RCCL communicator built and destroyed (loads RCCL's
+    device code into this process), on the slot's one visible GPU."""
+    import torch
+    import torch.distributed as dist
+
+    from ..utils import topology
+    t0 = time.time()
+    topology.pin_to_gpu(0)
+    if not torch.cuda.is_available():  # a GPU node with no usable HIP device: nothing to warm
+        return {"device": "none"}
+    torch.cuda.set_device(0)
+    torch.cuda.init()
+    dev = torch.device("cuda", 0)
+    t1 = time.time()
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=dev)
+    t = torch.ones(1, device=dev)
+    dist.all_reduce(t)
+    torch.cuda.synchronize(dev)
+    dist.destroy_process_group()
+    del t
+    return {"hip_s": round(t1 - t0, 4), "rccl_s": round(time.time() - t1, 4)}
+
+
+def _slot_main(dev: str, sock: socket.socket, listener: socket.socket):
+    """A forked GPU-warm slot: warm up, report READY, wait for one request,
+    become that rank.  Never returns."""
+    try:
+        listener.close()
+        os.setsid()
+        keep = sock.fileno()
+        os.closerange(3, keep)
+        os.closerange(keep + 1, 65536)
+        for sig in (signal.SIGTERM, signal.SIGCHLD):
+            signal.signal(sig, signal.SIG_DFL)
+        os.environ.pop("CUDA_VISIBLE_DEVICES", None)
+        os.environ["HIP_VISIBLE_DEVICES"] = dev
+        info = _warm_gpu()
+        info["pid"] = os.getpid()
+        sock.sendall(f"READY {json.dumps(info)}\n".encode())
+        req, fds = _recv_request(sock)
+    except EOFError:  # the zygote is shutting down
+        os._exit(0)
+    except BaseException as e:
+        try:
+            sock.sendall(f"FAIL {type(e).__name__}: {e}\n".encode())
+        except OSError:
+            pass
+        os._exit(3)
+    sock.close()
+    req.setdefault("env", {})["PDO_WARM_SLOT_USED"] = "1"
+    _become_rank(req, fds, warm=True)
+
+
+class _Slot:
+    def __init__(self, dev, pid, sock):
+        self.dev, self.pid, self.sock = dev, pid, sock
+        self.ready = False
+        self.t_spawn = time.time()
+        self.info: dict = {}
+
+
+def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]] = None):
     took = preload()
     try:
         os.unlink(path)
@@ -129,9 +254,90 @@ def serve(path: str, idle_exit_s: float = 0.0):
     stop = []
     signal.signal(signal.SIGTERM, lambda *a: stop.append(1))
     last_activity = time.time()
+    key = runtime_key(dict(os.environ))
+    slots: Dict[str, _Slot] = {}       # device -> its (single) warm slot
+    slot_pids: Dict[int, _Slot] = {}
+    slot_fails: Dict[str, int] = {}
+    pending: Dict[str, list] = {}      # device -> [(conn, req, fds)] waiting for a warming slot
+    served = {"warm": 0, "cold": 0}
+
+    def log(msg):
+        print(f"[pdo-zygote] {msg}", flush=True)
+
+    def spawn_slot(dev):
+        if stop or slot_fails.get(dev, 0) >= SLOT_RETRIES or dev in slots:
+            return
+        a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
+        pid = os.fork()
+        if pid == 0:
+            a.close()
+            _slot_main(dev, b, ls)
+        b.close()
+        sl = _Slot(dev, pid, a)
+        slots[dev] = sl
+        slot_pids[pid] = sl
+        sel.register(a, selectors.EVENT_READ, ("slot", sl))
+
+    def drop_slot(sl):
+        slots.pop(sl.dev, None)
+        try:
+            sel.unregister(sl.sock)
+        except (KeyError, ValueError):
+            pass
+        sl.sock.close()
+
+    def attach(pid, conn):
+        children[pid] = conn
+        try:
+            conn.sendall(f"PID {pid}\n".encode())
+        except OSError:
+            pass
+        conn.setblocking(False)
+        sel.register(conn, selectors.EVENT_READ, pid)
+
+    def cold(conn, req, fds):
+        pid = os.fork()
+        if pid == 0:
+            _child(req, fds, ls)
+        for fd in fds:
+            os.close(fd)
+        served["cold"] += 1
+        attach(pid, conn)
+
+    def handoff(sl, conn, req, fds):
+        try:
+            _send_request(sl.sock, req, fds)
+        except OSError as e:  # the slot died under us
+            log(f"slot {sl.dev} pid {sl.pid} handoff failed ({e}); cold fork")
+            drop_slot(sl)
+            cold(conn, req, fds)
+            return
+        for fd in fds:
+            os.close(fd)
+        drop_slot(sl)
+        slot_pids.pop(sl.pid, None)
+        served["warm"] += 1
+        attach(sl.pid, conn)
+        spawn_slot(sl.dev)  # the replacement warms while this job runs
+
+    def flush_pending(dev):
+        for conn, req, fds in pending.pop(dev, []):
+            sl = slots.get(dev)
+            if sl is not None and sl.ready:
+                handoff(sl, conn, req, fds)
+            else:
+                cold(conn, req, fds)
+
+    def status_table():
+        return {"pid": os.getpid(), "served": served,
+                "slots": {d: {"pid": sl.pid, "ready": sl.ready, **sl.info} for d, sl in slots.items()},
+                "devices": list(warm_devices or []), "failed": slot_fails}
+
+    for dev in warm_devices or []:
+        spawn_slot(dev)
     while not stop:
-        for key, _ in sel.select(timeout=0.01):
-            if key.data == "listen":
+        for skey, _ in sel.select(timeout=0.01):
+            if skey.data == "listen":
                 try:
                     conn, _ = ls.accept()
                 except BlockingIOError:
@@ -143,21 +349,47 @@ def serve(path: str, idle_exit_s: float = 0.0):
                     print(f"[pdo-zygote] bad request: {e}", file=sys.stderr, flush=True)
                     conn.close()
                     continue
-                pid = os.fork()
-                if pid == 0:
-                    _child(req, fds, ls)
-                for fd in fds:
-                    os.close(fd)
-                children[pid] = conn
-                try:
-                    conn.sendall(f"PID {pid}\n".encode())
-                except OSError:
-                    pass
-                conn.setblocking(False)
-                sel.register(conn, selectors.EVENT_READ, pid)
+                if req.get("op") == "status":
+                    try:
+                        conn.sendall(f"STATUS {json.dumps(status_table())}\n".encode())
+                    except OSError:
+                        pass
+                    conn.close()
+                    continue
                 last_activity = time.time()
+                dev = warm_device_of(req, key) if warm_devices else None
+                sl = slots.get(dev) if dev is not None else None
+                if sl is not None and sl.ready:
+                    handoff(sl, conn, req, fds)
+                elif sl is not None:  # warming: waiting is never slower than a cold start
+                    pending.setdefault(dev, []).append((conn, req, fds))
+                else:
+                    cold(conn, req, fds)
+            elif isinstance(skey.data, tuple):  # a slot's control socket
+                sl = skey.data[1]
+                try:
+                    line = sl.sock.recv(4096).decode(errors="replace")
+                except (BlockingIOError, InterruptedError):
+                    continue
+                except OSError:
+                    line = ""
+                if line.startswith("READY"):
+                    sl.ready = True
+                    try:
+                        sl.info = json.loads(line[5:].strip() or "{}")
+                    except ValueError:
+                        sl.info = {}
+                    sl.info["warm_s"] = round(time.time() - sl.t_spawn, 3)
+                    slot_fails.pop(sl.dev, None)
+                    log(f"slot gpu {sl.dev} warm in {sl.info['warm_s']}s ({sl.info})")
+                    flush_pending(sl.dev)
+                else:  # FAIL or EOF: the slot is gone; its pid is reaped below
+                    log(f"slot gpu {sl.dev} pid {sl.pid} failed: {line.strip() or 'EOF'}")
+                    slot_fails[sl.dev] = slot_fails.get(sl.dev, 0) + 1
+                    drop_slot(sl)
+                    flush_pending(sl.dev)
             else:
-                pid, conn = key.data, key.fileobj
+                pid, conn = skey.data, skey.fileobj
                 try:
                     data = conn.recv(64)
                 except (BlockingIOError, InterruptedError):
@@ -178,6 +410,14 @@ def serve(path: str, idle_exit_s: float = 0.0):
                 break
             if pid == 0:
                 break
+            sl = slot_pids.pop(pid, None)
+            if sl is not None:  # an unused slot exited
+                if slots.get(sl.dev) is sl:
+                    slot_fails[sl.dev] = slot_fails.get(sl.dev, 0) + 1
+                    drop_slot(sl)
+                    flush_pending(sl.dev)
+                spawn_slot(sl.dev)
+                continue
             conn = children.pop(pid, None)
             code = os.waitstatus_to_exitcode(status)
             code = 128 - code if code < 0 else code
@@ -200,6 +440,13 @@ def serve(path: str, idle_exit_s: float = 0.0):
             os.killpg(pid, signal.SIGTERM)
         except ProcessLookupError:
             pass
+    for sl in list(slots.values()):  # idle slots exit on EOF
+        drop_slot(sl)
+    for pid in list(slot_pids):
+        try:
+            os.waitpid(pid, 0)
+        except ChildProcessError:
+            pass
     ls.close()
     try:
         os.unlink(path)
@@ -212,8 +459,31 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="pdo-zygote")
     ap.add_argument("--socket", default=os.environ.get("PDO_ZYGOTE", "/tmp/pdo-zygote.sock"))
     ap.add_argument("--idle-exit", type=float, default=0.0)
+    ap.add_argument("--warm-devices", default="",
+                    help="comma-separated GPU ids (as HIP_VISIBLE_DEVICES values) to keep a warm slot for")
     a = ap.parse_args(argv)
-    serve(a.socket, a.idle_exit)
+    serve(a.socket, a.idle_exit, [d for d in a.warm_devices.split(",") if d.strip()])
+
+
+def query_status(path: str, timeout: float = 2.0) -> Optional[dict]:
+    """The zygote's slot table (``None`` if it is not reachable)."""
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.settimeout(timeout)
+    try:
+        s.connect(path)
+        _send_request(s, {"op": "status"}, [])
+        buf = b""
+        while not buf.endswith(b"\n"):
+            chunk = s.recv(65536)
+            if not chunk:
+                break
+            buf += chunk
+    except OSError:
+        return None
+    finally:
+        s.close()
+    line = buf.decode(errors="replace").strip()
+    return json.loads(line[7:]) if line.startswith("STATUS ") else None
 
 
 if __name__ == "__main__":

@@ -477,3 +477,60 @@ def test_zygote_warm_launch_and_kill(tmp_path):
         assert cl.wait_phase("zk", T.Phase.Failed, timeout=30), cl.job("zk")["status"]
     finally:
         cl.stop()
+
+
+def test_zygote_gpu_warm_slot_handoff(tmp_path):
+    """The zygote keeps one warm slot per node GPU; a 1-GPU rank is handed to
+    it (the slot becomes the rank), a replacement slot comes up, and requests
+    that must not use a slot (opt-out, elastic) take the cold fork.  On a CPU
+    box the slot has nothing to warm; the hand-off protocol is the same."""
+    pdo_launch = os.path.join(REPO, "bin", "pdo-launch")
+    if not os.path.exists(pdo_launch):
+        pytest.skip("bin/pdo-launch not built")
+    port = _free_port()
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), zygote=True,
+                      nodes=[{"name": "node0", "gpus": 1}], kv_endpoint=f"127.0.0.1:{port}")
+    cl.serve(f"127.0.0.1:{port}")
+    cl.start()
+
+    def job(name, args, extra_env=()):
+        cont = _launcher_container(args)
+        cont["command"] = [pdo_launch] + cont["command"][3:]
+        cont["env"] += [{"name": "PDO_KV", "value": f"127.0.0.1:{port}"}] + list(extra_env)
+        cont["resources"] = {"limits": {T.AMD_GPU: 1}}
+        cl.create(T.paddlejob(name, worker={"replicas": 1, "template": {"spec": {"containers": [cont]}}},
+                              clean_pod_policy="Never"))
+
+    try:
+        assert cl.wait_warm(timeout=120), cl.zygote_status()
+        st0 = cl.zygote_status()["node0"]
+        slot_pid = st0["slots"]["0"]["pid"]
+        job("w1", ["--workload", "noop", "--exit-after-ready"])
+        assert cl.wait_phase("w1", T.Phase.Completed, timeout=60), cl.job("w1")["status"]
+        rec = _ready_rec(cl, "w1", 0)
+        assert rec["warm_slot"] is True and rec["pid"] == slot_pid, rec
+        assert cl.wait_warm(timeout=120)
+        st1 = cl.zygote_status()["node0"]
+        assert st1["served"]["warm"] == 1 and st1["slots"]["0"]["pid"] != slot_pid
+        # opted out: cold fork, the slot stays
+        job("w2", ["--workload", "noop", "--exit-after-ready"], [{"name": "PDO_WARM_SLOT", "value": "0"}])
+        assert cl.wait_phase("w2", T.Phase.Completed, timeout=60)
+        assert _ready_rec(cl, "w2", 0)["warm_slot"] is False
+        # a different runtime environment (NCCL_* read once per process): cold
+        job("w3", ["--workload", "noop", "--exit-after-ready"], [{"name": "NCCL_DEBUG", "value": "WARN"}])
+        assert cl.wait_phase("w3", T.Phase.Completed, timeout=60)
+        assert _ready_rec(cl, "w3", 0)["warm_slot"] is False
+        st2 = cl.zygote_status()["node0"]
+        assert st2["served"] == {"warm": 1, "cold": 2} and st2["slots"]["0"]["pid"] == st1["slots"]["0"]["pid"]
+        # a long-running rank on a slot: the pod kill reaches it
+        job("wk", ["--workload", "resnet50", "--tiny", "--steps", "100000"])
+        assert cl.wait_phase("wk", T.Phase.Running, timeout=60)
+        assert cl.wait(lambda: _ready_rec(cl, "wk", 0) is not None, timeout=60)
+        rec = _ready_rec(cl, "wk", 0)
+        assert rec["warm_slot"] is True
+        assert cl.kill("wk-worker-0", 15)
+        assert cl.wait_phase("wk", T.Phase.Failed, timeout=30), cl.job("wk")["status"]
+        assert cl.wait(lambda: not os.path.exists(f"/proc/{rec['pid']}") or
+                       open(f"/proc/{rec['pid']}/stat").read().split()[2] == "Z", timeout=10)
+    finally:
+        cl.stop()

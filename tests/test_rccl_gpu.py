@@ -175,3 +175,20 @@ def test_allreduce_bench_binary_runs(cuda):
     assert r.returncode == 0, r.stderr[-2000:]
     rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(rows) >= 5 and all(x["ranks"] == 1 and x["us"] > 0 for x in rows if "us" in x), r.stdout
+
+
+def test_warm_slot_ready_on_gpu(cuda):
+    """bench.py --ready-only through the operator with the node's GPU-warm slot:
+    every rank is served by a slot (HIP + RCCL code already loaded) and the
+    job's own communicator init is no longer dominated by RCCL kernel loading
+    (≈1.1 s cold, profiles/r2_launched_bench_1gpu.md)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--ready-only", "--ready-trials", "3"],
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-4000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    ready = rec["ready"]
+    assert ready["warm_slot_fraction"] == 1.0, ready
+    assert ready["rank_phases_p50"]["comm"] < 0.5, ready
+    assert ready["p50"] < 1.0, ready
