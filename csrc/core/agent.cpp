@@ -551,6 +551,15 @@ bool Agent::step(Rt& rt, const Value& pod, double now) {
     }
     return false;  // init failed with Never → pod Failed (make_status)
   }
+  // ---- native start gate (pdo.amd.com/start-gate, released by the controller)
+  if (pod.at_path("metadata.annotations").get(api::kAnnotationStartGate).as_string() == api::kGateHold) {
+    if (rt.wait_reason != "StartGated") {
+      rt.wait_reason = "StartGated";
+      return true;
+    }
+    return false;
+  }
+  if (rt.wait_reason == "StartGated") rt.wait_reason.clear();
   // ---- main containers
   bool changed = false;
   if (opt_.config_retry_s > 0 && !rt.wait_reason.empty() && now < rt.next_retry) return false;

@@ -33,6 +33,14 @@ inline constexpr const char* kLabelResourceName = "paddle-res-name";
 inline constexpr const char* kLabelResourceType = "paddle-res-type";
 inline constexpr const char* kAnnotationResource = "paddle-resource";
 inline constexpr const char* kAnnotationHostPort = "host-port";
+// native start-order barrier (fast mode, local backend): "hold" until the
+// controller flips it to "released" in ps → worker → heter order; the
+// kubelet-lite agent does not start a held pod's main containers.  Replaces
+// the busybox init container + `kubectl exec touch goon` of the reference
+// (paddlejob_controller.go:308-330,491-518) with one event-driven API write.
+inline constexpr const char* kAnnotationStartGate = "pdo.amd.com/start-gate";
+inline constexpr const char* kGateHold = "hold";
+inline constexpr const char* kGateReleased = "released";
 inline constexpr const char* kFinalizer = "finalizers.paddlepaddle.org";
 
 // ---- roles (paddlejob_types.go:37-48) in start order ps → worker → heter

@@ -140,6 +140,17 @@ static void rewrite_gpu_resources(Value& container) {
   if (container["resources"].size() == 0) container.erase("resources");
 }
 
+bool start_gated(const PaddleJob& job, const std::string& role, const Options& opt) {
+  if (!opt.start_gate || !opt.init_image.empty()) return false;
+  // ordering only matters between roles; the first role present starts at once
+  // (its pods still wait for the ConfigMap, as in the reference)
+  for (auto& r : api::role_order()) {
+    if (!job.spec.role(r)) continue;
+    return r != role;
+  }
+  return false;
+}
+
 Value construct_pod(const PaddleJob& job, const std::string& role, int idx, const Options& opt) {
   const api::ResourceSpec* rs = job.spec.role(role);
   const std::string name = res_name(job.name(), role, idx);
@@ -156,6 +167,7 @@ Value construct_pod(const PaddleJob& job, const std::string& role, int idx, cons
   Value& ann = md["annotations"];
   if (!ann.is_object()) ann = Value::object();
   ann[api::kAnnotationResource] = role;
+  if (start_gated(job, role, opt)) ann[api::kAnnotationStartGate] = api::kGateHold;
   md["name"] = name;
   md["namespace"] = job.ns();
   pod["metadata"] = md;

@@ -44,7 +44,13 @@ struct Options {
   std::vector<std::string> etcd_endpoints;  // --etcd-server (elastic)
   bool gpu_resource_rewrite = true;
   bool launcher_env = true;
+  // native start-order barrier (kAnnotationStartGate): pods of every role after
+  // the first one present are created held; no effect with an init image
+  bool start_gate = false;
 };
+
+// true if pods of `role` are created held by the native start gate
+bool start_gated(const api::PaddleJob& job, const std::string& role, const Options& opt);
 
 std::string res_name(const std::string& job, const std::string& role, int idx);
 // "<job>-<role>-<idx>" → (role, idx); ("", 0) when the tail is not an int

@@ -50,6 +50,8 @@ Cluster::Cluster(ClusterOptions opt) : opt_(std::move(opt)) {
   ControllerOptions co;
   co.plan = compat ? plan::Options::compat_defaults() : plan::Options::fast_defaults();
   if (opt_.init_image_set) co.plan.build.init_image = opt_.init_image;
+  // the local agent honours the native start gate; fast mode uses it instead of exec
+  co.plan.build.start_gate = !compat && opt_.start_gate;
   co.plan.volcano = opt_.volcano;
   co.plan.kv = opt_.elastic_kv;
   if (opt_.elastic_kv) co.plan.build.etcd_endpoints = kvc_->endpoints();

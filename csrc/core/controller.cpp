@@ -206,6 +206,20 @@ void Controller::apply(const api::PaddleJob& job, Value raw, const plan::Plan& p
             if (exec_) exec_(ns, pod, build::kCoordContainer, {"touch", "goon"});
           break;
         }
+        case Op::ReleaseGate: {
+          for (auto& pod : a.targets) {
+            Value obj;
+            if (!cache_->try_get("Pod", ns, pod, &obj)) continue;
+            obj["metadata"]["annotations"][api::kAnnotationStartGate] = api::kGateReleased;
+            try {
+              api_->update("Pod", obj);
+            } catch (const store::ApiError& e) {
+              if (e.code == store::ApiError::NotFound) continue;
+              throw;  // conflict: requeue, the next pass re-lists the held pods
+            }
+          }
+          break;
+        }
         case Op::Event: {
           record_event(raw, api::kKind, a.role.empty() ? "Normal" : a.role, a.detail, a.obj.str());
           break;

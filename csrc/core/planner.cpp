@@ -27,6 +27,7 @@ const char* op_name(Op op) {
     case Op::CreateConfigMap: return "CreateConfigMap";
     case Op::SyncNP: return "SyncNP";
     case Op::ReleaseRole: return "ReleaseRole";
+    case Op::ReleaseGate: return "ReleaseGate";
     case Op::Event: return "Event";
   }
   return "?";
@@ -295,6 +296,37 @@ Plan reconcile(const Observed& obs, const Options& opt, HostPorts* ports, double
     p.actions.push_back(act(Op::CreateConfigMap, job.name(), cm));
     p.step = "configmap/create";
     return p;
+  }
+
+  // ---------------------------------------------- 14a. native start gate (fast)
+  // Same order as the coordinator below (ps → worker → heter, a role released
+  // once every earlier role is fully Running), but event-driven: a pod status
+  // change re-runs the pass, no 1 s requeue, no exec.
+  if (!compat && opt.build.start_gate && opt.build.init_image.empty()) {
+    bool earlier_running = true;
+    for (auto& role : api::role_order()) {
+      const api::ResourceSpec* rs = job.spec.role(role);
+      if (!rs) continue;
+      Action a = act(Op::ReleaseGate, role);
+      a.role = role;
+      for (auto& pod : obs.pods) {
+        if (pod.at_path("metadata.annotations").get(api::kAnnotationResource).as_string() == role &&
+            pod.at_path("metadata.annotations").get(api::kAnnotationStartGate).as_string() == api::kGateHold &&
+            pod.at_path("metadata.deletionTimestamp").is_null())
+          a.targets.push_back(obj_name(pod));
+      }
+      if (!a.targets.empty()) {
+        if (!earlier_running) {
+          p.step = "gate/wait-" + role;
+          return p;
+        }
+        p.actions.push_back(a);
+        p.step = "gate/release-" + role;
+        return p;
+      }
+      const api::ResourceStatus* st = job.status.role(role);
+      if (!st || st->running < rs->replicas) earlier_running = false;
+    }
   }
 
   // ---------------------------------------------------------- 14. coordinator

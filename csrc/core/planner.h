@@ -50,6 +50,7 @@ enum class Op {
   CreateConfigMap,
   SyncNP,       // elastic: put /paddle/<ns>-<name>/np
   ReleaseRole,  // coordinator: `touch goon` in the coord container of these pods
+  ReleaseGate,  // native barrier: set the start-gate annotation of these pods to "released"
   Event,
 };
 const char* op_name(Op op);

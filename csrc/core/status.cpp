@@ -110,7 +110,12 @@ static void count_pods(api::Status& st, const std::vector<Value>& pods, bool cou
     rs->present = true;
     const std::string& ph = pod.at_path("status.phase").as_string();
     if (ph == "Pending") {
-      if (coord_running(pod)) rs->starting++;
+      // held at the start barrier (coordinator init container, or the native gate
+      // once the pod has its IP) counts as starting, as paddlejob_controller.go:344-346
+      if (coord_running(pod) || (!pod.at_path("status.podIP").as_string().empty() &&
+                                 pod.at_path("metadata.annotations").get(api::kAnnotationStartGate).as_string() ==
+                                     api::kGateHold))
+        rs->starting++;
       else rs->pending++;
     } else if (ph == "Running") {
       if (pod_really_running(pod)) rs->running++;
