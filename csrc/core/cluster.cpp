@@ -32,7 +32,7 @@ Cluster::Cluster(ClusterOptions opt) : opt_(std::move(opt)) {
   api_.reset(new StoreApi(store_.get()));
   sched_.reset(new Scheduler(store_.get(), opt_.nodes));
   const bool compat = opt_.mode == plan::Mode::Compat;
-  int block = 1;
+  int block = opt_.ip_block_base;
   for (auto& n : opt_.nodes) {
     if (n.remote) continue;
     AgentOptions ao;

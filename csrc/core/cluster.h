@@ -39,7 +39,8 @@ struct ClusterOptions {
   std::string namespace_;
   std::string kv_endpoint = "127.0.0.1:2379";  // advertised to elastic pods (PADDLE_ELASTIC_SERVER)
   std::vector<std::string> zygote_cmd;          // per-node warm launcher (exec agents)
-  bool start_gate = true;                       // fast mode: native ps → worker → heter barrier
+  bool start_gate = true;
+  int ip_block_base = 1;                        // pods get 127.<base+node>.x.y                       // fast mode: native ps → worker → heter barrier
   // false: serve only the API server, gang scheduler, KV and kubelet-lite
   // agents — a single-node cluster for an external operator (e.g. pdo-manager
   // --backend=k8s pointed at this API), with no in-process PaddleJob controller

@@ -126,6 +126,7 @@ static pdo::ClusterOptions cluster_opts(const py::kwargs& kw) {
     else if (k == "kv_endpoint") o.kv_endpoint = v.cast<std::string>();
     else if (k == "zygote_cmd") o.zygote_cmd = v.cast<std::vector<std::string>>();
     else if (k == "start_gate") o.start_gate = v.cast<bool>();
+    else if (k == "ip_block_base") o.ip_block_base = v.cast<int>();
     else if (k == "nodes") {
       for (auto n : v.cast<py::list>()) {
         auto d = n.cast<py::dict>();

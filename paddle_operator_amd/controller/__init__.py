@@ -41,6 +41,12 @@ class LocalCluster:
             if root not in pp.split(os.pathsep):
                 os.environ["PYTHONPATH"] = root + (os.pathsep + pp if pp else "")
             opts["zygote_cmd"] = [sys.executable, "-m", "paddle_operator_amd.launch.zygote"]
+        if opts.get("agent") == "exec" and "ip_block_base" not in opts:
+            # every pod has its own 127.<block>.x.y; a per-process block keeps
+            # clusters of concurrently running processes (xdist) off each other's
+            # :2379 rendezvous ports
+            import os
+            opts["ip_block_base"] = 2 + os.getpid() % 200
         self._c = core().Cluster(**opts)
         self.opts = opts
         self.url: Optional[str] = None

@@ -138,10 +138,12 @@ def test_config1_wide_deep_ps_job_through_operator(tmp_path):
         tr_ready = recs("wide-ande-deep-worker-0", "PDO_READY")[0]
         assert ps_ready["role"] == "PSERVER" and tr_ready["role"] == "TRAINER"
         assert ps_ready["backend"] == "rpc+gloo"
-        # the trainer process was started only after the pserver pod ran (native gate)
-        assert tr_ready["t_start"] > ps_ready["t_start"], (ps_ready, tr_ready)
+        # the trainer's container was started only once the pserver's ran (native gate)
+        ps = cl.get("Pod", "wide-ande-deep-ps-0")
         trainer = cl.get("Pod", "wide-ande-deep-worker-0")
-        assert trainer["metadata"]["annotations"][GATE] == "released"
+        assert trainer["metadata"]["annotations"][GATE] == "released" and GATE not in ps["metadata"]["annotations"]
+        started = lambda p: p["status"]["containerStatuses"][0]["state"]["terminated"]["startedAt"]  # noqa: E731
+        assert started(trainer) >= started(ps)
         done = recs("wide-ande-deep-worker-0", "PDO_DONE")[0]
         assert done["last_loss"] < done["first_loss"] - 0.05, done
         st = cl.job("wide-ande-deep")["status"]
