@@ -2,6 +2,8 @@
 #include "sync.h"
 #include "store.h"
 
+#include "schema.h"
+
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -26,6 +28,8 @@ Store::Store(api::Clock clock) : clock_(std::move(clock)) {
   status_sub_[api::kKind] = true;  // +kubebuilder:subresource:status
   status_sub_["Pod"] = true;
   status_sub_["PodGroup"] = true;
+  // the PaddleJob CRD's structural schema: pruning + validation on write
+  admission_[api::kKind] = schema::admit_paddlejob;
 }
 
 void Store::set_status_subresource(const std::string& kind, bool on) {
@@ -52,7 +56,24 @@ void Store::emit_locked(EventType t, const std::string& kind, const Value& obj) 
   cv_.notify_all();
 }
 
+void Store::set_admission(const std::string& kind, Admission fn) {
+  std::lock_guard<std::mutex> g(mu_);
+  admission_[kind] = std::move(fn);
+}
+
+void Store::admit(const std::string& kind, Value& obj) const {
+  Admission fn;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = admission_.find(kind);
+    if (it == admission_.end()) return;
+    fn = it->second;
+  }
+  fn(obj);
+}
+
 Value Store::create(const std::string& kind, Value obj) {
+  admit(kind, obj);
   std::lock_guard<std::mutex> g(mu_);
   Key k = key_of(kind, obj);
   if (k.name.empty()) {
@@ -109,6 +130,7 @@ std::vector<Value> Store::list(const std::string& kind, const std::string& ns,
 }
 
 Value Store::update(const std::string& kind, Value obj) {
+  admit(kind, obj);
   std::lock_guard<std::mutex> g(mu_);
   Key k = key_of(kind, obj);
   auto it = objs_.find(k);

@@ -84,6 +84,10 @@ class Store {
 
   // kinds whose status is a subresource (update() ignores status changes)
   void set_status_subresource(const std::string& kind, bool on);
+  // admission of `kind` on create / update / update_status (mutate, or throw
+  // ApiError(Invalid)); not applied to mirror_* (server objects are admitted)
+  using Admission = std::function<void(Value&)>;
+  void set_admission(const std::string& kind, Admission fn);
 
   // informer-cache mode (k8s backend): store server objects verbatim
   void mirror_put(const std::string& kind, const Value& obj);
@@ -102,6 +106,8 @@ class Store {
   std::condition_variable cv_;
   std::map<Key, Value> objs_;
   std::map<std::string, bool> status_sub_;
+  std::map<std::string, Admission> admission_;
+  void admit(const std::string& kind, Value& obj) const;
   std::vector<WatchEvent> pending_;
   int64_t rev_ = 0;
   uint64_t uid_seq_ = 0;

@@ -6,11 +6,11 @@ Produces the apiextensions.k8s.io/v1 CRD (k8s ≥ 1.16) and the v1beta1 CRD
 version v1, kind PaddleJob, plural paddlejobs, short name pdj, printer
 columns Status/Mode/Age and the status subresource.
 
-Deviation (documented): the reference embeds the full corev1.PodTemplateSpec
-OpenAPI schema (~3k lines per role); here role templates are
-``x-kubernetes-preserve-unknown-fields`` objects — structurally valid, the
-apiserver still validates the Pods the operator creates from them.
-Enum fields stay plain strings like the reference (Appendix D-9).
+Role templates carry a structural corev1.PodTemplateSpec schema
+(api/podschema.py) like the reference's embedded one, so the apiserver
+validates them (containers required, container name required, field types)
+and prunes unknown fields at admission.  Enum fields stay plain strings like
+the reference (Appendix D-9).
 
 usage: python -m paddle_operator_amd.api.crd [--v1beta1] > crd.yaml
 """
@@ -22,6 +22,7 @@ import sys
 import yaml
 
 from . import types as T
+from .podschema import pod_template_schema
 
 
 def _int(desc, **kw):
@@ -46,11 +47,7 @@ def resource_spec_schema(role: str) -> dict:
             "requests": _int("Requests set the minimal replicas of server to be run"),
             "limits": _int("Limits set the maximal replicas of server to be run, elastic is auto enabled "
                            "if limits is set larger than 0"),
-            "template": {
-                "type": "object",
-                "description": "Template specifies the podspec of a server",
-                "x-kubernetes-preserve-unknown-fields": True,
-            },
+            "template": pod_template_schema(),
         },
     }
 

@@ -143,8 +143,16 @@ class PaddleJob(_Model):
 
 
 def validate(obj: dict) -> PaddleJob:
-    """Parse + schema-validate a PaddleJob dict (raises pydantic.ValidationError)."""
-    return PaddleJob.model_validate(obj)
+    """Parse + schema-validate a PaddleJob dict: the typed model (raises
+    pydantic.ValidationError) and then the CRD's structural schema, role
+    templates included, as the apiserver would at admission (ValueError)."""
+    job = PaddleJob.model_validate(obj)
+    from .crd import openapi_schema
+    from .podschema import check
+    errs = check(obj, openapi_schema())
+    if errs:
+        raise ValueError(f"{len(errs)} structural validation error(s): " + "; ".join(errs))
+    return job
 
 
 def container(name: str, command: List[str], image: str = "pdo/launcher:rocm", gpus: int = 0,
