@@ -125,13 +125,20 @@ class KVClient:
     def lease_revoke(self, lease: int):
         self._call("/v3/lease/revoke", {"ID": str(lease)})
 
-    def keepalive_thread(self, lease: int, ttl: int) -> threading.Event:
+    def keepalive_thread(self, lease: int, ttl: int,
+                         on_lost: Optional[Callable[[], None]] = None) -> threading.Event:
+        """Refresh ``lease`` every ttl/3 until the returned event is set.  If the
+        server reports the lease gone (it expired while the KV was unreachable,
+        or was revoked) the thread calls ``on_lost`` once and ends: the owner
+        must grant a new lease and re-announce what hung off the old one."""
         stop = threading.Event()
 
         def run():
             while not stop.wait(max(0.5, ttl / 3)):
                 try:
                     if self.lease_keepalive(lease) < 0:
+                        if on_lost is not None and not stop.is_set():
+                            on_lost()
                         return
                 except KVError:
                     pass

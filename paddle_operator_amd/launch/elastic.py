@@ -43,10 +43,11 @@ import os
 import signal
 import subprocess
 import sys
+import threading
 import time
 from typing import Dict, List, Optional, Tuple
 
-from ..kv.client import KVClient
+from ..kv.client import KVClient, KVError
 
 STORE_BASE_OFFSET = 2
 STORE_PORTS = 16
@@ -72,15 +73,41 @@ class ElasticAgent:
         self.lease = 0
         self.inc = 0
         self._ka = None
+        self._lease_lost = threading.Event()
+        self.reregistrations = 0
         self.proc: Optional[subprocess.Popen] = None
         self.history: List[dict] = []
 
     # ------------------------------------------------------------ membership
     def register(self):
         self.kv.put_if_absent(self.prefix + "np", str(self.np_default))
+        self._grant()
+
+    def _grant(self):
+        self._lease_lost.clear()
         self.lease = self.kv.lease_grant(self.ttl)
         self._announce()
-        self._ka = self.kv.keepalive_thread(self.lease, self.ttl)
+        self._ka = self.kv.keepalive_thread(self.lease, self.ttl, on_lost=self._lease_lost.set)
+
+    def ensure_registered(self) -> bool:
+        """Re-join after the membership lease was lost (the KV was unreachable
+        for more than a TTL): a new lease and a fresh ``nodes/`` record.  The
+        new lease id changes the generation plan, so peers re-form the world
+        with this member instead of it timing out in rendezvous.  True if a
+        re-registration happened."""
+        if not self._lease_lost.is_set():
+            return False
+        try:
+            if self._ka is not None:
+                self._ka.set()
+            self._grant()
+        except KVError as e:  # KV still away: the next poll retries
+            _log(f"re-register failed ({e}); retrying")
+            self._lease_lost.set()
+            return False
+        self.reregistrations += 1
+        _log(f"membership lease lost → re-registered with lease {self.lease}")
+        return True
 
     def _announce(self):
         self.kv.put(self.prefix + f"nodes/{self.id:06d}",
@@ -128,6 +155,7 @@ class ElasticAgent:
         Returns the world description, or None on timeout."""
         deadline = time.time() + self.timeout
         while time.time() < deadline:
+            self.ensure_registered()
             np_ = self.np()
             mem = self.members()
             if len(mem) < np_:
@@ -214,6 +242,7 @@ class ElasticAgent:
                     rc = self.proc.poll()
                     if rc is not None:
                         break
+                    self.ensure_registered()
                     if self.changed(world):
                         if self.gen_done(world):
                             rc = self.proc.wait()  # generation completed: let this worker finish too

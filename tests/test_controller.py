@@ -534,3 +534,43 @@ def test_zygote_gpu_warm_slot_handoff(tmp_path):
                        open(f"/proc/{rec['pid']}/stat").read().split()[2] == "Z", timeout=10)
     finally:
         cl.stop()
+
+
+def test_elastic_member_rejoins_after_lease_loss(tmp_path):
+    """A member whose KV lease is gone (expired while pdo-kv was unreachable,
+    here: revoked from outside) re-grants and re-announces instead of sitting
+    in rendezvous until the timeout (rc=3 → pod restart); the world re-forms
+    and the job completes without a restart."""
+    from paddle_operator_amd.kv.client import KVClient
+    port = _free_port()
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), elastic_kv=True,
+                      kv_endpoint=f"127.0.0.1:{port}")
+    cl.serve(f"127.0.0.1:{port}")
+    args = ["--workload", "resnet50", "--tiny", "--steps", "40", "--throttle-ms", "60",
+            "--ckpt-dir", str(tmp_path / "ckpt"), "--ckpt-every", "5"]
+    cont = _launcher_container(args)
+    cont["env"].append({"name": "PDO_ELASTIC_TTL", "value": "2"})
+    cl.create(T.paddlejob("el", worker={"replicas": 2, "template": {"spec": {"containers": [cont]}}}, elastic=1,
+                          clean_pod_policy="Never"))
+
+    def log(i):
+        d = cl.sandbox(f"el-worker-{i}")
+        p = os.path.join(d, "paddle.log") if d else ""
+        return open(p).read() if p and os.path.exists(p) else ""
+
+    try:
+        assert cl.wait(lambda: _ready_rec(cl, "el", 1) is not None, timeout=120)
+        kv = KVClient(f"127.0.0.1:{port}")
+        node = json.loads(kv.get("/paddle/default-el/nodes/000001"))
+        kv.lease_revoke(int(node["lease"]))  # the member's record vanishes with its lease
+        assert cl.wait(lambda: "re-registered" in log(1), timeout=30), log(1)[-3000:]
+        node2 = json.loads(kv.get("/paddle/default-el/nodes/000001"))
+        assert node2["lease"] != node["lease"]
+        ok = cl.wait_phase("el", T.Phase.Completed, timeout=180)
+        assert ok, (cl.job("el")["status"], log(0)[-2000:], log(1)[-2000:])
+        pod1 = cl.get("Pod", "el-worker-1")
+        assert pod1["status"]["containerStatuses"][0]["restartCount"] == 0
+        gens = {json.loads(l[10:]).get("gen") for l in log(1).splitlines() if l.startswith("PDO_READY ")}
+        assert len(gens) >= 2  # the world re-formed around the new lease
+    finally:
+        cl.stop()
