@@ -674,6 +674,11 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_impl", [](int impl) {
+    const int prev = pdo::gemm_nt_get_impl();
+    if (impl >= 0) pdo::gemm_nt_set_impl(impl);
+    return prev;
+  }, py::arg("impl") = -1, "select gemm_nt's mainloop (0 = 8-wave ring, 1 = 4-wave); returns the previous");
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
   m.def("gemm_nt_gelu", &gemm_nt_gelu);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),

@@ -232,12 +232,17 @@ int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
 
 int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
 
+static int g_impl = 0;
+void gemm_nt_set_impl(int impl) { g_impl = impl; }
+int gemm_nt_get_impl() { return g_impl; }
+
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
   if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
   if (epi != 0 && !bias) return -3;
   if ((epi == 2 || epi == 3) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
+  if (g_impl == 1 && K % 128 == 0 && K >= 256) return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st);
   const long long grid = (long long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;

@@ -1,0 +1,322 @@
+// SPDX-License-Identifier: Apache-2.0
+// C[M][N] = A[M][K] · B[N][K]ᵀ on gfx950 — the 4-wave, one-wave-per-SIMD
+// mainloop (same contract and epilogues as gemm_nt.hip, selected by
+// gemm_nt_set_impl).
+//
+// Why a second mainloop: PMC passes over gemm_nt (8 waves, 128 × 64 per wave,
+// two waves per SIMD ping-ponging between an MFMA phase and a read phase) at
+// [65536 × 1024] · [1024 × 4096]ᵀ show the matrix pipe busy 62 % of the
+// kernel's cycles, 25 % of wave cycles parked at barriers / waits, and 0.38
+// LDS instructions per MFMA; hipBLASLt's kernel on the same shape (4 waves,
+// 128 × 128 per wave) keeps it 80 % busy at 0.25 (profiles/r2_gemm_pmc.md).
+// Here each wave owns a 128 × 128 output block (64 16×16 accumulators = 256
+// fp32 registers, in the accumulator file) and one instruction stream
+// interleaves everything with its MFMAs:
+//
+//   tile t (BK = 64, LDS buffer t&1), 128 MFMAs per wave:
+//   block 0: 16 groups of {4 MFMAs on the k 0-31 fragments F0; 1 ds_read of a
+//            k 32-63 fragment F1; 2 LDS-DMA (global_load_lds_dwordx4) pieces
+//            of tile t+1 into the other buffer (groups 0-7)}
+//   block 1: 16 groups of {4 MFMAs on F1}; after group 11: retire this wave's
+//            DMA of tile t+1 (vmcnt(0)) and its F1 reads (lgkmcnt(0)), one
+//            s_barrier; groups 12-15 each read 4 fragments F0 of tile t+1.
+//
+// One barrier per k-tile.  RAW: tile t+1's bytes are read only after every
+// wave retired its own DMA and passed that barrier.  WAR: a buffer is
+// overwritten (block 0 of tile t+1 writes buffer t&1) only after the barrier
+// that follows every wave's last read of it (its F1 reads in block 0 of tile
+// t, retired before the barrier in block 1 of tile t).
+//
+// LDS: [buffer][A|B][256 rows][64 k] bf16 = 128 KiB; rows are 128 B with the
+// 16-B chunk c of row r stored at chunk c ^ ((r >> 1) & 7), so the 16 rows a
+// ds_read_b128 lane group touches land on 16 distinct bank slots.  The DMA
+// writes LDS linearly (1 KiB = 8 rows per wave-instruction) and applies the
+// swizzle on the per-lane global source address.
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
+constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 = 32 KiB
+
+template <int EPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           int lda, int ldb, int M, int N, int nk,
+                                                           bf16* __restrict__ C, int ldc,
+                                                           const bf16* __restrict__ bias, bf16* __restrict__ Y,
+                                                           int ldy, float* __restrict__ dbias_part) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * 256 * BK];  // [buf][A|B][256][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int tiles_n = N / BN;
+  const int nwg = (M / BM) * tiles_n;
+  int id = blockIdx.x;
+  {  // bijective XCD remap: each XCD walks a contiguous range of tiles (shared A panels in its L2)
+    const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tn = id % tiles_n, tm = id / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- LDS-DMA sources.  Wave w fills 8-row blocks b = w + 4i (i = 0..7) of
+  // both operands; lane l → row 8b + (l >> 3), LDS chunk l & 7, global chunk
+  // (l & 7) ^ swz(row) with swz(row) = (row >> 1) & 7 = 4(w & 1) + (l >> 4).
+  // The per-lane part is a 32-bit byte offset (one VGPR per operand); the
+  // wave-uniform part (tile origin, block, k-tile) is an SGPR base, so a DMA
+  // piece costs scalar adds instead of 64-bit vector address arithmetic.
+  const int rb = lane >> 3;
+  const int csrc = (lane & 7) ^ (4 * (w & 1) + (lane >> 4));
+  const unsigned voffA = (unsigned)((rb * lda + csrc * 8) * 2), voffB = (unsigned)((rb * ldb + csrc * 8) * 2);
+  const bf16* baseA = A + ((size_t)m0 + 8 * w) * lda;
+  const bf16* baseB = B + ((size_t)n0 + 8 * w) * ldb;
+  const unsigned stepAb = (unsigned)(64 * lda), stepBb = (unsigned)(64 * ldb);  // 32 rows, bytes
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem + (unsigned)(w * 1024);
+  auto glds = [](unsigned voff, const bf16* sbase, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds_byte)
+                 : "memory");
+  };
+  // pieces of tile kt into buffer BUF: p < 8 → A block w + 4p, else B block w + 4(p - 8).
+  // The per-tile bases and strides pass through an empty asm so hipcc forms each
+  // piece's 64-bit base with two scalar adds next to its DMA instead of keeping
+  // 16 precomputed bases live (they pushed the kernel past the 102-SGPR limit
+  // and into AGPR shuttling)
+  struct Src {
+    const char* a;
+    const char* b;
+    unsigned sa, sb;
+  };
+  auto srcs = [&](int kt) {
+    Src r{reinterpret_cast<const char*>(baseA + (size_t)kt * BK), reinterpret_cast<const char*>(baseB + (size_t)kt * BK),
+          stepAb, stepBb};
+    asm volatile("" : "+s"(r.a), "+s"(r.b), "+s"(r.sa), "+s"(r.sb));
+    return r;
+  };
+  auto dma = [&](const Src& sr, auto buf_tag, int p) {
+    constexpr int BUF = decltype(buf_tag)::value;
+    const unsigned base = lds0 + (unsigned)(BUF * 2 * OPB);
+    if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
+    else glds(voffB, reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+  };
+
+  // ---- fragment reads: 16x16x32 operand = rows (l & 15), k chunk 4kk + (l >> 4)
+  const unsigned char* lds = reinterpret_cast<const unsigned char*>(smem);
+  const int sw = (lane >> 1) & 7;
+  const int ra = (wm * 128 + (lane & 15)) * 128, rbb = (wn * 128 + (lane & 15)) * 128;
+  const int oA0 = ra + ((((lane >> 4)) ^ sw) << 4), oA1 = ra + (((4 + (lane >> 4)) ^ sw) << 4);
+  const int oB0 = OPB + rbb + ((((lane >> 4)) ^ sw) << 4), oB1 = OPB + rbb + (((4 + (lane >> 4)) ^ sw) << 4);
+  // read order within a k-half: A0, B0..B7, A1..A7 (the order block MFMAs consume them)
+  auto rd = [&](auto buf_tag, int kk, int q) -> bf16x8 {
+    constexpr int BUF = decltype(buf_tag)::value;
+    const int o = (q == 0) ? (kk ? oA1 : oA0) : (q <= 8) ? (kk ? oB1 : oB0) + (q - 1) * 2048
+                                                          : (kk ? oA1 : oA0) + (q - 8) * 2048;
+    return *reinterpret_cast<const bf16x8*>(lds + BUF * 2 * OPB + o);
+  };
+  // MFMA with the accumulator pinned to the accumulator file ("+a"): with the
+  // builtin, hipcc kept part of the 256 accumulators in arch VGPRs and shuttled
+  // them through v_accvgpr_read/write around every MFMA (≈3 VALU per MFMA).
+  // hipcc does not see inside the asm, so the asm must not depend on its hazard
+  // padding: the operands come from ds_read (hipcc's lgkmcnt waits cover asm
+  // inputs), an accumulator is rewritten 64 MFMAs after its previous write, the
+  // first write of each one takes C = 0 (mma0: no v_accvgpr_write init that a
+  // following MFMA would read too early), and the epilogue pads before reading.
+  auto mma = [](f32x4& c, const bf16x8& b, const bf16x8& a) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+  };
+  auto mma0 = [](f32x4& c, const bf16x8& b, const bf16x8& a) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+
+  f32x4 acc[8][8];  // first written by mma0 in tile 0's block 0
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  // ---- prologue: tile 0 → buffer 0, F0 of tile 0
+  {
+    const Src s0 = srcs(0);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const bf16x8 v = rd(B0{}, 0, q);
+    if (q == 0) fa0[0] = v;
+    else if (q <= 8) fb0[q - 1] = v;
+    else fa0[q - 8] = v;
+  }
+
+  // one k-tile in LDS buffer BUF; MORE = a next tile exists (its DMA, the
+  // barrier and its F0 reads)
+  auto tile = [&](int t, auto buf_tag, auto more_tag, auto first_tag) {
+    constexpr int BUF = decltype(buf_tag)::value;
+    constexpr bool MORE = decltype(more_tag)::value;
+    constexpr bool FIRST = decltype(first_tag)::value;
+    using NB = std::integral_constant<int, BUF ^ 1>;
+    Src sn{};
+    if constexpr (MORE) sn = srcs(t + 1);
+    // ---- block 0: MFMAs on F0, reads of F1 (this tile), DMA of tile t+1
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int i = g >> 1, j0 = 4 * (g & 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if constexpr (FIRST) mma0(acc[i][j0 + j], fb0[j0 + j], fa0[i]);
+        else mma(acc[i][j0 + j], fb0[j0 + j], fa0[i]);
+      const bf16x8 v = rd(buf_tag, 1, g);
+      if (g == 0) fa1[0] = v;
+      else if (g <= 8) fb1[g - 1] = v;
+      else fa1[g - 8] = v;
+      if constexpr (MORE) {
+        if (g < 8) {
+          dma(sn, NB{}, 2 * g);
+          dma(sn, NB{}, 2 * g + 1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- block 1: MFMAs on F1; barrier; reads of F0 (next tile)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int i = g >> 1, j0 = 4 * (g & 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        mma(acc[i][j0 + j], fb1[j0 + j], fa1[i]);
+      if constexpr (MORE) {
+        if (g == 11) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (g >= 12) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = 4 * (g - 12) + u;
+            const bf16x8 v = rd(NB{}, 0, q);
+            if (q == 0) fa0[0] = v;
+            else if (q <= 8) fb0[q - 1] = v;
+            else fa0[q - 8] = v;
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  // nk is even and ≥ 4 (host contract): pairs of tiles keep the buffer index static
+  tile(0, B0{}, T_{}, T_{});
+  tile(1, B1{}, T_{}, F_{});
+  for (int t = 2; t < nk - 2; t += 2) {
+    tile(t, B0{}, T_{}, F_{});
+    tile(t + 1, B1{}, T_{}, F_{});
+  }
+  tile(nk - 2, B0{}, T_{}, F_{});
+  tile(nk - 1, B1{}, F_{}, F_{});
+
+  // ---- epilogue ----
+  // The accumulators leave the accumulator file through explicit
+  // v_accvgpr_read ("a" operands): with plain VALU uses here, hipcc's register
+  // classes put part of the 256 accumulators in arch VGPRs for the whole
+  // kernel and shuttled them through v_accvgpr_read/write around every MFMA
+  // (≈3 VALU per MFMA).  hipcc does not pad the asm against the last MFMAs:
+  // 16 wait states first (≥ the 8-pass XDL D → read requirement).
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  auto rd_acc = [](const f32x4& a) {
+    f32x4 v;
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\tv_accvgpr_read_b32 %3, %7"
+                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3])
+                 : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
+    return v;
+  };
+  // acc[i][j][e] = C[m][n], m = wm·128 + 16i + (l&15), n = wn·128 + 16j + 4(l>>4) + e.
+  // Staged through LDS as bf16 [256][256] (chunk c of row m at c ^ (m & 31))
+  // and written back as whole 512-B rows, 16 B per lane.
+  __syncthreads();
+  unsigned char* st = reinterpret_cast<unsigned char*>(smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == 1) {
+      const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * 128 + 16 * j + 4 * (lane >> 4));
+      bv = f32x4{(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
+    }
+    const int c = wn * 16 + 2 * j + (lane >> 5);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = wm * 128 + 16 * i + (lane & 15);
+      const f32x4 a = rd_acc(acc[i][j]) + bv;
+      const bf16x4 o = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+      *reinterpret_cast<bf16x4*>(st + m * 512 + ((c ^ (m & 31)) << 4) + 8 * ((lane >> 4) & 1)) = o;
+    }
+  }
+  __syncthreads();
+  // row phase: thread t owns 16-B column chunk t & 31 of rows 8·it + (t >> 5)
+  const int c = tid & 31, r0 = tid >> 5;
+  const int n = n0 + 8 * c;
+  f32x8 bv8;
+  if constexpr (EPI >= 2) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
+  f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const int r = 8 * it + r0;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * 512 + ((c ^ (r & 31)) << 4));
+    const size_t m = (size_t)(m0 + r);
+    if constexpr (EPI <= 1) {
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+    } else if constexpr (EPI == 2) {
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+      const f32x8 x = to_f32(v) + bv8;
+      f32x8 y;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
+      *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
+    } else {
+      const f32x8 x = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n)) + bv8;
+      const f32x8 dy = to_f32(v);
+      f32x8 d;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = dy[e] * gelu_sig_grad(x[e]);
+      colp += d;
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(d);
+    }
+  }
+  if constexpr (EPI == 3) {
+    // one fp32 partial row per (M-tile, row class r0): 8 rows per M-tile, as gemm_nt
+    float* prow = dbias_part + (size_t)(8 * tm + r0) * N + n;
+    *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
+    *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
+  }
+}
+
+}  // namespace
+
+int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
+             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
+  const long long grid = (long long)(M / BM) * (N / BN);
+  if (grid > 0x7fffffffLL) return -2;
+  const int nk = K / BK;
+  if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
+  switch (epi) {
+    case 0: gemm_nt4_kernel<0><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 1: gemm_nt4_kernel<1><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 2: gemm_nt4_kernel<2><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 3: gemm_nt4_kernel<3><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    default: return -4;
+  }
+  return 0;
+}
+
+}  // namespace pdo

@@ -72,10 +72,14 @@ def build_hip(jobs=8, verbose=False):
     headers = glob.glob(os.path.join(src_dir, "*.h"))
     kernels = sorted(glob.glob(os.path.join(src_dir, "*.hip")))
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
-              "-Wno-unused-result", "-munsafe-fp-atomics",
-              # MFMA accumulators in arch VGPRs: no v_accvgpr copies around the
-              # VALU work on accumulators (softmax / rescale / epilogues)
-              "-mllvm", "-amdgpu-mfma-vgpr-form"]
+              "-Wno-unused-result", "-munsafe-fp-atomics"]
+    # MFMA accumulators in arch VGPRs: no v_accvgpr copies around the VALU work
+    # on accumulators (softmax / rescale / epilogues) — except where the
+    # accumulators alone exceed the 256 arch VGPRs (gemm_nt4: 256 fp32 per lane
+    # live in the accumulator file; the vgpr form made hipcc shuttle them
+    # through arch VGPRs, 3 VALU per MFMA)
+    vgpr_form = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+    agpr_files = {"gemm_nt4.hip"}
     # per-file extras: attention's softmax max-reductions become v_max3 only
     # without NaN canonicalisation (scores are never NaN; ±inf masks keep working)
     extra = {"attention.hip": ["-fno-honor-nans"]}
@@ -83,12 +87,13 @@ def build_hip(jobs=8, verbose=False):
     for s in kernels:
         o = os.path.join(obj_dir, os.path.basename(s) + ".o")
         if _newer(o, [s] + headers + [os.path.abspath(__file__)]):
-            jobs_list.append([HIPCC] + common + extra.get(os.path.basename(s), []) + ["-c", s, "-o", o])
+            form = [] if os.path.basename(s) in agpr_files else vgpr_form
+            jobs_list.append([HIPCC] + common + form + extra.get(os.path.basename(s), []) + ["-c", s, "-o", o])
     tcf, tld = torch_flags()
     bind = os.path.join(src_dir, "bind.cpp")
     bind_o = os.path.join(obj_dir, "bind.o")
     if _newer(bind_o, [bind] + headers):
-        jobs_list.append([HIPCC] + common + tcf + ["-x", "hip", "-c", bind, "-o", bind_o])
+        jobs_list.append([HIPCC] + common + vgpr_form + tcf + ["-x", "hip", "-c", bind, "-o", bind_o])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for out in ex.map(_run, jobs_list):
             if verbose and out.strip():

@@ -8,11 +8,16 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from paddle_operator_amd import _native  # noqa: E402
+from paddle_operator_amd.utils.tuning import enable_tuned_gemms  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 it = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+impl = int(sys.argv[4]) if len(sys.argv) > 4 else -1
+enable_tuned_gemms()
 m = _native.require_hip()
+if impl >= 0:
+    m.gemm_nt_impl(impl)
 x = torch.randn(65536, K, device="cuda", dtype=torch.bfloat16)
 w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
 for _ in range(it):
