@@ -232,7 +232,7 @@ int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
 
 int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
 
-static int g_impl = 0;
+static int g_impl = 1;  // 4-wave mainloop, variant 0 (tools/nt4_probe.py)
 void gemm_nt_set_impl(int impl) { g_impl = impl; }
 int gemm_nt_get_impl() { return g_impl; }
 
@@ -242,7 +242,8 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
   if (epi != 0 && !bias) return -3;
   if ((epi == 2 || epi == 3) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
-  if (g_impl == 1 && K % 128 == 0 && K >= 256) return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st);
+  if (g_impl >= 1 && K % 128 == 0 && K >= 256)
+    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, g_impl - 1);
   const long long grid = (long long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;

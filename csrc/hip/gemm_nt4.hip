@@ -44,7 +44,7 @@ namespace {
 constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
 constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 = 32 KiB
 
-template <int EPI>
+template <int EPI, int GPG, int BAR>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
@@ -77,10 +77,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   const bf16* baseB = B + ((size_t)n0 + 8 * w) * ldb;
   const unsigned stepAb = (unsigned)(64 * lda), stepBb = (unsigned)(64 * ldb);  // 32 rows, bytes
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem + (unsigned)(w * 1024);
+  // M0 is not saved around the DMA: nothing else in this kernel uses it (check
+  // the .s for other M0 readers after editing); s_nop 0 = the SALU M0 write →
+  // LDS-DMA wait state
   auto glds = [](unsigned voff, const bf16* sbase, unsigned lds_byte) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
                  : "v"(voff), "s"(sbase), "s"(lds_byte)
                  : "memory");
   };
@@ -160,13 +162,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 
   // one k-tile in LDS buffer BUF; MORE = a next tile exists (its DMA, the
   // barrier and its F0 reads)
-  auto tile = [&](int t, auto buf_tag, auto more_tag, auto first_tag) {
+  // E = DMA pieces of tile t+2 issued early, in block 1 of tile t right after
+  // its barrier (buffer t&1 is free then: every wave retired its last reads
+  // of it before that barrier); block 0 of tile t+1 issues the other 16 - E
+  constexpr int E = 15 - BAR;
+  // ps: MORE = tile t+1 exists; EIN = its first E pieces were issued early;
+  // EOUT = issue the first E pieces of tile t+2 after this tile's barrier
+  auto tile = [&](int t, auto buf_tag, auto more_tag, auto first_tag, auto ein_tag, auto eout_tag) {
     constexpr int BUF = decltype(buf_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
     constexpr bool FIRST = decltype(first_tag)::value;
+    constexpr bool EIN = decltype(ein_tag)::value;
+    constexpr bool EOUT = decltype(eout_tag)::value;
+    constexpr int P0 = EIN ? E : 0;  // first piece of tile t+1 block 0 issues
     using NB = std::integral_constant<int, BUF ^ 1>;
-    Src sn{};
+    using SB = std::integral_constant<int, BUF>;
+    Src sn{}, sn2{};
     if constexpr (MORE) sn = srcs(t + 1);
+    if constexpr (EOUT) sn2 = srcs(t + 2);
     // ---- block 0: MFMAs on F0, reads of F1 (this tile), DMA of tile t+1
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
@@ -180,10 +193,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       else if (g <= 8) fb1[g - 1] = v;
       else fa1[g - 8] = v;
       if constexpr (MORE) {
-        if (g < 8) {
-          dma(sn, NB{}, 2 * g);
-          dma(sn, NB{}, 2 * g + 1);
-        }
+#pragma unroll
+        for (int u = 0; u < GPG; ++u)
+          if (P0 + GPG * g + u < 16) dma(sn, NB{}, P0 + GPG * g + u);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -195,15 +207,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       for (int j = 0; j < 4; ++j)
         mma(acc[i][j0 + j], fb1[j0 + j], fa1[i]);
       if constexpr (MORE) {
-        if (g == 11) {
+        if (g == BAR) {
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if (g >= 12) {
+        if (g > BAR) {
+          if constexpr (EOUT) dma(sn2, SB{}, g - BAR - 1);
+          constexpr int RPG = 16 / (15 - BAR);  // F0 reads per remaining group
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int q = 4 * (g - 12) + u;
+          for (int u = 0; u < RPG; ++u) {
+            const int q = RPG * (g - BAR - 1) + u;
             const bf16x8 v = rd(NB{}, 0, q);
             if (q == 0) fa0[0] = v;
             else if (q <= 8) fb0[q - 1] = v;
@@ -217,14 +231,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   using T_ = std::true_type;
   using F_ = std::false_type;
   // nk is even and ≥ 4 (host contract): pairs of tiles keep the buffer index static
-  tile(0, B0{}, T_{}, T_{});
-  tile(1, B1{}, T_{}, F_{});
+  tile(0, B0{}, T_{}, T_{}, F_{}, T_{});
+  tile(1, B1{}, T_{}, F_{}, T_{}, T_{});
   for (int t = 2; t < nk - 2; t += 2) {
-    tile(t, B0{}, T_{}, F_{});
-    tile(t + 1, B1{}, T_{}, F_{});
+    tile(t, B0{}, T_{}, F_{}, T_{}, T_{});
+    tile(t + 1, B1{}, T_{}, F_{}, T_{}, T_{});
   }
-  tile(nk - 2, B0{}, T_{}, F_{});
-  tile(nk - 1, B1{}, F_{}, F_{});
+  tile(nk - 2, B0{}, T_{}, F_{}, T_{}, F_{});
+  tile(nk - 1, B1{}, F_{}, F_{}, F_{}, F_{});
 
   // ---- epilogue ----
   // The accumulators leave the accumulator file through explicit
@@ -304,17 +318,34 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 }  // namespace
 
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
-             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
+             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant) {
   const long long grid = (long long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;
   if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
-  switch (epi) {
-    case 0: gemm_nt4_kernel<0><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-    case 1: gemm_nt4_kernel<1><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-    case 2: gemm_nt4_kernel<2><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-    case 3: gemm_nt4_kernel<3><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-    default: return -4;
+  auto launch = [&](auto gpg, auto bar) {
+    constexpr int G = decltype(gpg)::value, R = decltype(bar)::value;
+    switch (epi) {
+      case 0: gemm_nt4_kernel<0, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 1: gemm_nt4_kernel<1, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 2: gemm_nt4_kernel<2, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 3: gemm_nt4_kernel<3, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      default: return -4;
+    }
+    return 0;
+  };
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I7 = std::integral_constant<int, 7>;
+  using I11 = std::integral_constant<int, 11>;
+  using I13 = std::integral_constant<int, 13>;
+  // schedule variants under A/B (tools/nt4_probe.py, profiles/r2_gemm_nt4.md):
+  // 0 = one DMA piece per group + barrier after block-1 group 11 (the default)
+  switch (variant) {
+    case 1: return launch(I1{}, I7{});
+    case 2: return launch(I1{}, I13{});
+    case 3: return launch(I2{}, I11{});
+    default: return launch(I1{}, I11{});
   }
   return 0;
 }

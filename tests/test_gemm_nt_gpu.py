@@ -71,3 +71,33 @@ def test_rejects_unsupported_shapes(hip):
     x, w, _ = _mk(320, 256, 64)
     with pytest.raises(RuntimeError):
         hip.gemm_nt(x, w)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (256, 768, 384), (1024, 512, 2048), (768, 256, 128)])
+def test_nt4_mainloop_matches_ring(hip, M, N, K):
+    """The 4-wave mainloop (gemm_nt4.hip, every schedule variant) runs the k-tiles
+    in the same order as the 8-wave ring: outputs equal bit for bit; K = 128
+    falls back to the ring (the 4-wave loop needs ≥ 4 even k-tiles)."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bias = torch.empty(N, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16).uniform_(-2, 2, generator=g)
+    prev = hip.gemm_nt_impl(0)
+    try:
+        ref = hip.gemm_nt(a, b, bias)
+        ref_p, ref_y = hip.gemm_nt_gelu(a, b, bias)
+        ref_dx, ref_db = hip.gemm_nt_dgelu(a, b, pre, bias)
+        for impl in (1, 2, 3, 4):
+            hip.gemm_nt_impl(impl)
+            assert torch.equal(hip.gemm_nt(a, b, bias), ref), impl
+            p, y = hip.gemm_nt_gelu(a, b, bias)
+            assert torch.equal(p, ref_p) and torch.equal(y, ref_y), impl
+            dx, db = hip.gemm_nt_dgelu(a, b, pre, bias)
+            assert torch.equal(dx, ref_dx), impl
+            # bias-gradient partials are summed in another order: fp32 rounding only
+            torch.testing.assert_close(db.float(), ref_db.float(), rtol=2e-2, atol=2e-2)
+        exact = a.float() @ b.float().t() + bias.float()
+        torch.testing.assert_close(ref.float(), exact, rtol=2e-2, atol=6e-2)
+    finally:
+        hip.gemm_nt_impl(prev)

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--variants", type=int, default=1, help="gemm_nt4 schedule variants to A/B (impl 1..N)")
     a = ap.parse_args()
     enable_tuned_gemms()
     m = _native.require_hip()
@@ -65,14 +66,15 @@ def main():
         else:
             ours = lambda: m.gemm_nt_dgelu(x, w, pre, b)  # noqa: E731
             lib = lambda: m.bias_gelu_bwd(F.linear(x, w), pre, b)  # noqa: E731
+        impls = [0] + [1 + v for v in range(a.variants)]
         outs = {}
-        for impl in (0, 1):
+        for impl in impls:
             m.gemm_nt_impl(impl)
             o = ours()
             outs[impl] = [t.clone() for t in (o if isinstance(o, (list, tuple)) else [o])]
         torch.cuda.synchronize()
-        ident = all(torch.equal(p, q) for p, q in zip(outs[0], outs[1]))
-        maxdiff = max((p.float() - q.float()).abs().max().item() for p, q in zip(outs[0], outs[1]))
+        ident = all(torch.equal(p, q) for i in impls[1:] for p, q in zip(outs[0], outs[i]))
+        maxdiff = max((p.float() - q.float()).abs().max().item() for i in impls[1:] for p, q in zip(outs[0], outs[i]))
         R = 512
         ref = x[-R:].float() @ w.float().t()
         c0 = outs[0][0][-R:].float()
@@ -80,12 +82,12 @@ def main():
             ref = ref + b.float()
         ref_err = (c0 - ref).abs().max().item() if epi in ("plain", "bias", "gelu") else None
         del outs
-        times = {"nt0": [], "nt1": [], "lib": []}
+        times = {f"nt{i}": [] for i in impls}
+        times["lib"] = []
         for _ in range(a.rounds):
-            m.gemm_nt_impl(0)
-            times["nt0"].append(bench(ours, a.iters))
-            m.gemm_nt_impl(1)
-            times["nt1"].append(bench(ours, a.iters))
+            for i in impls:
+                m.gemm_nt_impl(i)
+                times[f"nt{i}"].append(bench(ours, a.iters))
             times["lib"].append(bench(lib, a.iters))
         fl = 2.0 * M * N * K
         rec = {"shape": name, "N": N, "K": K, "epi": epi, "bitwise_equal": ident, "max_diff": maxdiff,
