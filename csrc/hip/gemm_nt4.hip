@@ -44,7 +44,7 @@ namespace {
 constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
 constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 = 32 KiB
 
-template <int EPI, int GPG, int BAR>
+template <int EPI, int GPG, int BAR, int BUFLD>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
@@ -97,16 +97,38 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     unsigned sa, sb;
   };
   auto srcs = [&](int kt) {
-    Src r{reinterpret_cast<const char*>(baseA + (size_t)kt * BK), reinterpret_cast<const char*>(baseB + (size_t)kt * BK),
-          stepAb, stepBb};
+    Src r;
+    if constexpr (BUFLD) {
+      r = Src{reinterpret_cast<const char*>((uintptr_t)(kt * BK * 2)), nullptr, stepAb, stepBb};
+    } else {
+      r = Src{reinterpret_cast<const char*>(baseA + (size_t)kt * BK), reinterpret_cast<const char*>(baseB + (size_t)kt * BK),
+              stepAb, stepBb};
+    }
     asm volatile("" : "+s"(r.a), "+s"(r.b), "+s"(r.sa), "+s"(r.sb));
     return r;
+  };
+  // BUFLD: the same pieces as buffer_load_dwordx4 … offen lds (buffer
+  // descriptor per operand, the per-piece offset in soffset) — A/B variant
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(baseA), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(baseB), 0, 0x7fffffff, 0x00020000);
+  auto bld = [](unsigned voff, __amdgpu_buffer_rsrc_t rs, unsigned soff, unsigned lds_byte) {
+    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+                 :
+                 : "v"(voff), "s"(rs), "s"(soff), "s"(lds_byte)
+                 : "memory");
   };
   auto dma = [&](const Src& sr, auto buf_tag, int p) {
     constexpr int BUF = decltype(buf_tag)::value;
     const unsigned base = lds0 + (unsigned)(BUF * 2 * OPB);
-    if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
-    else glds(voffB, reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+    if constexpr (BUFLD) {
+      // sr.a / sr.b carry the k-tile byte offset in this mode
+      const unsigned ko = (unsigned)(uintptr_t)sr.a;
+      if (p < 8) bld(voffA, rsA, ko + p * sr.sa, base + (unsigned)(4096 * p));
+      else bld(voffB, rsB, ko + (p - 8) * sr.sb, base + OPB + (unsigned)(4096 * (p - 8)));
+    } else {
+      if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
+      else glds(voffB, reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+    }
   };
 
   // ---- fragment reads: 16x16x32 operand = rows (l & 15), k chunk 4kk + (l >> 4)
@@ -323,17 +345,18 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;
   if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
-  auto launch = [&](auto gpg, auto bar) {
-    constexpr int G = decltype(gpg)::value, R = decltype(bar)::value;
+  auto launch = [&](auto gpg, auto bar, auto bufld) {
+    constexpr int G = decltype(gpg)::value, R = decltype(bar)::value, L = decltype(bufld)::value;
     switch (epi) {
-      case 0: gemm_nt4_kernel<0, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-      case 1: gemm_nt4_kernel<1, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-      case 2: gemm_nt4_kernel<2, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-      case 3: gemm_nt4_kernel<3, G, R><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 0: gemm_nt4_kernel<0, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 1: gemm_nt4_kernel<1, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 2: gemm_nt4_kernel<2, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 3: gemm_nt4_kernel<3, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
       default: return -4;
     }
     return 0;
   };
+  using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I7 = std::integral_constant<int, 7>;
@@ -342,10 +365,10 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   // schedule variants under A/B (tools/nt4_probe.py, profiles/r2_gemm_nt4.md):
   // 0 = one DMA piece per group + barrier after block-1 group 11 (the default)
   switch (variant) {
-    case 1: return launch(I1{}, I7{});
-    case 2: return launch(I1{}, I13{});
-    case 3: return launch(I2{}, I11{});
-    default: return launch(I1{}, I11{});
+    case 1: return launch(I1{}, I7{}, I0{});
+    case 2: return launch(I1{}, I13{}, I0{});
+    case 3: return launch(I1{}, I11{}, I1{});
+    default: return launch(I1{}, I11{}, I0{});
   }
   return 0;
 }
