@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstring>
 #include <dirent.h>
+
+#include <algorithm>
 #include <fstream>
 #include <map>
 #include <string>
@@ -89,6 +91,55 @@ static int detect_gpus() {
     n = std::min(n, cnt);
   }
   return n;
+}
+
+// NUMA-local CPU list of every GPU, in KFD node order (= HIP device order),
+// from sysfs: KFD node properties (domain, location_id = PCI bus/dev/fn) →
+// /sys/bus/pci/devices/<bdf>/local_cpulist.  The kubelet-lite agent pins each
+// rank process to the list of its GPU (agent.cpp start_proc).  Mapped through
+// HIP_VISIBLE_DEVICES when the manager itself is restricted.
+static std::vector<std::string> detect_gpu_cpulists() {
+  std::vector<std::pair<long, std::string>> nodes;  // (kfd node id, cpulist)
+  DIR* d = opendir("/sys/class/kfd/kfd/topology/nodes");
+  if (!d) return {};
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] == '.') continue;
+    std::ifstream f(std::string("/sys/class/kfd/kfd/topology/nodes/") + e->d_name + "/properties");
+    std::string k;
+    long long v, simd = 0, loc = 0, dom = 0;
+    while (f >> k >> v) {
+      if (k == "simd_count") simd = v;
+      else if (k == "location_id") loc = v;
+      else if (k == "domain") dom = v;
+    }
+    if (simd <= 0) continue;
+    char bdf[32];
+    snprintf(bdf, sizeof bdf, "%04llx:%02llx:%02llx.%llx", dom, (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 0x7);
+    std::ifstream c(std::string("/sys/bus/pci/devices/") + bdf + "/local_cpulist");
+    std::string list;
+    std::getline(c, list);
+    nodes.emplace_back(strtol(e->d_name, nullptr, 10), list);
+  }
+  closedir(d);
+  std::sort(nodes.begin(), nodes.end());
+  std::vector<std::string> all;
+  for (auto& n : nodes) all.push_back(n.second);
+  const char* pv = getenv("HIP_VISIBLE_DEVICES");
+  if (!pv || !*pv) pv = getenv("CUDA_VISIBLE_DEVICES");
+  if (!pv || !*pv) return all;
+  std::vector<std::string> out;
+  std::string cur;
+  for (const char* q = pv;; ++q) {
+    if (*q == ',' || *q == 0) {
+      const long i = cur.empty() ? -1 : strtol(cur.c_str(), nullptr, 10);
+      out.push_back(i >= 0 && i < (long)all.size() ? all[i] : "");
+      cur.clear();
+      if (!*q) break;
+    } else {
+      cur += *q;
+    }
+  }
+  return out;
 }
 
 static void usage() {
@@ -237,6 +288,8 @@ int main(int argc, char** argv) {
   pdo::NodeInfo node;
   node.name = "local";
   node.gpus = f.gpus >= 0 ? f.gpus : detect_gpus();
+  node.gpu_cpulists = detect_gpu_cpulists();
+  if ((int)node.gpu_cpulists.size() > node.gpus) node.gpu_cpulists.resize(node.gpus);
   co.nodes.push_back(node);
   pdo::Cluster cluster(co);
   pdo::WatchHub hub;

@@ -173,3 +173,38 @@ def _cast_scale(src: torch.Tensor, dst: torch.Tensor, scale: float):
         _native.require_hip().cast_scale_bf16_f32(src, dst, scale)
     else:
         torch.mul(src.float(), scale, out=dst)
+
+
+def broadcast_buffers(tensors, src: int = 0, group=None):
+    """Broadcast many small non-arena tensors (BatchNorm running stats, step
+    counters) in one collective per dtype instead of one each.
+
+    On the GPU the pack/unpack is a single HIP launch each way
+    (``flatten_scale``, csrc/hip/bucket.hip); ResNet-50's 106 fp32 BN stats
+    become one RCCL broadcast at job start.  Other dtypes (the int64
+    ``num_batches_tracked``) go through torch.cat / copy_."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for dt, ts in by_dtype.items():
+        n = sum(t.numel() for t in ts)
+        flat = torch.empty(n, dtype=dt, device=ts[0].device)
+        offs, o = [], 0
+        for t in ts:
+            offs.append(o)
+            o += t.numel()
+        hip = ts[0].is_cuda and dt in (torch.float32, torch.bfloat16) and all(t.is_contiguous() for t in ts)
+        if hip:
+            from .. import _native
+            m = _native.require_hip()
+            m.flatten_scale(ts, flat, offs, 1.0, False)
+        else:
+            torch.cat([t.reshape(-1) for t in ts], out=flat)
+        dist.broadcast(flat, src, group=group)
+        if hip:
+            m.flatten_scale(ts, flat, offs, 1.0, True)
+        else:
+            for t, off in zip(ts, offs):
+                t.copy_(flat[off:off + t.numel()].view_as(t))

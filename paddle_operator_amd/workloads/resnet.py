@@ -20,7 +20,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from ..models.resnet import resnet18_like_tiny, resnet50
-from ..parallel.ddp import BucketedDDP
+from ..parallel.ddp import BucketedDDP, broadcast_buffers
 from ..parallel.flat import FlatParams
 
 
@@ -71,8 +71,7 @@ class ResNetTrainer:
     def sync_initial_weights(self):
         self.ddp.broadcast_params(0)
         if self.ddp.world > 1:
-            for b in self.model.buffers():
-                dist.broadcast(b, 0)
+            broadcast_buffers(list(self.model.buffers()), 0)
 
     def batch(self):
         x = torch.randn(self.B, 3, self.res, self.res, device=self.device, generator=self.gen)

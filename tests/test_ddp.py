@@ -204,3 +204,30 @@ def test_grad_reduce_precision_4_ranks(tmp_path):
     assert e_single < 0.05, e_single  # sanity: the bf16 model itself
     assert e_bf16 < 1.5 * e_single + 1e-3, (e_bf16, e_single)
     assert e_fp32 < 1.5 * e_single + 1e-3, (e_fp32, e_single)
+
+
+def _bcast_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from paddle_operator_amd.parallel.ddp import broadcast_buffers
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ts = [torch.full((3, 2), float(rank)), torch.full((5,), float(rank) + 0.5), torch.tensor(rank, dtype=torch.long)]
+    broadcast_buffers(ts, 0)
+    q.put((rank, [t.tolist() for t in ts]))
+    dist.destroy_process_group()
+
+
+def test_broadcast_buffers_one_collective_per_dtype():
+    """ResNet BN running stats + counters reach every rank from rank 0."""
+    import torch.multiprocessing as mp
+    from test_launch import free_port_block
+    port = free_port_block(2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bcast_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(3):
+        assert out[r] == [[[0.0, 0.0]] * 3, [0.5] * 5, 0], out[r]
