@@ -674,6 +674,11 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_dw_impl", [](int impl) {
+    const int prev = pdo::gemm_dw_get_impl();
+    if (impl >= 0) pdo::gemm_dw_set_impl(impl);
+    return prev;
+  }, py::arg("impl") = -1, "select gemm_dw's mainloop (0 = 8-wave, 1.. = 4-wave variants); returns the previous");
   m.def("gemm_nt_impl", [](int impl) {
     const int prev = pdo::gemm_nt_get_impl();
     if (impl >= 0) pdo::gemm_nt_set_impl(impl);

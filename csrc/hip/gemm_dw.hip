@@ -215,8 +215,28 @@ __global__ __launch_bounds__(NTHR) void gemm_dw_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
+static int g_dw_impl = 2;  // 4-wave mainloop (gemm_dw4.hip) variant 1 (barrier after group 7), where its contract holds
+void gemm_dw_set_impl(int impl) { g_dw_impl = impl; }
+int gemm_dw_get_impl() { return g_dw_impl; }
+
+// gemm_dw4: every split's k-tile count even and ≥ 4 (no remainder), ≤ 256
+// workgroups (one resident round, one workgroup per CU)
+static int dw4_splits(long long T, int M, int N) {
+  const int tiles = (M / BM) * (N / BN);
+  const long long ks = T / BK;
+  for (int s = 16; s >= 1; --s) {
+    if ((long long)tiles * s > 256 && s > 1) continue;
+    if (ks % s == 0 && (ks / s) % 2 == 0 && ks / s >= 4) return s;
+  }
+  return 0;
+}
+
 int gemm_dw_splits(long long T, int M, int N) {
   if (M % BM || N % BN || T % BK || T <= 0) return 0;
+  if (g_dw_impl >= 1) {
+    const int s = dw4_splits(T, M, N);
+    if (s) return s;
+  }
   // one resident round of ≤ 256 workgroups (one per CU), as many as fit:
   // measured, 240 WGs in one round beat 768 in three (per-WG prologue, fold)
   const int tiles = (M / BM) * (N / BN);
@@ -232,6 +252,10 @@ int gemm_dw(const bf16* A, const bf16* B, long long T, int M, int N, int lda, in
   if (M % BM || N % BN || T % BK || splits < 1 || splits > 16) return -2;
   const long long ks = T / BK;
   if (ks < splits || ks > 0x7fffffffLL) return -2;
+  if (g_dw_impl >= 1) {
+    const int rc = gemm_dw4(A, B, T, M, N, lda, ldb, C, ldc, accumulate, ws, splits, st, g_dw_impl - 1);
+    if (rc != -2) return rc;  // -2: this split count breaks its contract → the 8-wave loop
+  }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles * splits;
   if (splits == 1) {

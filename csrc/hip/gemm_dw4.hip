@@ -1,0 +1,285 @@
+// SPDX-License-Identifier: Apache-2.0
+// Weight-gradient GEMM C[M][N] (+)= Σ_t A[t][M] · B[t][N] on gfx950 — the
+// 4-wave, one-wave-per-SIMD mainloop (same contract as gemm_dw.hip, selected
+// by gemm_dw_set_impl).  The operand handling is gemm_dw's: token-major tiles
+// staged into LDS as they lie in memory (LDS-DMA, swizzle on the source
+// address) and every fragment read with ds_read_b64_tr_b16; the schedule is
+// gemm_nt4's (profiles/r2_gemm_nt4.md): each wave owns 128 × 128 outputs = 16
+// v_mfma_f32_32x32x16_bf16 accumulators (256 registers, pinned to the
+// accumulator file), and one instruction stream per wave interleaves MFMAs,
+// transposed reads and DMA:
+//
+//   tile t (64 tokens, LDS buffer t&1), 64 MFMAs per wave:
+//   block 0 (tokens 0-31): 16 groups of {2 MFMAs on fragments F0; 1 fragment
+//            of F1 (tokens 32-63) read; 1 DMA piece of tile t+1 (the first
+//            E pieces went out at the end of tile t-1)}
+//   block 1 (tokens 32-63): 16 groups of {2 MFMAs on F1}; after group BAR the
+//            wave retires its DMA (vmcnt(0)) and reads (lgkmcnt(0)), one
+//            s_barrier; the remaining groups read F0 of tile t+1 and issue the
+//            first E = 15 - BAR DMA pieces of tile t+2 into buffer t&1.
+//
+// RAW / WAR: as gemm_nt4.hip (one barrier per tile; a buffer is refilled only
+// after the barrier that follows every wave's last read of it).
+#include <type_traits>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int LROW = 256;             // LDS row (elements) of a [BK][256] tile
+constexpr int TILE = BK * LROW;       // elements per operand tile
+constexpr int OPB = TILE * 2;         // bytes per operand tile (32 KiB)
+constexpr int NTHR = 256;
+
+// element offset of (token row r, 16-B chunk ch) in the swizzled LDS tile
+__device__ __forceinline__ int loff(int r, int ch) { return r * LROW + ((ch ^ ((r & 3) << 2)) << 3); }
+
+// per-lane element offset of the transposed 32x32x16 fragment for columns
+// [cb, cb + 32) at token 0 (gemm_dw.hip frag_base)
+__device__ __forceinline__ int frag_base(int cb, int lane) {
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  const int col = cb + 16 * (g & 1) + 4 * p;
+  const int r0 = 4 * (g >> 1) + q;
+  return loff(r0, col >> 3) + (col & 7);
+}
+
+template <int K0>
+__device__ __forceinline__ bf16x8 frag(const bf16* T) {
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(T + K0 * LROW));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(T + (K0 + 8) * LROW));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BAR>
+__global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           int lda, int ldb, int M, int N, int ksteps_total,
+                                                           int splits, bf16* __restrict__ C, int ldc,
+                                                           long long split_stride, int accumulate) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];  // [buf][A|B][BK][256]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int tiles_n = N / BN, tiles_m = M / BM;
+  const int nwg = tiles_m * tiles_n * splits;
+  int id = blockIdx.x;
+  {  // bijective XCD remap (gemm_dw.hip)
+    const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tn = id % tiles_n;
+  const int tm = (id / tiles_n) % tiles_m;
+  const int split = id / (tiles_n * tiles_m);
+  const int kq = ksteps_total / splits, kr = ksteps_total % splits;
+  const int k0 = split * kq + min(split, kr);
+  const int nk = kq + (split < kr ? 1 : 0);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- LDS-DMA: a wave-instruction fills 1 KiB = 2 token rows of 512 B.  Wave
+  // w's piece i (0..7) of an operand covers rows 2(4i + w) + (l >> 5), LDS chunk
+  // l & 31 holding global chunk (l & 31) ^ 4·(row & 3); row & 3 = (2w + (l >> 5))
+  // & 3 is fixed per lane.  Per-lane byte offset in a VGPR, wave-uniform base
+  // (k-tile, piece) in SGPRs.
+  const int rl = lane >> 5;
+  const int cs = (lane & 31) ^ (((2 * w + rl) & 3) << 2);
+  const unsigned voffA = (unsigned)((rl * lda + cs * 8) * 2), voffB = (unsigned)((rl * ldb + cs * 8) * 2);
+  const bf16* baseA = A + ((size_t)k0 * BK + 2 * w) * lda + m0;
+  const bf16* baseB = B + ((size_t)k0 * BK + 2 * w) * ldb + n0;
+  const unsigned stepAb = (unsigned)(16 * lda), stepBb = (unsigned)(16 * ldb);  // 8 rows, bytes
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem + (unsigned)(w * 1024);
+  // M0 is not saved around the DMA: nothing else in this kernel uses it
+  auto glds = [](unsigned voff, const bf16* sbase, unsigned lds_byte) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
+                 : "v"(voff), "s"(sbase), "s"(lds_byte)
+                 : "memory");
+  };
+  struct Src {
+    const char* a;
+    const char* b;
+    unsigned sa, sb;
+  };
+  auto srcs = [&](int kt) {  // laundered per tile: pieces form their bases with scalar adds
+    Src r{reinterpret_cast<const char*>(baseA + (size_t)kt * BK * lda),
+          reinterpret_cast<const char*>(baseB + (size_t)kt * BK * ldb), stepAb, stepBb};
+    asm volatile("" : "+s"(r.a), "+s"(r.b), "+s"(r.sa), "+s"(r.sb));
+    return r;
+  };
+  auto dma = [&](const Src& sr, auto buf_tag, int p) {  // p < 8: A piece p, else B piece p - 8
+    constexpr int BUF = decltype(buf_tag)::value;
+    const unsigned base = lds0 + (unsigned)(BUF * 2 * OPB);
+    if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
+    else glds(voffB, reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+  };
+
+  // ---- fragments: block half h (0: tokens 0-31, 1: 32-63) holds k-steps 2h, 2h+1;
+  // slot q (0..15) = k-step q >> 3, operand (q & 7) < 4 ? A mb : B nb
+  const bf16* smA[2] = {smem, smem + 2 * TILE};
+  int fa[4], fb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    fa[i] = frag_base(wm * 128 + 32 * i, lane);
+    fb[i] = TILE + frag_base(wn * 128 + 32 * i, lane);
+  }
+  auto rd = [&](auto buf_tag, int h, int q) -> bf16x8 {
+    constexpr int BUF = decltype(buf_tag)::value;
+    const bf16* T = smA[BUF] + ((q & 7) < 4 ? fa[q & 3] : fb[q & 3]);
+    const int ks = 2 * h + (q >> 3);
+    switch (ks) {
+      case 0: return frag<0>(T);
+      case 1: return frag<16>(T);
+      case 2: return frag<32>(T);
+      default: return frag<48>(T);
+    }
+  };
+  auto mma = [](f32x16& c, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  };
+  auto mma0 = [](f32x16& c, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+
+  f32x16 acc[4][4];  // first written by mma0 in tile 0's block 0
+  bf16x8 f0[16], f1[16];
+
+  {
+    const Src s0 = srcs(0);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) f0[q] = rd(B0{}, 0, q);
+
+  constexpr int E = 15 - BAR;
+  auto tile = [&](int t, auto buf_tag, auto more_tag, auto first_tag, auto ein_tag, auto eout_tag) {
+    constexpr int BUF = decltype(buf_tag)::value;
+    constexpr bool MORE = decltype(more_tag)::value;
+    constexpr bool FIRST = decltype(first_tag)::value;
+    constexpr bool EIN = decltype(ein_tag)::value;
+    constexpr bool EOUT = decltype(eout_tag)::value;
+    constexpr int P0 = EIN ? E : 0;
+    using NB = std::integral_constant<int, BUF ^ 1>;
+    using SB = std::integral_constant<int, BUF>;
+    Src sn{}, sn2{};
+    if constexpr (MORE) sn = srcs(t + 1);
+    if constexpr (EOUT) sn2 = srcs(t + 2);
+    // ---- block 0: MFMAs on F0 (k-steps 0, 1), F1 reads, DMA of tile t+1
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int ks = g >> 3, mb = (g >> 1) & 3, nb0 = 2 * (g & 1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (FIRST && ks == 0) mma0(acc[mb][nb0 + u], f0[8 * ks + mb], f0[8 * ks + 4 + nb0 + u]);
+        else mma(acc[mb][nb0 + u], f0[8 * ks + mb], f0[8 * ks + 4 + nb0 + u]);
+      }
+      f1[g] = rd(buf_tag, 1, g);
+      if constexpr (MORE) {
+        if (P0 + g < 16) dma(sn, NB{}, P0 + g);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- block 1: MFMAs on F1 (k-steps 2, 3); barrier; F0 reads of tile t+1
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int ks = g >> 3, mb = (g >> 1) & 3, nb0 = 2 * (g & 1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) mma(acc[mb][nb0 + u], f1[8 * ks + mb], f1[8 * ks + 4 + nb0 + u]);
+      if constexpr (MORE) {
+        if (g == BAR) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if (g > BAR) {
+          if constexpr (EOUT) dma(sn2, SB{}, g - BAR - 1);
+          constexpr int RPG = 16 / (15 - BAR);
+#pragma unroll
+          for (int u = 0; u < RPG; ++u) f0[RPG * (g - BAR - 1) + u] = rd(NB{}, 0, RPG * (g - BAR - 1) + u);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  // nk is even and ≥ 4 (host contract)
+  tile(0, B0{}, T_{}, T_{}, F_{}, T_{});
+  tile(1, B1{}, T_{}, F_{}, T_{}, T_{});
+  for (int t = 2; t < nk - 2; t += 2) {
+    tile(t, B0{}, T_{}, F_{}, T_{}, T_{});
+    tile(t + 1, B1{}, T_{}, F_{}, T_{}, T_{});
+  }
+  tile(nk - 2, B0{}, T_{}, F_{}, T_{}, F_{});
+  tile(nk - 1, B1{}, F_{}, F_{}, F_{}, F_{});
+
+  // ---- epilogue: acc[mb][nb][r] = C[m0 + wm·128 + 32mb + (r&3) + 8(r>>2) + 4hh][n0 + wn·128 + 32nb + (l&31)]
+  // the accumulators leave through explicit v_accvgpr_read, padded against the
+  // last MFMAs (hipcc does not see into the asm): 16 wait states
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  bf16* Cb = C + (size_t)split * split_stride;
+  const int hh = lane >> 5, li = lane & 31;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[r]) : "a"(acc[mb][nb][r]));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const int n = n0 + wn * 128 + 32 * nb + li;
+        bf16* p = Cb + (size_t)m * ldc + n;
+        float x = v[r];
+        if (accumulate) x += (float)*p;
+        *p = (bf16)x;
+      }
+    }
+}
+
+}  // namespace
+
+// nk per split must be even and ≥ 4: the caller's split count keeps every slice
+// long enough; returns -2 when a slice would not be
+int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
+             int accumulate, bf16* ws, int splits, hipStream_t st, int variant) {
+  if (M % BM || N % BN || T % BK || splits < 1 || splits > 16) return -2;
+  const long long ks = T / BK;
+  if (ks > 0x7fffffffLL) return -2;
+  // every split's k-tile count even and ≥ 4
+  const long long kq = ks / splits, kr = ks % splits;
+  if (kq < 4 || kq % 2 || kr) return -2;
+  const int tiles = (M / BM) * (N / BN);
+  const int grid = tiles * splits;
+  bf16* out = C;
+  int ldo = ldc;
+  long long stride = 0;
+  int acc = accumulate;
+  if (splits > 1) {
+    if (!ws || ldc != N) return -3;
+    out = ws;
+    ldo = N;
+    stride = (long long)M * N;
+    acc = 0;
+  }
+  if (variant == 1)
+    gemm_dw4_kernel<7><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+  else
+    gemm_dw4_kernel<11><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+  if (splits > 1) return splitk_add(ws, splits, (long long)M * N, C, accumulate, st);
+  return 0;
+}
+
+}  // namespace pdo

@@ -62,6 +62,12 @@ int maxpool3s2_bwd(const bf16* dy, const uint8_t* arg, int N, int H, int W, int 
 int gemm_dw_splits(long long T, int M, int N);
 int gemm_dw(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
             int accumulate, bf16* ws, int splits, hipStream_t st);
+// gemm_dw4.hip: the same contract on the 4-wave / 128 × 128-per-wave mainloop (-2: split count unsupported)
+int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
+             int accumulate, bf16* ws, int splits, hipStream_t st, int variant);
+// which mainloop gemm_dw() runs: 0 = 8-wave (gemm_dw.hip), 1.. = 4-wave variant impl - 1
+void gemm_dw_set_impl(int impl);
+int gemm_dw_get_impl();
 // transpose.hip: out[C][R] = in[R][C], R and C multiples of 64
 // gemm_nt.hip: C[M][N] = A[M][K]·B[N][K]ᵀ with a fused epilogue
 // (0 plain, 1 +bias, 2 C = pre-activation & Y = gelu(C + bias),

@@ -546,3 +546,26 @@ def test_maxpool3s2_nhwc(cuda, N, C, H, W):
     y.backward(dy)
     yf.backward(dy.float())
     assert rel_err(x.grad, xf.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T,M,N,acc", [(8192, 4096, 4096, True), (65536, 1024, 3072, False), (16384, 512, 768, True)])
+def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
+    """The 4-wave dW mainloop (gemm_dw4.hip, both schedule variants; split-K or
+    in-kernel accumulate at one split) and the 8-wave one against fp32."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    g = torch.Generator(device=cuda).manual_seed(21)
+    dy = torch.empty(T, M, device=cuda).uniform_(-1, 1, generator=g).bfloat16()
+    x = torch.empty(T, N, device=cuda).uniform_(-1, 1, generator=g).bfloat16()
+    base = torch.empty(M, N, device=cuda).uniform_(-4, 4, generator=g).bfloat16() if acc else \
+        torch.zeros(M, N, device=cuda).bfloat16()
+    ref = base.float() + dy.float().t() @ x.float()
+    prev = m.gemm_dw_impl(0)
+    try:
+        for impl in (0, 1, 2):
+            m.gemm_dw_impl(impl)
+            out = base.clone()
+            assert m.gemm_dw(dy, x, out, True)
+            assert rel_err(out, ref) < 1e-2, (impl, m.gemm_dw_splits(T, M, N))
+    finally:
+        m.gemm_dw_impl(prev)

@@ -79,7 +79,7 @@ def build_hip(jobs=8, verbose=False):
     # live in the accumulator file; the vgpr form made hipcc shuttle them
     # through arch VGPRs, 3 VALU per MFMA)
     vgpr_form = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
-    agpr_files = {"gemm_nt4.hip"}
+    agpr_files = {"gemm_nt4.hip", "gemm_dw4.hip"}
     # per-file extras: attention's softmax max-reductions become v_max3 only
     # without NaN canonicalisation (scores are never NaN; ±inf masks keep working)
     extra = {"attention.hip": ["-fno-honor-nans"]}
