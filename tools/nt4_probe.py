@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="")
     ap.add_argument("--variants", type=int, default=1, help="gemm_nt4 schedule variants to A/B (impl 1..N)")
+    ap.add_argument("--impls", default="", help="explicit impl list, e.g. 0,1,5,6 (first = reference)")
     a = ap.parse_args()
     enable_tuned_gemms()
     m = _native.require_hip()
@@ -66,18 +67,19 @@ def main():
         else:
             ours = lambda: m.gemm_nt_dgelu(x, w, pre, b)  # noqa: E731
             lib = lambda: m.bias_gelu_bwd(F.linear(x, w), pre, b)  # noqa: E731
-        impls = [0] + [1 + v for v in range(a.variants)]
+        impls = [int(x) for x in a.impls.split(",")] if a.impls else [0] + [1 + v for v in range(a.variants)]
         outs = {}
         for impl in impls:
             m.gemm_nt_impl(impl)
             o = ours()
             outs[impl] = [t.clone() for t in (o if isinstance(o, (list, tuple)) else [o])]
         torch.cuda.synchronize()
-        ident = all(torch.equal(p, q) for i in impls[1:] for p, q in zip(outs[0], outs[i]))
-        maxdiff = max((p.float() - q.float()).abs().max().item() for i in impls[1:] for p, q in zip(outs[0], outs[i]))
+        i0 = impls[0]
+        ident = all(torch.equal(p, q) for i in impls[1:] for p, q in zip(outs[i0], outs[i]))
+        maxdiff = max((p.float() - q.float()).abs().max().item() for i in impls[1:] for p, q in zip(outs[i0], outs[i]))
         R = 512
         ref = x[-R:].float() @ w.float().t()
-        c0 = outs[0][0][-R:].float()
+        c0 = outs[impls[-1]][0][-R:].float()
         if epi == "bias":
             ref = ref + b.float()
         ref_err = (c0 - ref).abs().max().item() if epi in ("plain", "bias", "gelu") else None
