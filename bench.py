@@ -78,8 +78,12 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="ranks to launch (one MI355X each)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="gpt2", choices=["gpt2", "resnet50"],
+                    help="gpt2 = the BASELINE headline (GPT-2-medium tokens/s); resnet50 = configs 2/3 (images/s)")
     ap.add_argument("--model", default="gpt2-medium")
-    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("PDO_MICRO_BATCH", "64")))
+    ap.add_argument("--tiny", action="store_true", help=argparse.SUPPRESS)  # CPU tests: tiny resnet
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("PDO_MICRO_BATCH", "0")),
+                    help="per-rank batch (default 64 sequences for gpt2, 256 images for resnet50)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--ready-trials", type=int, default=10)
     ap.add_argument("--compat-trials", type=int, default=0,
@@ -215,6 +219,8 @@ def orchestrate(a):
     from paddle_operator_amd.utils.topology import gpu_count
 
     N = a.gpus
+    if not a.micro_batch:
+        a.micro_batch = 64 if a.workload == "gpt2" else 256
     detected = 0 if a.cpu else gpu_count()
     if detected and detected < N:
         log(f"--gpus {N} but only {detected} GPU(s) visible")
@@ -240,9 +246,12 @@ def orchestrate(a):
                                           if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "PDO_"))}}),
                       flush=True)
                 return 0
-            name = "gpt2-bench"
-            wl = ["--workload", "gpt2", "--model", a.model, "--batch", str(a.micro_batch), "--seq", str(a.seq),
-                  "--steps", str(a.steps), "--warmup", str(a.warmup), "--bench", "--timeout", "600"]
+            name = f"{a.workload}-bench"
+            if a.workload == "gpt2":
+                wl = ["--workload", "gpt2", "--model", a.model, "--batch", str(a.micro_batch), "--seq", str(a.seq)]
+            else:
+                wl = ["--workload", "resnet50", "--batch", str(a.micro_batch)] + (["--tiny"] if a.tiny else [])
+            wl += ["--steps", str(a.steps), "--warmup", str(a.warmup), "--bench", "--timeout", "600"]
             t0 = L.launch(name, N, wl, a.ops)
             rs = L.wait_records(name, "bench", N, a.timeout)
             L.finish(name)
@@ -265,46 +274,48 @@ def orchestrate(a):
 
     rs = out["bench"]
     dt = max(r["seconds"] for r in rs)  # max over ranks
-    tokens = sum(r["tokens_per_step_rank"] for r in rs) * a.steps
-    tps = tokens / dt
-    cfg = GPT2Config.named(a.model)
-    flops_gpu = cfg.flops_per_token(a.seq) * tps / N
-    rec = {
-        "metric": "launched tokens/sec (GPT-2-medium PaddleJob through the pdo operator, collective DP over RCCL)",
-        "value": round(tps, 1),
-        "unit": "tokens/s",
-        "n_gpus": N,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(dt / a.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
+    items = sum(r["tokens_per_step_rank"] for r in rs) * a.steps
+    rate = items / dt
+    common = {
+        "n_gpus": N, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,  # BASELINE.json publishes no number ("published": {})
         "dtype": "bf16",
-        "data": "synthetic (on-device random tokens), random-init weights",
-        "config": {
-            "model": a.model,
-            "global_batch": a.micro_batch * N,
-            "micro_batch_per_gpu": a.micro_batch,
-            "seq_len": a.seq,
-            "parallelism": f"dp{N}",
-            "launch": f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}, "
-                      f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}",
-            "grad_reduce": rs[0].get("grad_reduce"),
-            "buckets": rs[0].get("buckets"),
-            "ops": a.ops,
-            "device": "cpu/gloo" if not gpus else rs[0].get("gpu_name", "gpu"),
-        },
+    }
+    launch = (f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}, "
+              f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}")
+    extra = {
         "baseline_metric": BASELINE_METRIC,
         "ready_p50_s": out["ready"]["p50"] if out.get("ready") else None,
         "ready": out.get("ready"),
         "compat_ready": out.get("compat_ready"),
-        "gpt2_job_ready_s": round(out["bench_ready_s"], 3),
-        "model_tflops_per_gpu": round(flops_gpu / 1e12, 1),
-        "mfu_vs_2.5PF_dense": round(flops_gpu / 2.5e15, 4),
+        "job_ready_s": round(out["bench_ready_s"], 3),
         "final_loss": rs[0].get("loss"),
         "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in rs),
     }
+    dev = "cpu/gloo" if not gpus else rs[0].get("gpu_name", "gpu")
+    if a.workload == "gpt2":
+        cfg = GPT2Config.named(a.model)
+        flops_gpu = cfg.flops_per_token(a.seq) * rate / N
+        rec = {"metric": "launched tokens/sec (GPT-2-medium PaddleJob through the pdo operator, collective DP over RCCL)",
+               "value": round(rate, 1), "unit": "tokens/s", **common,
+               "data": "synthetic (on-device random tokens), random-init weights",
+               "config": {"model": a.model, "global_batch": a.micro_batch * N, "micro_batch_per_gpu": a.micro_batch,
+                          "seq_len": a.seq, "parallelism": f"dp{N}", "launch": launch,
+                          "grad_reduce": rs[0].get("grad_reduce"), "buckets": rs[0].get("buckets"), "ops": a.ops,
+                          "device": dev},
+               **extra,
+               "gpt2_job_ready_s": extra["job_ready_s"],
+               "model_tflops_per_gpu": round(flops_gpu / 1e12, 1),
+               "mfu_vs_2.5PF_dense": round(flops_gpu / 2.5e15, 4)}
+    else:
+        rec = {"metric": "launched images/sec (ResNet-50 PaddleJob through the pdo operator, collective DP over RCCL)",
+               "value": round(rate, 1), "unit": "images/s", **common,
+               "data": "synthetic (on-device random 224x224 images and labels), random-init weights",
+               "config": {"model": "resnet50", "global_batch": a.micro_batch * N, "micro_batch_per_gpu": a.micro_batch,
+                          "resolution": 224, "parallelism": f"dp{N}", "launch": launch,
+                          "grad_reduce": rs[0].get("grad_reduce"), "buckets": rs[0].get("buckets"), "device": dev},
+               **extra}
     print(json.dumps(rec), flush=True)
     return 0
 

@@ -231,3 +231,15 @@ def test_broadcast_buffers_one_collective_per_dtype():
         p.join(60)
     for r in range(3):
         assert out[r] == [[[0.0, 0.0]] * 3, [0.5] * 5, 0], out[r]
+
+
+def test_bench_launched_resnet_workload():
+    """bench.py --workload resnet50 (configs 2/3 through the operator): images/s record."""
+    args = ["--workload", "resnet50", "--tiny", "--micro-batch", "4", "--steps", "2", "--warmup", "1",
+            "--ready-trials", "1", "--cpu"]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + args, cwd=REPO, env=_bench_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["unit"] == "images/s" and rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 8
+    assert abs(rec["value"] - 4 * 2 * 2 / (rec["ms_per_step"] * 2 / 1e3)) / rec["value"] < 1e-2
