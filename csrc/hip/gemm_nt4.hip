@@ -44,7 +44,7 @@ namespace {
 constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
 constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 = 32 KiB
 
-template <int EPI, int GPG, int BAR, int BUFLD>
+template <int EPI, int EPG, int BAR, int BUFLD>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   // E = DMA pieces of tile t+2 issued early, in block 1 of tile t right after
   // its barrier (buffer t&1 is free then: every wave retired its last reads
   // of it before that barrier); block 0 of tile t+1 issues the other 16 - E
-  constexpr int E = 15 - BAR;
+  constexpr int E = EPG * (15 - BAR) < 16 ? EPG * (15 - BAR) : 16;  // EPG early pieces per group after the barrier
   // ps: MORE = tile t+1 exists; EIN = its first E pieces were issued early;
   // EOUT = issue the first E pieces of tile t+2 after this tile's barrier
   auto tile = [&](int t, auto buf_tag, auto more_tag, auto first_tag, auto ein_tag, auto eout_tag) {
@@ -215,9 +215,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       else if (g <= 8) fb1[g - 1] = v;
       else fa1[g - 8] = v;
       if constexpr (MORE) {
-#pragma unroll
-        for (int u = 0; u < GPG; ++u)
-          if (P0 + GPG * g + u < 16) dma(sn, NB{}, P0 + GPG * g + u);
+        if (P0 + g < 16) dma(sn, NB{}, P0 + g);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -235,7 +233,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           __builtin_amdgcn_s_barrier();
         }
         if (g > BAR) {
-          if constexpr (EOUT) dma(sn2, SB{}, g - BAR - 1);
+          if constexpr (EOUT) {
+#pragma unroll
+            for (int u = 0; u < EPG; ++u)
+              if (EPG * (g - BAR - 1) + u < E) dma(sn2, SB{}, EPG * (g - BAR - 1) + u);
+          }
           constexpr int RPG = 16 / (15 - BAR);  // F0 reads per remaining group
 #pragma unroll
           for (int u = 0; u < RPG; ++u) {
@@ -359,15 +361,16 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
+  using I4 = std::integral_constant<int, 4>;
   using I7 = std::integral_constant<int, 7>;
   using I11 = std::integral_constant<int, 11>;
   using I13 = std::integral_constant<int, 13>;
   // schedule variants under A/B (tools/nt4_probe.py, profiles/r2_gemm_nt4.md):
-  // 0 = one DMA piece per group + barrier after block-1 group 11 (the default)
+  // 0 = barrier after block-1 group 11, the first 4 DMA pieces of tile t+2 after it, the rest one per block-0 group (default)
   switch (variant) {
     case 1: return launch(I1{}, I7{}, I0{});
-    case 2: return launch(I1{}, I13{}, I0{});
-    case 3: return launch(I1{}, I11{}, I1{});
+    case 2: return launch(I2{}, I7{}, I0{});   // every piece of tile t+2 right after tile t's barrier
+    case 3: return launch(I4{}, I11{}, I0{});  // the same, 4 per group after a later barrier
     default: return launch(I1{}, I11{}, I0{});
   }
   return 0;
