@@ -27,6 +27,8 @@
 // ds_read immediates (toff_v; 1.6 % on the forward, bitwise-identical output).
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -78,6 +80,17 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = (bf16)x[8 * s + j];
   return r;
+}
+
+// lane l ↔ lane l ^ 32 combine through v_permlane32_swap (a VALU op; __shfl_xor
+// by 32 is a ds_bpermute LDS round trip on the softmax critical path)
+__device__ __forceinline__ float xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 // Retire loop-invariant operand loads BEFORE the tile loop.  Otherwise
@@ -268,7 +281,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
       float tmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+      tmax = xhalf_max(tmax) * c2;
       const bool grow = tmax > m + 8.f;
       if (__any(grow)) {
         const float mn = grow ? fmaxf(m, tmax) : m;
@@ -313,7 +326,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
     }
     __syncthreads();
   }
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = xhalf_sum(l);
   const float inv = 1.f / lt;
   bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
   store_acc_rows(orow, o0, 0, hh, inv);
@@ -401,22 +414,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
           sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
           dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
         }
-        const bool diag = qb0 < wave_kmin + 31;
-        // rows r: q = qb0 + (r&3) + 8(r>>2) + 4hh
+        // rows r: q = qb0 + (r&3) + 8(r>>2) + 4hh.  The causal mask only touches the
+        // diagonal sub-tile (wave-uniform): a separate body keeps its compares and
+        // selects out of every other tile
+        auto softmax_grad = [&](auto masked) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int qr = 32 * qs + 8 * g + 4 * hh;
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(L2 + qr);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + qr);
+          for (int g = 0; g < 4; ++g) {
+            const int qr = 32 * qs + 8 * g + 4 * hh;
+            const f32x4 l4 = *reinterpret_cast<const f32x4*>(L2 + qr);
+            const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + qr);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            float p = __builtin_amdgcn_exp2f(sacc[r] * c2 - l4[e]);
-            if (diag && (q0 + qr + e) < key) p = 0.f;
-            sacc[r] = p;
-            dpacc[r] = p * (dpacc[r] - d4[e]);
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g + e;
+              float p = __builtin_amdgcn_exp2f(sacc[r] * c2 - l4[e]);
+              if constexpr (decltype(masked)::value) p = (q0 + qr + e) < key ? 0.f : p;
+              sacc[r] = p;
+              dpacc[r] = p * (dpacc[r] - d4[e]);
+            }
           }
-        }
+        };
+        if (qb0 < wave_kmin + 31)
+          softmax_grad(std::true_type{});
+        else
+          softmax_grad(std::false_type{});
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 pb = pack8(sacc, sst);
@@ -453,7 +473,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
 // ============================================================================
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
 // ============================================================================
-__global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
                                                        int H, float c2, float scale, float* __restrict__ dbias_part) {
@@ -491,7 +511,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) dpart = __builtin_fmaf(a[j], c[j], dpart);
     }
   }
-  const float dq_delta = dpart + __shfl_xor(dpart, 32, 64);
+  const float dq_delta = xhalf_sum(dpart);
   if (hh == 0) delta[(size_t)bh * S + q] = dq_delta;
   retire(qf);
   retire(df);
@@ -526,13 +546,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_d64(const bf16* __restrict__ 
           s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
           dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
         }
+        auto softmax_grad = [&](auto masked) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          float p = __builtin_amdgcn_exp2f(s[r] * c2 - lq);
-          if (diag && kr > q) p = 0.f;
-          s[r] = p * (dp[r] - dq_delta);  // dS^T
-        }
+          for (int r = 0; r < 16; ++r) {
+            float p = __builtin_amdgcn_exp2f(s[r] * c2 - lq);
+            if constexpr (decltype(masked)::value) {
+              const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              p = kr > q ? 0.f : p;
+            }
+            s[r] = p * (dp[r] - dq_delta);  // dS^T
+          }
+        };
+        if (diag)  // wave-uniform: only the diagonal tile pays for the mask
+          softmax_grad(std::true_type{});
+        else
+          softmax_grad(std::false_type{});
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 dsb = pack8(s, sst);
