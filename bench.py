@@ -246,6 +246,11 @@ def orchestrate(a):
                                           if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "PDO_"))}}),
                       flush=True)
                 return 0
+            if os.environ.get("PDO_BENCH_PS"):
+                import psutil
+                kids = psutil.Process().children(recursive=True)
+                log(f"{len(kids)} descendant processes before the bench job: " +
+                    "; ".join(f"{k.pid} {' '.join(k.cmdline()[:3])[-60:]}" for k in kids))
             name = f"{a.workload}-bench"
             if a.workload == "gpt2":
                 wl = ["--workload", "gpt2", "--model", a.model, "--batch", str(a.micro_batch), "--seq", str(a.seq)]

@@ -460,6 +460,53 @@ class _GeluLinearFn(torch.autograd.Function):
         return dhp.view(ctx.shape), db1, dw2
 
 
+class _NTMLPFn(torch.autograd.Function):
+    """m = gelu(x·W1ᵀ + b1)·W2ᵀ with both GELU passes inside gemm_nt epilogues.
+
+    fc1 forward runs gemm_nt's GELU epilogue (csrc/hip/gemm_nt4.hip, EPI 2):
+    the tile writes the pre-activation hp (the backward's GELU' input) and
+    h = gelu(hp + b1) from registers, so the [tokens, 4C] activation is not
+    re-read by a separate bias-GELU pass.  Backward = _GeluLinearFn's fused
+    dGELU epilogue plus fc1's dW / dX.  Measured at [65536, 1024] → 4096 on
+    1×MI355X: 598.7 µs vs 644.5 µs for hipBLASLt + bias_gelu_fwd
+    (tools/nt4_probe.py fc1_fwd, profiles/r2_gemm_nt4.md)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        m = _native.require_hip()
+        x2 = x.reshape(-1, x.shape[-1])
+        hp, h = m.gemm_nt_gelu(x2, w1, b1)
+        ctx.save_for_backward(x2, w1, hp, h, w2)
+        ctx.b1 = b1
+        ctx.shape = x.shape
+        return F.linear(h, w2).view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x2, w1, hp, h, w2 = ctx.saved_tensors
+        b1 = ctx.b1
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dw2 = _weight_grad(w2, dy2, h) if ctx.needs_input_grad[3] else None
+        gd = _arena_grads((b1,))
+        if gd is not None:
+            (dhp,) = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1, db_out=gd[0])
+            _signal_ready((b1,))
+            db1 = None
+        else:
+            dhp, db1 = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1)
+        dw1 = _weight_grad(w1, dhp, x2) if ctx.needs_input_grad[1] else None  # its bucket can go first
+        dx = _input_grad(dhp, w1).view(ctx.shape) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2
+
+
+# fc1 forward with the fused GELU epilogue (gemm_nt): off by default.  In the
+# GPT-2-medium step (tools/gpu_ab_probe.sh PDO_NT_GELU=0/1, same box, 2 rounds)
+# it ran 152.25 / 152.80 ms vs 152.74 / 153.21 ms for hipBLASLt + bias_gelu_fwd:
+# the probe's 46 µs per call does not survive cold operands.  PDO_NT_GELU=1 on.
+_NT_GELU = [os.environ.get("PDO_NT_GELU", "0") == "1"]
+
+
 # fc2 input gradient with the fused GELU' epilogue (gemm_nt) where its shape
 # contract holds; PDO_NT_DGELU=0 restores hipBLASLt + the bias-GELU kernel.
 _NT_DGELU = [os.environ.get("PDO_NT_DGELU", "1") != "0"]
@@ -481,6 +528,10 @@ def mlp(x, w1, b1, w2):
             _FUSED_MLP[0] = False
             if os.environ.get("PDO_VERBOSE"):
                 print(f"[pdo] fused MLP disabled: {e}")
+    if (_NT_GELU[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.is_contiguous()
+            and _nt_dgelu_ok(x, w2)
+            and _native.require_hip().gemm_nt_supported(x.numel() // x.shape[-1], w1.shape[0], w1.shape[1])):
+        return _NTMLPFn.apply(x, w1, b1, w2)
     hp = linear(x, w1)
     if use_hip(hp) and _nt_dgelu_ok(hp, w2):
         return _GeluLinearFn.apply(hp, b1, w2)

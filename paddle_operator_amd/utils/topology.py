@@ -196,12 +196,23 @@ def pin_to_gpu(local_rank: int, topo: Optional[Topology] = None) -> List[int]:
     if phys >= topo.n:
         return []
     cpus = topo.gpus[phys].cpus
-    if cpus:
-        try:
-            os.sched_setaffinity(0, cpus)
-        except OSError:
-            return []
-    return cpus
+    if not cpus or os.environ.get("PDO_PIN_CPUS", "1") == "0":
+        return []
+    # only within what this process may already use (a container / cgroup cpuset
+    # narrower than the NUMA node): never pin a rank's launch thread onto a
+    # handful of CPUs it then shares with the HIP runtime's own threads
+    allowed = os.sched_getaffinity(0)
+    use = [c for c in cpus if c in allowed]
+    if len(use) < min(_MIN_PIN_CPUS, len(allowed)):
+        return []
+    try:
+        os.sched_setaffinity(0, use)
+    except OSError:
+        return []
+    return use
+
+
+_MIN_PIN_CPUS = 4
 
 
 def gpu_count() -> int:

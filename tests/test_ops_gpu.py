@@ -465,8 +465,10 @@ def test_qkv_attention_fused_bias_grad(cuda):
 
 
 @pytest.mark.gpu
-def test_mlp_nt_dgelu_matches_unfused(cuda):
-    """fc2 input gradient with the fused GELU' epilogue (gemm_nt) == hipBLASLt + bias-GELU kernel."""
+@pytest.mark.parametrize("nt_gelu", [True, False])
+def test_mlp_nt_dgelu_matches_unfused(cuda, nt_gelu):
+    """gemm_nt epilogues in the MLP — fc1 GELU forward (_NTMLPFn) and/or fc2's input
+    gradient ⊙ GELU' — == hipBLASLt + the bias-GELU kernels (output and every gradient)."""
     ops = _ops()
     T, C = 4096, 512
     g = torch.Generator(device=cuda).manual_seed(5)
@@ -475,15 +477,20 @@ def test_mlp_nt_dgelu_matches_unfused(cuda):
             (0.1 * torch.randn(4 * C, device=cuda, generator=g)).bfloat16(),
             (0.05 * torch.randn(C, 4 * C, device=cuda, generator=g)).bfloat16()]
     dy = torch.randn(T, C, device=cuda, generator=g).bfloat16()
-    grads = []
+    grads, outs = [], []
     for fused in (True, False):
         ops._NT_DGELU[0] = fused
+        ops._NT_GELU[0] = fused and nt_gelu
         try:
             ts = [t.clone().requires_grad_() for t in base]
-            ops.mlp(*ts).backward(dy)
+            y = ops.mlp(*ts)
+            y.backward(dy)
         finally:
             ops._NT_DGELU[0] = True
+            ops._NT_GELU[0] = True
+        outs.append(y.detach().float())
         grads.append([t.grad.float() for t in ts])
+    assert rel_err(outs[0], outs[1]) < 1e-2, "y"
     for a, b, name in zip(grads[0], grads[1], ("dx", "dw1", "db1", "dw2")):
         assert rel_err(a, b) < 1e-2, name
 

@@ -10,7 +10,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def bench(fn, iters=20, warm=5):
