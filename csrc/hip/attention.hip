@@ -126,6 +126,43 @@ __device__ __forceinline__ void stage_store(const Stage& st, bf16* T, int tid) {
   }
 }
 
+// ----- global → LDS by LDS-DMA: no register staging, no ds_write -----
+// A [64 rows][64] bf16 tile in the toff() image is 8 pieces of 8 rows; a piece
+// is one wave-instruction (1 KiB: lane l → row 8p + (l >> 3), LDS chunk l & 7).
+// The XOR swizzle is applied on the SOURCE side: the lane fetches logical chunk
+// (l & 7) ^ swz(row), which toff() places at chunk l & 7.  Wave w moves pieces
+// 2w and 2w + 1 of every tile; swz() only sees row bits 1-3, so the per-lane
+// byte offsets of an even and an odd piece are two loop-invariant VGPRs.  M0
+// carries the piece's LDS address (nothing else in these kernels reads M0);
+// s_nop 0 = the SALU M0 write → LDS-DMA wait state.  The DMA counts in vmcnt:
+// consumers wait with s_waitcnt vmcnt(N) for their own pieces, then barrier.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ unsigned dma_voff(int lane, size_t row_stride, int odd) {
+  const int rr = lane >> 3;
+  return (unsigned)(((size_t)rr * row_stride + (size_t)(((lane & 7) ^ swz(8 * odd + rr)) << 3)) * 2);
+}
+__device__ __forceinline__ void glds16(unsigned voff, const void* sbase, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_byte)
+               : "memory");
+}
+__device__ __forceinline__ void glds4(unsigned voff, const void* sbase, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_byte)
+               : "memory");
+}
+// rows [row0 + 16w, row0 + 16w + 16) of a [rows][64] bf16 matrix → the wave's 2 pieces of an LDS tile
+__device__ __forceinline__ void dma_tile(const bf16* base, size_t row_stride, int row0, int wu, unsigned v_even,
+                                         unsigned v_odd, unsigned lds_tile) {
+  const bf16* src = base + (size_t)(row0 + 16 * wu) * row_stride;
+  glds16(v_even, src, lds_tile + 2048 * wu);
+  glds16(v_odd, src + 8 * row_stride, lds_tile + 2048 * wu + 1024);
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // store a 32x32 f32 accumulator (lane col = row index `rowv`, regs = 32 columns
 // starting at c0) as bf16 into dst[rowv][c0 + ...] with scale
 __device__ __forceinline__ void store_acc_rows(bf16* dst_row, const f32x16& acc, int c0, int hh, float s) {
@@ -341,9 +378,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
                                                          const float* __restrict__ lse, const float* __restrict__ delta,
                                                          bf16* __restrict__ dqkv, int B, int S, int H, float c2,
                                                          float scale, float* __restrict__ dbias_part) {
-  // [buf][Q|dO][64][64] bf16 + [buf][lse2|delta][64] f32
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD + 2 * 2 * TROWS * 2];
-  float* sstat = reinterpret_cast<float*>(smem + 2 * 2 * TROWS * HD);
+  // ring of 3 slots × {Q [64][64] bf16, dO [64][64] bf16, lse·log2e [64] f32, delta [64] f32}
+  constexpr int SLOT = 2 * TROWS * HD + 2 * TROWS * 2;  // bf16 units (16896 B)
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nkb = S / 128;
   const int bh = blockIdx.x % (B * H);
@@ -355,8 +392,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
   const bf16* kbase = qbase + (size_t)H * HD;
   const bf16* vbase = qbase + (size_t)2 * H * HD;
   const bf16* dobase = dout + (size_t)b * S * ors + (size_t)h * HD;
-  const float* lse_bh = lse + (size_t)bh * S;
+  const float* lse2_bh = delta + (size_t)B * H * S + (size_t)bh * S;  // lse·log2e, written by the dQ kernel
   const float* del_bh = delta + (size_t)bh * S;
+  (void)lse;
   (void)nkb;
 
   const int key = kb * 128 + w * 32 + li;  // this lane's key (column of S / dP)
@@ -373,35 +411,35 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
   const int nqt = S / TROWS;
   const int wave_kmin = kb * 128 + w * 32;
 
-  Stage sq, sd;
-  // threads 0-63 carry lse·log2e, 64-127 delta of the staged query tile (one
-  // register, one load: a two-variable select here became a scratch array)
-  float st_v = 0.f;
-  const float* st_src = tid < 64 ? lse_bh + tid : del_bh + (tid - 64);
-  const float st_mul = tid < 64 ? LOG2E : 1.f;
-  auto load_tile = [&](int qt) {
-    stage_load(sq, qbase, rs, qt * TROWS, tid);
-    stage_load(sd, dobase, ors, qt * TROWS, tid);
-    if (tid < 128) st_v = st_src[qt * TROWS];  // scaled at store time: no wait here
+  // tile qt → ring slot: Q and dO pieces (2 + 2 per wave) and one stats row per
+  // wave (waves 0/2 lse·log2e, 1/3 delta — the pairs write identical bytes), so
+  // every wave issues 5 DMAs per tile and waits with the same vmcnt
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned vq0 = dma_voff(lane, rs, 0), vq1 = dma_voff(lane, rs, 1);
+  const unsigned vd0 = dma_voff(lane, ors, 0), vd1 = dma_voff(lane, ors, 1);
+  auto issue = [&](int qt, int slot) {
+    const unsigned base = lds0 + (unsigned)(slot * SLOT * 2);
+    dma_tile(qbase, rs, qt * TROWS, wu, vq0, vq1, base);
+    dma_tile(dobase, ors, qt * TROWS, wu, vd0, vd1, base + TROWS * HD * 2);
+    glds4((unsigned)lane * 4, ((wu & 1) ? del_bh : lse2_bh) + qt * TROWS,
+          base + 2 * TROWS * HD * 2 + (unsigned)(wu & 1) * 256);
   };
-  auto store_tile = [&](int buf) {
-    bf16* T = smem + buf * 2 * TROWS * HD;
-    stage_store(sq, T, tid);
-    stage_store(sd, T + TROWS * HD, tid);
-    if (tid < 128) sstat[buf * 2 * TROWS + tid] = st_v * st_mul;
-  };
-  load_tile(qt0);
-  store_tile(0);
-  __syncthreads();
+  issue(qt0, 0);
+  if (qt0 + 1 < nqt) issue(qt0 + 1, 1);
+  int sl = 0;
 
   for (int qt = qt0; qt < nqt; ++qt) {
-    const int buf = (qt - qt0) & 1;
-    const bf16* Qt = smem + buf * 2 * TROWS * HD;
+    if (qt + 1 < nqt)
+      vm_wait<5>();  // this wave's pieces of tile qt have landed (qt + 1's 5 may still fly)
+    else
+      vm_wait<0>();
+    __syncthreads();  // ... and every other wave's; slot (sl + 2) % 3 is free again
+    if (qt + 2 < nqt) issue(qt + 2, sl == 0 ? 2 : sl - 1);
+    const bf16* Qt = smem + sl * SLOT;
     const bf16* Dt = Qt + TROWS * HD;
-    const float* L2 = sstat + buf * 2 * TROWS;
+    const float* L2 = reinterpret_cast<const float*>(Qt + 2 * TROWS * HD);
     const float* DL = L2 + TROWS;
-    const bool more = qt + 1 < nqt;
-    if (more) load_tile(qt + 1);
     const int q0 = qt * TROWS;
     if (q0 + TROWS - 1 >= wave_kmin) {
 #pragma unroll
@@ -448,9 +486,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
         }
       }
     }
-    if (more) store_tile(buf ^ 1);
-    __syncthreads();
+    sl = sl == 2 ? 0 : sl + 1;
   }
+  __syncthreads();  // the epilogue's column sums reuse the ring
   // dK = scale * dS^T Q ; dV = P^T dO.  dqkv row `key`, slot 1 (k) and 2 (v)
   bf16* krow = dqkv + (size_t)(b * S + key) * rs + (size_t)H * HD + (size_t)h * HD;
   bf16* vrow = krow + (size_t)H * HD;
@@ -477,7 +515,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
                                                        int H, float c2, float scale, float* __restrict__ dbias_part) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * 2 * TROWS * HD];  // ring of 3 × [K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   const int bh = blockIdx.x % (B * H);
@@ -512,7 +550,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
   }
   const float dq_delta = xhalf_sum(dpart);
-  if (hh == 0) delta[(size_t)bh * S + q] = dq_delta;
+  if (hh == 0) {
+    delta[(size_t)bh * S + q] = dq_delta;
+    delta[(size_t)B * H * S + (size_t)bh * S + q] = lq;  // lse·log2e for the dK/dV kernel's DMA
+  }
   retire(qf);
   retire(df);
   retire(lq);
@@ -521,20 +562,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
-  Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
-  stage_store(sk, smem, tid);
-  stage_store(sv, smem + TROWS * HD, tid);
-  __syncthreads();
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned vo0 = dma_voff(lane, rs, 0), vo1 = dma_voff(lane, rs, 1);
+  auto issue = [&](int t, int slot) {
+    const unsigned base = lds0 + (unsigned)(slot * 2 * TROWS * HD * 2);
+    dma_tile(kbase, rs, t * TROWS, wu, vo0, vo1, base);
+    dma_tile(vbase, rs, t * TROWS, wu, vo0, vo1, base + TROWS * HD * 2);
+  };
+  issue(0, 0);
+  if (ntiles > 1) issue(1, 1);
+  int sl = 0;
   for (int t = 0; t < ntiles; ++t) {
-    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
+    if (t + 1 < ntiles)
+      vm_wait<4>();
+    else
+      vm_wait<0>();
+    __syncthreads();
+    if (t + 2 < ntiles) issue(t + 2, sl == 0 ? 2 : sl - 1);
+    const bf16* Kt = smem + sl * 2 * TROWS * HD;
     const bf16* Vt = Kt + TROWS * HD;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
-      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
-    }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
@@ -569,17 +616,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
       }
     }
-    if (more) {
-      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-      stage_store(sk, Kn, tid);
-      stage_store(sv, Kn + TROWS * HD, tid);
-    }
-    __syncthreads();
+    sl = sl == 2 ? 0 : sl + 1;
   }
   bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
   store_acc_rows(qrow, a0, 0, hh, scale);
   store_acc_rows(qrow, a1, 32, hh, scale);
   if (dbias_part) {  // q slot of the QKV bias-gradient partial row b·(S/128) + qb
+    __syncthreads();  // the column sums reuse the ring
     float* prow = dbias_part + (size_t)(b * (S / 128) + qb) * (3 * H * HD) + (size_t)h * HD;
     float* red = reinterpret_cast<float*>(smem);
     colsum_acc(a0, 0, scale, red + w * 64, lane);

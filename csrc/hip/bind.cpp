@@ -491,7 +491,7 @@ std::vector<at::Tensor> attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, 
   TORCH_CHECK(dout.sizes() == o.sizes() && o.size(2) == C && lse.numel() == (int64_t)B * H * S);
   TORCH_CHECK(D == 64 && S % 128 == 0);
   auto dqkv = at::empty_like(qkv);
-  auto delta = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  auto delta = at::empty({2, B, H, S}, qkv.options().dtype(at::kFloat));  // delta | lse·log2e
   const int G = B * (S / 128), NC = 3 * C;
   at::Tensor part;
   if (with_bias_grad)
