@@ -222,8 +222,17 @@ int gemm_dw_get_impl() { return g_dw_impl; }
 // gemm_dw4: every split's k-tile count even and ≥ 4 (no remainder), ≤ 256
 // workgroups (one resident round, one workgroup per CU)
 static int dw4_splits(long long T, int M, int N) {
-  const int tiles = (M / BM) * (N / BN);
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const long long ks = T / BK;
+  if (tiles > 256) {
+    // several rounds of one workgroup per CU: the smallest split whose last round
+    // is nearly full (LM head, 788 tiles: 1 slice = 3.08 rounds in 4, 4 slices = 12.3 in 13)
+    for (int s = 1; s <= 8; ++s) {
+      if (ks % s || (ks / s) % 2 || ks / s < 4) continue;
+      const long long wg = (long long)tiles * s, rounds = (wg + 255) / 256;
+      if (wg * 100 >= rounds * 256 * 94) return s;
+    }
+  }
   for (int s = 16; s >= 1; --s) {
     if ((long long)tiles * s > 256 && s > 1) continue;
     if (ks % s == 0 && (ks / s) % 2 == 0 && ks / s >= 4) return s;
@@ -232,11 +241,12 @@ static int dw4_splits(long long T, int M, int N) {
 }
 
 int gemm_dw_splits(long long T, int M, int N) {
-  if (M % BM || N % BN || T % BK || T <= 0) return 0;
+  if (M % (BM / 2) || N % BN || T % BK || T <= 0) return 0;
   if (g_dw_impl >= 1) {
     const int s = dw4_splits(T, M, N);
     if (s) return s;
   }
+  if (M % BM) return 0;  // the half-height edge tile is gemm_dw4's only
   // one resident round of ≤ 256 workgroups (one per CU), as many as fit:
   // measured, 240 WGs in one round beat 768 in three (per-WG prologue, fold)
   const int tiles = (M / BM) * (N / BN);
@@ -249,13 +259,14 @@ int gemm_dw_splits(long long T, int M, int N) {
 
 int gemm_dw(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
             int accumulate, bf16* ws, int splits, hipStream_t st) {
-  if (M % BM || N % BN || T % BK || splits < 1 || splits > 16) return -2;
+  if (M % (BM / 2) || N % BN || T % BK || splits < 1 || splits > 16) return -2;
   const long long ks = T / BK;
   if (ks < splits || ks > 0x7fffffffLL) return -2;
   if (g_dw_impl >= 1) {
     const int rc = gemm_dw4(A, B, T, M, N, lda, ldb, C, ldc, accumulate, ws, splits, st, g_dw_impl - 1);
     if (rc != -2) return rc;  // -2: this split count breaks its contract → the 8-wave loop
   }
+  if (M % BM) return -2;
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles * splits;
   if (splits == 1) {

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int tiles_n = N / BN, tiles_m = M / BM;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;  // M % 256 == 128: a half-height last row of tiles
   const int nwg = tiles_m * tiles_n * splits;
   int id = blockIdx.x;
   {  // bijective XCD remap (gemm_dw.hip)
@@ -88,7 +88,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
   // (k-tile, piece) in SGPRs.
   const int rl = lane >> 5;
   const int cs = (lane & 31) ^ (((2 * w + rl) & 3) << 2);
-  const unsigned voffA = (unsigned)((rl * lda + cs * 8) * 2), voffB = (unsigned)((rl * ldb + cs * 8) * 2);
+  // half-height edge tile (columns m0 + 128 .. m0 + 255 of A do not exist): those
+  // lanes re-fetch columns m0 .. m0 + 127 — in bounds, and the rows they feed are
+  // never stored
+  const int csa = (m0 + BM > M && cs >= 16) ? cs - 16 : cs;
+  const unsigned voffA = (unsigned)((rl * lda + csa * 8) * 2), voffB = (unsigned)((rl * ldb + cs * 8) * 2);
   const bf16* baseA = A + ((size_t)k0 * BK + 2 * w) * lda + m0;
   const bf16* baseB = B + ((size_t)k0 * BK + 2 * w) * ldb + n0;
   const unsigned stepAb = (unsigned)(16 * lda), stepBb = (unsigned)(16 * ldb);  // 8 rows, bytes
@@ -240,6 +244,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m >= M) continue;  // edge tile: wave-uniform (wm = 1 holds rows m0 + 128 ..)
         const int n = n0 + wn * 128 + 32 * nb + li;
         bf16* p = Cb + (size_t)m * ldc + n;
         float x = v[r];
@@ -255,13 +260,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
 // long enough; returns -2 when a slice would not be
 int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
              int accumulate, bf16* ws, int splits, hipStream_t st, int variant) {
-  if (M % BM || N % BN || T % BK || splits < 1 || splits > 16) return -2;
+  if (M % (BM / 2) || N % BN || T % BK || splits < 1 || splits > 16) return -2;
   const long long ks = T / BK;
   if (ks > 0x7fffffffLL) return -2;
   // every split's k-tile count even and ≥ 4
   const long long kq = ks / splits, kr = ks % splits;
   if (kq < 4 || kq % 2 || kr) return -2;
-  const int tiles = (M / BM) * (N / BN);
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const int grid = tiles * splits;
   bf16* out = C;
   int ldo = ldc;

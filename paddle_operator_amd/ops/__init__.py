@@ -257,6 +257,15 @@ def _weight_grad(w, dy2, x2):
     stalled one run on cross-stream allocator reuse; they stay in-stream.)"""
     Fo, K = dy2.shape[1], x2.shape[1]
     if not _direct_ok(w):
+        # a gradient tensor for autograd to accumulate (the tied LM head / embedding
+        # weight): HIP dW GEMM where its shape contract holds (incl. the 50304-row
+        # vocabulary's half-height tile row: 5.42 vs 6.41 ms alone, tools/lm_dw_probe.py;
+        # in the step 159.08 / 159.20 vs 159.24 / 159.44 ms, tools/gpu_so_ab.sh)
+        if (_HIP_DW[0] and dy2.is_cuda and dy2.dtype == torch.bfloat16 and dy2.is_contiguous()
+                and x2.is_contiguous()):
+            g = torch.empty(Fo, K, device=dy2.device, dtype=dy2.dtype)
+            if _native.require_hip().gemm_dw(dy2, x2, g, False):
+                return g
         s = _splitk(dy2.shape[0], Fo, K) if use_hip(dy2) else 1
         if s == 1:
             return dy2.t() @ x2

@@ -188,11 +188,11 @@ def test_gemm_dw_rejects_unsupported_shape(cuda):
     assert not m.gemm_dw(dy, x, torch.zeros(256, 256, device=cuda).bfloat16(), True)
 
 
-def test_linear_splitk_nondirect_weight_grad(cuda):
-    """Wide dW (≥256 tiles, K ≥ 32768) outside the arena: split-K into a fresh tensor."""
+@pytest.mark.parametrize("T,Fo,K", [(32768, 4096, 4096), (8192, 640, 512)])
+def test_linear_splitk_nondirect_weight_grad(cuda, T, Fo, K):
+    """dW outside the arena (a fresh tensor for autograd, as for the tied LM head):
+    gemm_dw (incl. a half-height last tile row) or split-K hipBLASLt."""
     from paddle_operator_amd import ops
-    T, Fo, K = 32768, 4096, 4096
-    assert ops._splitk(T, Fo, K) == 4
     g = torch.Generator(device=cuda).manual_seed(12)
     w = (0.02 * torch.randn(Fo, K, device=cuda, generator=g)).bfloat16().requires_grad_()
     x = torch.randn(T, K, device=cuda, generator=g).bfloat16()
@@ -553,6 +553,32 @@ def test_maxpool3s2_nhwc(cuda, N, C, H, W):
     y.backward(dy)
     yf.backward(dy.float())
     assert rel_err(x.grad, xf.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T,M,N,acc,splits", [(8192, 384, 512, True, 0), (8192, 384, 512, False, 1),
+                                              (16384, 2944, 256, True, 0), (4096, 640, 768, True, 2)])
+def test_gemm_dw4_half_height_edge(cuda, T, M, N, acc, splits):
+    """M % 256 == 128 (the LM head's 50304-row vocabulary): gemm_dw4's half-height last
+    tile row — its missing A columns re-fetched in bounds, its rows never stored."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    g = torch.Generator(device=cuda).manual_seed(23)
+    dy = torch.empty(T, M, device=cuda).uniform_(-1, 1, generator=g).bfloat16()
+    x = torch.empty(T, N, device=cuda).uniform_(-1, 1, generator=g).bfloat16()
+    base = torch.empty(M, N, device=cuda).uniform_(-4, 4, generator=g).bfloat16() if acc else \
+        torch.zeros(M, N, device=cuda).bfloat16()
+    ref = base.float() + dy.float().t() @ x.float()
+    prev = m.gemm_dw_impl(-1)
+    try:
+        for impl in (1, 2):
+            m.gemm_dw_impl(impl)
+            out = base.clone()
+            assert m.gemm_dw(dy, x, out, True, splits)
+            assert rel_err(out, ref) < 1e-2, (impl, splits, m.gemm_dw_splits(T, M, N))
+        m.gemm_dw_impl(0)  # the 8-wave loop has no edge tile: unsupported, never wrong
+        assert not m.gemm_dw(dy, x, base.clone(), True) or M % 256 == 0
+    finally:
+        m.gemm_dw_impl(prev)
 
 
 @pytest.mark.parametrize("T,M,N,acc", [(8192, 4096, 4096, True), (65536, 1024, 3072, False), (16384, 512, 768, True)])

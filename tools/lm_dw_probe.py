@@ -9,7 +9,9 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.gemm_probe import bench  # noqa: E402
 from paddle_operator_amd import _native  # noqa: E402
 
@@ -29,9 +31,10 @@ for V in (50304, 50432):
         m.splitk_add(part, g, True)
 
     out[f"lib_split4_V{V}"] = bench(lib, iters=5, warm=2)
-    if V % 256 == 0:
+    if V % 128 == 0:
         ref = (dy.float().t() @ x.float())
-        for sp in (1, 2, 3, 4, 8):
+        out[f"gemm_dw_auto_splits_V{V}"] = m.gemm_dw_splits(T, V, C)
+        for sp in (0, 1, 2, 4, 8):
             g.zero_()
             assert m.gemm_dw(dy, x, g, False, sp)
             err = ((g.float() - ref).abs().max() / ref.abs().max()).item()
@@ -44,6 +47,8 @@ res = {}
 for k, v in out.items():
     if k.endswith("relerr"):
         res[k] = round(v, 5)
+    elif "auto" in k:
+        res[k] = v
     else:
         V = int(k.rsplit("V", 1)[1])
         res[k] = (round(v, 1), round(2 * T * V * C / (v * 1e-6) / 1e12))
