@@ -40,6 +40,10 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int HD = 64;     // head dim
 constexpr int TROWS = 64;  // rows per LDS tile
+#ifndef PDO_FWD_SLOTS
+#define PDO_FWD_SLOTS 2
+#endif
+constexpr int FWD_SLOTS = PDO_FWD_SLOTS;  // forward K/V ring depth (2 or 3)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -104,27 +108,6 @@ __device__ __forceinline__ void retire(const bf16x8 (&v)[N]) {
   for (int i = 0; i < N; ++i) asm volatile("" ::"v"(v[i]));
 }
 __device__ __forceinline__ void retire(float x) { asm volatile("" ::"v"(x)); }
-
-// ----- global → register → LDS staging of a [64 rows][64] tile (256 threads) -----
-struct Stage {
-  bf16x8 v[2];
-};
-
-__device__ __forceinline__ void stage_load(Stage& st, const bf16* base, size_t row_stride, int row0, int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    st.v[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(row0 + r) * row_stride + ch * 8);
-  }
-}
-
-__device__ __forceinline__ void stage_store(const Stage& st, bf16* T, int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *reinterpret_cast<bf16x8*>(T + toff(r, ch)) = st.v[i];
-  }
-}
 
 // ----- global → LDS by LDS-DMA: no register staging, no ds_write -----
 // A [64 rows][64] bf16 tile in the toff() image is 8 pieces of 8 rows; a piece
@@ -234,14 +217,6 @@ __device__ __forceinline__ void colsum_finish(const float* red, float* const (&o
 // per-tile address arithmetic.  K keeps the row-read swizzle (toff).
 __device__ __forceinline__ int toff_v(int r, int ch) { return r * HD + ((ch ^ (((r >> 1) & 1) << 2)) << 3); }
 
-__device__ __forceinline__ void stage_store_v(const Stage& st, bf16* T, int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    *reinterpret_cast<bf16x8*>(T + toff_v(r, ch)) = st.v[i];
-  }
-}
-
 // per-lane element offset of the tr fragment rows k0 = 0 (lo) for V columns cbase
 __device__ __forceinline__ int tr_base_v(int cbase, int lane) {
   const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
@@ -259,7 +234,7 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
 
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int B, int S, int H, float c2) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
+  __shared__ __attribute__((aligned(16))) bf16 smem[FWD_SLOTS * 2 * TROWS * HD];  // ring of [K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   const int bh = blockIdx.x % (B * H);
@@ -282,21 +257,31 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
-  Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
-  stage_store(sk, smem, tid);
-  stage_store_v(sv, smem + TROWS * HD, tid);
-  __syncthreads();
-
+  // K / V tiles by LDS-DMA into a 3-slot ring (dma_tile); V uses its own
+  // transposed-read swizzle (toff_v: chunk ^ 4·bit1(row), one per-lane offset)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned vk0 = dma_voff(lane, rs, 0), vk1 = dma_voff(lane, rs, 1);
+  const unsigned vv = (unsigned)(((size_t)(lane >> 3) * rs + (size_t)(((lane & 7) ^ ((((lane >> 3) >> 1) & 1) << 2)) << 3)) * 2);
+  auto issue = [&](int t, int slot) {
+    const unsigned base = lds0 + (unsigned)(slot * 2 * TROWS * HD * 2);
+    dma_tile(kbase, rs, t * TROWS, wu, vk0, vk1, base);
+    dma_tile(vbase, rs, t * TROWS, wu, vv, vv, base + TROWS * HD * 2);
+  };
+  // FWD_SLOTS = 2: 32 KiB, 126 VGPRs → 4 workgroups (waves/SIMD) per CU, tile t+1's
+  // DMA issued after tile t's barrier; 3: tile t+2 in flight too, 3 per CU
+  issue(0, 0);
+  if (FWD_SLOTS == 3 && ntiles > 1) issue(1, 1);
+  int sl = 0;
   for (int t = 0; t < ntiles; ++t) {
-    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
+    if (FWD_SLOTS == 3 && t + 1 < ntiles)
+      vm_wait<4>();
+    else
+      vm_wait<0>();
+    __syncthreads();
+    if (t + FWD_SLOTS - 1 < ntiles) issue(t + FWD_SLOTS - 1, sl == 0 ? FWD_SLOTS - 1 : sl - 1);
+    const bf16* Kt = smem + sl * 2 * TROWS * HD;
     const bf16* Vt = Kt + TROWS * HD;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
-      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
-    }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       f32x16 s0 = zero16(), s1 = zero16();
@@ -356,12 +341,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         o1 = mfma(tr_frag_v<48>(V1), p1, o1);
       }
     }
-    if (more) {
-      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-      stage_store(sk, Kn, tid);
-      stage_store_v(sv, Kn + TROWS * HD, tid);
-    }
-    __syncthreads();
+    sl = sl == FWD_SLOTS - 1 ? 0 : sl + 1;
   }
   const float lt = xhalf_sum(l);
   const float inv = 1.f / lt;
