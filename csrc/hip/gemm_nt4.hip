@@ -98,7 +98,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   };
   auto srcs = [&](int kt) {
     Src r;
-    if constexpr (BUFLD) {
+    if constexpr (BUFLD & 1) {
       r = Src{reinterpret_cast<const char*>((uintptr_t)(kt * BK * 2)), nullptr, stepAb, stepBb};
     } else {
       r = Src{reinterpret_cast<const char*>(baseA + (size_t)kt * BK), reinterpret_cast<const char*>(baseB + (size_t)kt * BK),
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   auto dma = [&](const Src& sr, auto buf_tag, int p) {
     constexpr int BUF = decltype(buf_tag)::value;
     const unsigned base = lds0 + (unsigned)(BUF * 2 * OPB);
-    if constexpr (BUFLD) {
+    if constexpr (BUFLD & 1) {
       // sr.a / sr.b carry the k-tile byte offset in this mode
       const unsigned ko = (unsigned)(uintptr_t)sr.a;
       if (p < 8) bld(voffA, rsA, ko + p * sr.sa, base + (unsigned)(4096 * p));
@@ -207,9 +207,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     for (int g = 0; g < 16; ++g) {
       const int i = g >> 1, j0 = 4 * (g & 1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if constexpr (FIRST) mma0(acc[i][j0 + j], fb0[j0 + j], fa0[i]);
-        else mma(acc[i][j0 + j], fb0[j0 + j], fa0[i]);
+      for (int j = 0; j < 4; ++j) {
+        // BUFLD & 2: B-stationary order (the group's 4 MFMAs share SrcA, as hipBLASLt's loop does)
+        const int ii = (BUFLD & 2) ? 4 * (g & 1) + j : i, jj = (BUFLD & 2) ? (g >> 1) : j0 + j;
+        if constexpr (FIRST) mma0(acc[ii][jj], fb0[jj], fa0[ii]);
+        else mma(acc[ii][jj], fb0[jj], fa0[ii]);
+      }
       const bf16x8 v = rd(buf_tag, 1, g);
       if (g == 0) fa1[0] = v;
       else if (g <= 8) fb1[g - 1] = v;
@@ -224,8 +227,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     for (int g = 0; g < 16; ++g) {
       const int i = g >> 1, j0 = 4 * (g & 1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        mma(acc[i][j0 + j], fb1[j0 + j], fa1[i]);
+      for (int j = 0; j < 4; ++j) {
+        const int ii = (BUFLD & 2) ? 4 * (g & 1) + j : i, jj = (BUFLD & 2) ? (g >> 1) : j0 + j;
+        mma(acc[ii][jj], fb1[jj], fa1[ii]);
+      }
       if constexpr (MORE) {
         if (g == BAR) {
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -366,12 +371,15 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   using I11 = std::integral_constant<int, 11>;
   using I13 = std::integral_constant<int, 13>;
   // schedule variants under A/B (tools/nt4_probe.py, profiles/r2_gemm_nt4.md):
-  // 0 = barrier after block-1 group 11, the first 4 DMA pieces of tile t+2 after it, the rest one per block-0 group (default)
+  // 0 = barrier after block-1 group 11, the first 4 DMA pieces of tile t+2 after it, the rest one per
+  // block-0 group, B-stationary MFMA order (each group's 4 MFMAs share SrcA; default: 1-4 % faster
+  // than the A-stationary order of variant 4 on qkv_fwd / proj_dx, bit-identical)
   switch (variant) {
     case 1: return launch(I1{}, I7{}, I0{});
     case 2: return launch(I2{}, I7{}, I0{});   // every piece of tile t+2 right after tile t's barrier
     case 3: return launch(I4{}, I11{}, I0{});  // the same, 4 per group after a later barrier
-    default: return launch(I1{}, I11{}, I0{});
+    case 4: return launch(I1{}, I11{}, I0{});  // variant 0 with the A-stationary order
+    default: return launch(I1{}, I11{}, I2{});
   }
   return 0;
 }
