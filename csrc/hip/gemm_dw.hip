@@ -219,8 +219,8 @@ static int g_dw_impl = 2;  // 4-wave mainloop (gemm_dw4.hip) variant 1 (barrier 
 void gemm_dw_set_impl(int impl) { g_dw_impl = impl; }
 int gemm_dw_get_impl() { return g_dw_impl; }
 
-// gemm_dw4: every split's k-tile count even and ≥ 4 (no remainder), ≤ 256
-// workgroups (one resident round, one workgroup per CU)
+// gemm_dw4: k-tiles dealt to the slices in pairs, ≥ 2 pairs per slice; ≤ 256
+// workgroups (one resident round, one workgroup per CU) unless the tiles alone exceed it
 static int dw4_splits(long long T, int M, int N) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const long long ks = T / BK;
@@ -228,14 +228,16 @@ static int dw4_splits(long long T, int M, int N) {
     // several rounds of one workgroup per CU: the smallest split whose last round
     // is nearly full (LM head, 788 tiles: 1 slice = 3.08 rounds in 4, 4 slices = 12.3 in 13)
     for (int s = 1; s <= 8; ++s) {
-      if (ks % s || (ks / s) % 2 || ks / s < 4) continue;
+      if (ks % 2 || (ks / 2) / s < 2) continue;
       const long long wg = (long long)tiles * s, rounds = (wg + 255) / 256;
       if (wg * 100 >= rounds * 256 * 94) return s;
     }
   }
+  // the most slices that keep one resident round (≤ 256 workgroups): qkv's 48 tiles
+  // take 5 uneven slices (240 workgroups) instead of 4 even ones (192)
   for (int s = 16; s >= 1; --s) {
     if ((long long)tiles * s > 256 && s > 1) continue;
-    if (ks % s == 0 && (ks / s) % 2 == 0 && ks / s >= 4) return s;
+    if (ks % 2 == 0 && (ks / 2) / s >= 2) return s;
   }
   return 0;
 }

@@ -76,9 +76,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
   const int tn = id % tiles_n;
   const int tm = (id / tiles_n) % tiles_m;
   const int split = id / (tiles_n * tiles_m);
-  const int kq = ksteps_total / splits, kr = ksteps_total % splits;
-  const int k0 = split * kq + min(split, kr);
-  const int nk = kq + (split < kr ? 1 : 0);
+  // k-tiles are dealt to the splits in pairs (the mainloop runs tiles in pairs):
+  // the first P % splits slices take one pair more
+  const int pq = (ksteps_total >> 1) / splits, pr = (ksteps_total >> 1) % splits;
+  const int k0 = 2 * (split * pq + min(split, pr));
+  const int nk = 2 * (pq + (split < pr ? 1 : 0));
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- LDS-DMA: a wave-instruction fills 1 KiB = 2 token rows of 512 B.  Wave
@@ -256,16 +258,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
 
 }  // namespace
 
-// nk per split must be even and ≥ 4: the caller's split count keeps every slice
-// long enough; returns -2 when a slice would not be
+// every slice gets ≥ 2 pairs of k-tiles (uneven splits allowed: pairs are dealt
+// out); returns -2 when a slice would be shorter
 int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, int ldb, bf16* C, int ldc,
              int accumulate, bf16* ws, int splits, hipStream_t st, int variant) {
   if (M % (BM / 2) || N % BN || T % BK || splits < 1 || splits > 16) return -2;
   const long long ks = T / BK;
   if (ks > 0x7fffffffLL) return -2;
-  // every split's k-tile count even and ≥ 4
-  const long long kq = ks / splits, kr = ks % splits;
-  if (kq < 4 || kq % 2 || kr) return -2;
+  // every split's k-tile count even and ≥ 4 (pairs dealt out, remainder to the first slices)
+  if (ks % 2 || (ks / 2) / splits < 2) return -2;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const int grid = tiles * splits;
   bf16* out = C;

@@ -581,7 +581,8 @@ def test_gemm_dw4_half_height_edge(cuda, T, M, N, acc, splits):
         m.gemm_dw_impl(prev)
 
 
-@pytest.mark.parametrize("T,M,N,acc", [(8192, 4096, 4096, True), (65536, 1024, 3072, False), (16384, 512, 768, True)])
+@pytest.mark.parametrize("T,M,N,acc", [(8192, 4096, 4096, True), (65536, 1024, 3072, False), (16384, 512, 768, True),
+                                       (16384, 3072, 1024, True)])  # last: 48 tiles → 5 uneven slices
 def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
     """The 4-wave dW mainloop (gemm_dw4.hip, both schedule variants; split-K or
     in-kernel accumulate at one split) and the 8-wave one against fp32."""
