@@ -287,6 +287,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   // acc[i][j][e] = C[m][n], m = wm·128 + 16i + (l&15), n = wn·128 + 16j + 4(l>>4) + e.
   // Staged through LDS as bf16 [256][256] (chunk c of row m at c ^ (m & 31))
   // and written back as whole 512-B rows, 16 B per lane.
+  // row phase: thread t owns 16-B column chunk t & 31 of rows 8·it + (t >> 5)
+  const int c = tid & 31, r0 = tid >> 5;
+  const int n = n0 + 8 * c;
+  // dGELU: the tile's pre-activation rows (512 B per lane) are loaded before the
+  // accumulator staging, into the registers the mainloop's fragments used — their
+  // HBM latency hides behind the staging instead of stalling every row batch
+  bf16x8 pre[EPI == 3 ? 32 : 1];
+  if constexpr (EPI == 3) {
+#pragma unroll
+    for (int it = 0; it < 32; ++it) pre[it] = *reinterpret_cast<const bf16x8*>(Y + (size_t)(m0 + 8 * it + r0) * ldy + n);
+  }
   __syncthreads();
   unsigned char* st = reinterpret_cast<unsigned char*>(smem);
 #pragma unroll
@@ -306,13 +317,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     }
   }
   __syncthreads();
-  // row phase: thread t owns 16-B column chunk t & 31 of rows 8·it + (t >> 5)
-  const int c = tid & 31, r0 = tid >> 5;
-  const int n = n0 + 8 * c;
   f32x8 bv8;
   if constexpr (EPI >= 2) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
   f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+#pragma unroll
   for (int it = 0; it < 32; ++it) {
     const int r = 8 * it + r0;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * 512 + ((c ^ (r & 31)) << 4));
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
       *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
     } else {
-      const f32x8 x = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n)) + bv8;
+      const f32x8 x = to_f32(pre[it]) + bv8;
       const f32x8 dy = to_f32(v);
       f32x8 d;
 #pragma unroll
