@@ -215,7 +215,7 @@ __global__ __launch_bounds__(NTHR) void gemm_dw_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
-static int g_dw_impl = 2;  // 4-wave mainloop (gemm_dw4.hip) variant 1 (barrier after group 7), where its contract holds
+static int g_dw_impl = 3;  // 4-wave mainloop (gemm_dw4.hip) variant 2 (half-buffer refill, two barriers per tile), where its contract holds
 void gemm_dw_set_impl(int impl) { g_dw_impl = impl; }
 int gemm_dw_get_impl() { return g_dw_impl; }
 

@@ -156,6 +156,89 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
   f32x16 acc[4][4];  // first written by mma0 in tile 0's block 0
   bf16x8 f0[16], f1[16];
 
+  if constexpr (BAR < 0) {
+    // ---- half-buffer refill schedule (BAR < 0): each 32-token half of a buffer is
+    // refilled as soon as every wave has read it — tile t+2's first half during
+    // block 0 of tile t (after barrier B0: F0(t) reads done), its second half during
+    // block 1 (after B1: F1(t) reads done).  Tile t+1's data therefore has ≈1.5 tiles
+    // of lead (issued during tile t-1, first read after B1 of tile t) instead of ≈0.5,
+    // at the price of two barriers per tile (hipBLASLt's gfx950 loop does the same
+    // with three).  Pieces: first half = A 0-3, B 8-11; second half = A 4-7, B 12-15.
+    {
+      const Src s0 = srcs(0), s1 = srcs(1);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) dma(s1, B1{}, p);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (tile 1 may fly)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) f0[q] = rd(B0{}, 0, q);
+    auto tileH = [&](int t, auto buf_tag, auto more_tag, auto first_tag, auto eout_tag) {
+      constexpr int BUF = decltype(buf_tag)::value;
+      constexpr bool MORE = decltype(more_tag)::value;
+      constexpr bool FIRST = decltype(first_tag)::value;
+      constexpr bool EOUT = decltype(eout_tag)::value;
+      using NB = std::integral_constant<int, BUF ^ 1>;
+      using SB = std::integral_constant<int, BUF>;
+      Src sn2{};
+      if constexpr (EOUT) sn2 = srcs(t + 2);
+      // B0: every wave's F0(t) reads (buffer BUF, tokens 0-31) are done
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int ks = g >> 3, mb = (g >> 1) & 3, nb0 = 2 * (g & 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (FIRST && ks == 0) mma0(acc[mb][nb0 + u], f0[8 * ks + mb], f0[8 * ks + 4 + nb0 + u]);
+          else mma(acc[mb][nb0 + u], f0[8 * ks + mb], f0[8 * ks + 4 + nb0 + u]);
+        }
+        f1[g] = rd(buf_tag, 1, g);
+        if constexpr (EOUT) {
+          if (g & 1) dma(sn2, SB{}, (g >> 1) < 4 ? (g >> 1) : (g >> 1) + 4);  // first-half pieces
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // B1: every wave's F1(t) reads are done (tokens 32-63 of BUF free) and tile t+1
+      // has landed (only tile t+2's first-half pieces may still fly)
+      if constexpr (MORE || EOUT) {
+        if constexpr (EOUT)
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int ks = g >> 3, mb = (g >> 1) & 3, nb0 = 2 * (g & 1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) mma(acc[mb][nb0 + u], f1[8 * ks + mb], f1[8 * ks + 4 + nb0 + u]);
+        if constexpr (MORE) f0[g] = rd(NB{}, 0, g);
+        if constexpr (EOUT) {
+          if (g & 1) dma(sn2, SB{}, (g >> 1) < 4 ? (g >> 1) + 4 : (g >> 1) + 8);  // second-half pieces
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    tileH(0, B0{}, T_{}, T_{}, T_{});
+    tileH(1, B1{}, T_{}, F_{}, T_{});
+    for (int t = 2; t < nk - 2; t += 2) {
+      tileH(t, B0{}, T_{}, F_{}, T_{});
+      tileH(t + 1, B1{}, T_{}, F_{}, T_{});
+    }
+    tileH(nk - 2, B0{}, T_{}, F_{}, F_{});
+    tileH(nk - 1, B1{}, F_{}, F_{}, F_{});
+  } else {
   {
     const Src s0 = srcs(0);
 #pragma unroll
@@ -229,6 +312,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
   }
   tile(nk - 2, B0{}, T_{}, F_{}, T_{}, F_{});
   tile(nk - 1, B1{}, F_{}, F_{}, F_{}, F_{});
+  }
 
   // ---- epilogue: acc[mb][nb][r] = C[m0 + wm·128 + 32mb + (r&3) + 8(r>>2) + 4hh][n0 + wn·128 + 32nb + (l&31)]
   // the accumulators leave through explicit v_accvgpr_read, padded against the
@@ -282,6 +366,8 @@ int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, i
   }
   if (variant == 1)
     gemm_dw4_kernel<7><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+  else if (variant == 2)  // half-buffer refill schedule (two barriers per tile, ≈1.5 tiles of DMA lead)
+    gemm_dw4_kernel<-1><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   else
     gemm_dw4_kernel<11><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   if (splits > 1) return splitk_add(ws, splits, (long long)M * N, C, accumulate, st);
