@@ -14,11 +14,19 @@
 // Backward: two kernels without atomics.
 //   dK/dV: workgroup = 128 keys (32 per wave, key on the lane), S and dP are
 //     computed as [q × key] so P and dS are the B operands of dV^T = dO^T·P
-//     and dK^T = Q^T·dS; Q / dO tiles stream through LDS.
+//     and dK^T = Q^T·dS; Q / dO / lse / delta tiles reach LDS by LDS-DMA
+//     through a 3-slot ring (no register staging: 196 instead of 222 VGPRs).
 //   dQ:   workgroup = 128 queries, S^T / dP^T with the query on the lane,
-//     dQ^T = K^T·dS^T; K / V tiles stream through LDS.  Runs first and also
-//     writes delta = rowsum(dO ∘ O) (its dO fragments are already in
-//     registers), which dK/dV then reads: no separate delta pass.
+//     dQ^T = K^T·dS^T; K / V tiles stream through LDS (register-staged).  Runs
+//     first and also writes delta = rowsum(dO ∘ O) (its dO fragments are
+//     already in registers) and lse·log2e, which dK/dV then DMAs: no
+//     separate delta pass.
+// Staging choice per kernel measured in the training step (tools/gpu_so_prof.sh:
+// rocprofv3 per-kernel times of extension variants in one session): LDS-DMA
+// wins for dK/dV (427.7 vs 448.0 µs) but not for the forward (DMA 2-slot ring at
+// 4 waves/SIMD 278.5 µs, 3-slot 275.6, register staging 267.4 — although the
+// microbenchmark on random inputs ranked them the other way) nor for dQ
+// (365.6 vs 358.6 µs; 373.0 vs 369.9 on a second box).
 // LDS tiles are [64 rows][64 bf16] with one XOR swizzle of the 16-B chunk
 // index, chosen so BOTH the row reads (ds_read_b128, 16 rows per lane group)
 // and the transposed reads (4 rows × 64 B per half-wave) are conflict-free.
@@ -40,10 +48,6 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int HD = 64;     // head dim
 constexpr int TROWS = 64;  // rows per LDS tile
-#ifndef PDO_FWD_SLOTS
-#define PDO_FWD_SLOTS 2
-#endif
-constexpr int FWD_SLOTS = PDO_FWD_SLOTS;  // forward K/V ring depth (2 or 3)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -108,6 +112,27 @@ __device__ __forceinline__ void retire(const bf16x8 (&v)[N]) {
   for (int i = 0; i < N; ++i) asm volatile("" ::"v"(v[i]));
 }
 __device__ __forceinline__ void retire(float x) { asm volatile("" ::"v"(x)); }
+
+// ----- global → register → LDS staging of a [64 rows][64] tile (256 threads) -----
+struct Stage {
+  bf16x8 v[2];
+};
+
+__device__ __forceinline__ void stage_load(Stage& st, const bf16* base, size_t row_stride, int row0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    st.v[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(row0 + r) * row_stride + ch * 8);
+  }
+}
+
+__device__ __forceinline__ void stage_store(const Stage& st, bf16* T, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *reinterpret_cast<bf16x8*>(T + toff(r, ch)) = st.v[i];
+  }
+}
 
 // ----- global → LDS by LDS-DMA: no register staging, no ds_write -----
 // A [64 rows][64] bf16 tile in the toff() image is 8 pieces of 8 rows; a piece
@@ -217,6 +242,14 @@ __device__ __forceinline__ void colsum_finish(const float* red, float* const (&o
 // per-tile address arithmetic.  K keeps the row-read swizzle (toff).
 __device__ __forceinline__ int toff_v(int r, int ch) { return r * HD + ((ch ^ (((r >> 1) & 1) << 2)) << 3); }
 
+__device__ __forceinline__ void stage_store_v(const Stage& st, bf16* T, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    *reinterpret_cast<bf16x8*>(T + toff_v(r, ch)) = st.v[i];
+  }
+}
+
 // per-lane element offset of the tr fragment rows k0 = 0 (lo) for V columns cbase
 __device__ __forceinline__ int tr_base_v(int cbase, int lane) {
   const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
@@ -234,7 +267,7 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
 
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int B, int S, int H, float c2) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[FWD_SLOTS * 2 * TROWS * HD];  // ring of [K|V][64][64]
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   const int bh = blockIdx.x % (B * H);
@@ -257,31 +290,21 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
-  // K / V tiles by LDS-DMA into a 3-slot ring (dma_tile); V uses its own
-  // transposed-read swizzle (toff_v: chunk ^ 4·bit1(row), one per-lane offset)
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const unsigned lds0 = lds_addr(smem);
-  const unsigned vk0 = dma_voff(lane, rs, 0), vk1 = dma_voff(lane, rs, 1);
-  const unsigned vv = (unsigned)(((size_t)(lane >> 3) * rs + (size_t)(((lane & 7) ^ ((((lane >> 3) >> 1) & 1) << 2)) << 3)) * 2);
-  auto issue = [&](int t, int slot) {
-    const unsigned base = lds0 + (unsigned)(slot * 2 * TROWS * HD * 2);
-    dma_tile(kbase, rs, t * TROWS, wu, vk0, vk1, base);
-    dma_tile(vbase, rs, t * TROWS, wu, vv, vv, base + TROWS * HD * 2);
-  };
-  // FWD_SLOTS = 2: 32 KiB, 126 VGPRs → 4 workgroups (waves/SIMD) per CU, tile t+1's
-  // DMA issued after tile t's barrier; 3: tile t+2 in flight too, 3 per CU
-  issue(0, 0);
-  if (FWD_SLOTS == 3 && ntiles > 1) issue(1, 1);
-  int sl = 0;
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store_v(sv, smem + TROWS * HD, tid);
+  __syncthreads();
+
   for (int t = 0; t < ntiles; ++t) {
-    if (FWD_SLOTS == 3 && t + 1 < ntiles)
-      vm_wait<4>();
-    else
-      vm_wait<0>();
-    __syncthreads();
-    if (t + FWD_SLOTS - 1 < ntiles) issue(t + FWD_SLOTS - 1, sl == 0 ? FWD_SLOTS - 1 : sl - 1);
-    const bf16* Kt = smem + sl * 2 * TROWS * HD;
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
     const bf16* Vt = Kt + TROWS * HD;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       f32x16 s0 = zero16(), s1 = zero16();
@@ -341,7 +364,12 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         o1 = mfma(tr_frag_v<48>(V1), p1, o1);
       }
     }
-    sl = sl == FWD_SLOTS - 1 ? 0 : sl + 1;
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store_v(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
   }
   const float lt = xhalf_sum(l);
   const float inv = 1.f / lt;
@@ -495,7 +523,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
                                                        int H, float c2, float scale, float* __restrict__ dbias_part) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * 2 * TROWS * HD];  // ring of 3 × [K|V][64][64]
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   const int bh = blockIdx.x % (B * H);
@@ -542,26 +570,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const unsigned lds0 = lds_addr(smem);
-  const unsigned vo0 = dma_voff(lane, rs, 0), vo1 = dma_voff(lane, rs, 1);
-  auto issue = [&](int t, int slot) {
-    const unsigned base = lds0 + (unsigned)(slot * 2 * TROWS * HD * 2);
-    dma_tile(kbase, rs, t * TROWS, wu, vo0, vo1, base);
-    dma_tile(vbase, rs, t * TROWS, wu, vo0, vo1, base + TROWS * HD * 2);
-  };
-  issue(0, 0);
-  if (ntiles > 1) issue(1, 1);
-  int sl = 0;
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store(sv, smem + TROWS * HD, tid);
+  __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles)
-      vm_wait<4>();
-    else
-      vm_wait<0>();
-    __syncthreads();
-    if (t + 2 < ntiles) issue(t + 2, sl == 0 ? 2 : sl - 1);
-    const bf16* Kt = smem + sl * 2 * TROWS * HD;
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
     const bf16* Vt = Kt + TROWS * HD;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
@@ -596,13 +618,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
       }
     }
-    sl = sl == 2 ? 0 : sl + 1;
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
   }
   bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
   store_acc_rows(qrow, a0, 0, hh, scale);
   store_acc_rows(qrow, a1, 32, hh, scale);
   if (dbias_part) {  // q slot of the QKV bias-gradient partial row b·(S/128) + qb
-    __syncthreads();  // the column sums reuse the ring
     float* prow = dbias_part + (size_t)(b * (S / 128) + qb) * (3 * H * HD) + (size_t)h * HD;
     float* red = reinterpret_cast<float*>(smem);
     colsum_acc(a0, 0, scale, red + w * 64, lane);
