@@ -99,6 +99,36 @@ __device__ __forceinline__ float gelu_sig_grad(float x) {
   return __builtin_fmaf(sg, q, sg);
 }
 
+// The same two functions on a pair of values in packed fp32 (v_pk_mul_f32 /
+// v_pk_fma_f32 / v_pk_add_f32: one issue per pair; exp2 / rcp stay per value).
+// The operation sequence and rounding are those of the scalar forms.  For the
+// GEMM epilogues, whose VALU work runs with the matrix pipe idle (one wave per
+// SIMD); beside MFMAs packed fp32 is an anti-lever (MI355X_MICROARCH.md).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 exp2_2(f32x2 z) {
+  return f32x2{__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
+}
+__device__ __forceinline__ f32x2 rcp_2(f32x2 z) { return f32x2{__builtin_amdgcn_rcpf(z[0]), __builtin_amdgcn_rcpf(z[1])}; }
+
+__device__ __forceinline__ f32x2 gelu_sig2(f32x2 x) {
+  const f32x2 t = x * x;
+  const f32x2 z = x * pk_fma(t, f32x2(-2.f * GK0 * GK1 * GL2E), f32x2(-2.f * GK0 * GL2E));
+  return x * rcp_2(exp2_2(z) + 1.f);
+}
+
+// m1 = (-1, -1) from the caller behind an empty asm: 1 - s then stays one
+// packed fma (a literal -1 is folded into 1 - s, which the backend scalarises)
+__device__ __forceinline__ f32x2 gelu_sig_grad2(f32x2 x, f32x2 m1) {
+  const f32x2 t = x * x;
+  const f32x2 z = x * pk_fma(t, f32x2(-2.f * GK0 * GK1 * GL2E), f32x2(-2.f * GK0 * GL2E));
+  const f32x2 sg = rcp_2(exp2_2(z) + 1.f);
+  const f32x2 w = pk_fma(t, f32x2(6.f * GK0 * GK1), f32x2(2.f * GK0));
+  const f32x2 q = x * pk_fma(sg, m1, -m1) * w;  // 1 - s (exact as an fma)
+  return pk_fma(sg, q, sg);
+}
+
 // number of workgroups for a grid-stride memory-bound kernel (256 CUs × 8)
 inline int stream_grid(long long work_items, int per_block) {
   long long g = (work_items + per_block - 1) / per_block;

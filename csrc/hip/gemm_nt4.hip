@@ -320,6 +320,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   f32x8 bv8;
   if constexpr (EPI >= 2) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
   f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x2 m1 = {-1.f, -1.f};
+  asm volatile("" : "+v"(m1));
 #pragma unroll
   for (int it = 0; it < 32; ++it) {
     const int r = 8 * it + r0;
@@ -332,14 +334,22 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       const f32x8 x = to_f32(v) + bv8;
       f32x8 y;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
+      for (int e = 0; e < 8; e += 2) {  // packed pairs (common.h)
+        const f32x2 g = gelu_sig2(f32x2{x[e], x[e + 1]});
+        y[e] = g[0];
+        y[e + 1] = g[1];
+      }
       *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
     } else {
       const f32x8 x = to_f32(pre[it]) + bv8;
       const f32x8 dy = to_f32(v);
       f32x8 d;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] = dy[e] * gelu_sig_grad(x[e]);
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 g = f32x2{dy[e], dy[e + 1]} * gelu_sig_grad2(f32x2{x[e], x[e + 1]}, m1);
+        d[e] = g[0];
+        d[e + 1] = g[1];
+      }
       colp += d;
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(d);
     }
