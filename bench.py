@@ -214,6 +214,20 @@ def ready_stats(trials):
     return out
 
 
+def _comm_summary(rs):
+    """Worst rank's exposed all-reduce time per step and slowest bucket all-reduce."""
+    cs = [r["comm"] for r in rs if r.get("comm")]
+    if not cs:
+        return None
+    out = {"ranks": len(cs), "allreduce_bytes": cs[0].get("allreduce_bytes"),
+           "allreduce_busbw_GBps_min": min(c["allreduce_busbw_GBps"] for c in cs)}
+    ex = [c["exposed_ms"] for c in cs if "exposed_ms" in c]
+    if ex:
+        out["exposed_ms_max"] = max(ex)
+        out["nosync_step_ms_max"] = max(c["nosync_step_ms"] for c in cs if "nosync_step_ms" in c)
+    return out
+
+
 def orchestrate(a):
     from paddle_operator_amd.models.gpt2 import GPT2Config
     from paddle_operator_amd.utils.topology import gpu_count
@@ -297,6 +311,8 @@ def orchestrate(a):
         "job_ready_s": round(out["bench_ready_s"], 3),
         "final_loss": rs[0].get("loss"),
         "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in rs),
+        # N > 1: measured after the timed region by every rank (launch/run.py _comm_diag)
+        "comm": _comm_summary(rs),
     }
     dev = "cpu/gloo" if not gpus else rs[0].get("gpu_name", "gpu")
     if a.workload == "gpt2":

@@ -200,6 +200,8 @@ def _bench(args, b, jenv, trainer, tokens_per_step, ready_rec) -> int:
     if dev.type == "cuda":
         res["gpu_name"] = torch.cuda.get_device_name(dev)
         res["max_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 2)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        res["comm"] = _comm_diag(trainer, fence, dev, dt / max(args.steps, 1))
     print("PDO_BENCH " + json.dumps(res), flush=True)
     kv = jenv.kv_endpoints()
     if kv:
@@ -209,6 +211,52 @@ def _bench(args, b, jenv, trainer, tokens_per_step, ready_rec) -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _comm_diag(trainer, fence, dev, step_s, nosync_steps=3, iters=10):
+    """Communication evidence for a multi-rank bench, measured AFTER the timed
+    region (the bench record's timing is untouched):
+
+    * ``exposed_ms``: timed step minus the same step with the gradient
+      all-reduce switched off (``BucketedDDP.no_sync``) — the part of the
+      bucketed RCCL traffic the backward did not hide;
+    * ``allreduce_busbw_GBps``: one bucket-sized (64 MiB on GPU) bf16
+      all-reduce, ring bus bandwidth = bytes · 2(n−1)/n / time — what xGMI
+      delivers to this job's communicator.
+
+    The no-sync steps leave the ranks' weights different; the job ends here."""
+    import torch
+    import torch.distributed as dist
+
+    out = {}
+    n = dist.get_world_size()
+    ddp = getattr(trainer, "ddp", None)
+    if ddp is not None and getattr(ddp, "enabled", False):
+        with ddp.no_sync():
+            trainer.step()
+            fence()
+            t0 = time.perf_counter()
+            for _ in range(nosync_steps):
+                trainer.step()
+            fence()
+        ns = (time.perf_counter() - t0) / nosync_steps
+        out["step_ms"] = round(step_s * 1e3, 3)
+        out["nosync_step_ms"] = round(ns * 1e3, 3)
+        out["exposed_ms"] = round((step_s - ns) * 1e3, 3)
+    nbytes = (64 << 20) if dev.type == "cuda" else (4 << 20)
+    buf = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=dev)
+    for _ in range(3):
+        dist.all_reduce(buf)
+    fence()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(buf)
+    fence()
+    t = (time.perf_counter() - t0) / iters
+    out["allreduce_bytes"] = nbytes
+    out["allreduce_us"] = round(t * 1e6, 1)
+    out["allreduce_busbw_GBps"] = round(nbytes * 2 * (n - 1) / n / t / 1e9, 1)
+    return out
 
 
 def run_ps(args, jenv) -> int:

@@ -103,6 +103,11 @@ def _check_record(rec, n):
     assert rec["config"]["parallelism"] == f"dp{n}" and rec["config"]["global_batch"] == 2 * n
     assert "PaddleJob" in rec["config"]["launch"]
     assert rec["ready"]["trials"] == 2 and 0 < rec["ready_p50_s"] < 60
+    if n > 1:  # communication evidence measured after the timed region (launch/run.py _comm_diag)
+        c = rec["comm"]
+        assert c["ranks"] == n and c["allreduce_busbw_GBps_min"] > 0 and "exposed_ms_max" in c, c
+    else:
+        assert rec["comm"] is None
     tokens = 2 * 64 * n * 2  # micro-batch × seq × world × steps
     assert abs(rec["value"] - tokens / (rec["ms_per_step"] * 2 / 1e3)) / rec["value"] < 1e-2
 
