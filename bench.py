@@ -97,13 +97,17 @@ def parse_args(argv=None):
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
     ap.add_argument("--ready-only", action="store_true", help="only the ready trials (prints their record)")
+    # N ranks on ONE GPU over gloo (RCCL refuses two ranks per device): rehearses the
+    # multi-rank launched GPU path (agent GPU accounting, DDP hooks over the HIP
+    # kernels, per-rank records, comm diagnostics) on a 1-GPU box; not a benchmark
+    ap.add_argument("--rehearse-shared-gpu", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
 class Launcher:
     """One in-process local backend; launches PaddleJobs and reads pdo-kv."""
 
-    def __init__(self, mode, zygote, gpus, sandbox):
+    def __init__(self, mode, zygote, gpus, sandbox, extra_args=()):
         from paddle_operator_amd.controller import LocalCluster
         from paddle_operator_amd.kv.client import KVClient
 
@@ -111,6 +115,7 @@ class Launcher:
         self.gpus = gpus
         self.sandbox = sandbox
         self.zygote = zygote
+        self.extra_args = list(extra_args)
         self.cl = LocalCluster(mode=mode, agent="exec", sandbox_root=sandbox,
                                nodes=[{"name": "node0", "gpus": gpus}],
                                kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote)
@@ -141,7 +146,7 @@ class Launcher:
     def launch(self, name, ranks, args, ops):
         from paddle_operator_amd.api import types as T
         job = T.paddlejob(name, worker={"replicas": ranks,
-                                        "template": {"spec": {"containers": [self.container(args, ops)]}}},
+                                        "template": {"spec": {"containers": [self.container(list(args) + self.extra_args, ops)]}}},
                           clean_pod_policy="Always")
         t0 = time.time()
         self.cl.create(job)
@@ -151,6 +156,7 @@ class Launcher:
         prefix = f"/pdo/default-{name}/{kind}/"
         deadline = time.time() + timeout
         recs = {}
+        beat = time.time() + 30
         while time.time() < deadline:
             recs = self.kv.get_prefix(prefix)
             if len(recs) >= n:
@@ -158,12 +164,15 @@ class Launcher:
             phase = ((self.cl.job(name) or {}).get("status") or {}).get("phase")
             if phase == "Failed":
                 break
+            if time.time() > beat:  # progress line for long jobs (many ranks, slow steps)
+                log(f"{name}: {len(recs)}/{n} {kind} records, phase {phase}")
+                beat = time.time() + 30
             time.sleep(0.005)
         self.dump_logs(name)
         raise RuntimeError(f"{name}: {len(recs)}/{n} {kind} records (phase "
                            f"{((self.cl.job(name) or {}).get('status') or {}).get('phase')})")
 
-    def dump_logs(self, name, tail=4000):
+    def dump_logs(self, name, tail=int(os.environ.get("PDO_BENCH_LOG_TAIL", "4000"))):
         import glob
         for path in sorted(glob.glob(os.path.join(self.sandbox, "*", f"default_{name}-*", "*.log")) +
                            glob.glob(os.path.join(self.sandbox, "*", "zygote.log"))):
@@ -236,6 +245,18 @@ def orchestrate(a):
     if not a.micro_batch:
         a.micro_batch = 64 if a.workload == "gpt2" else 256
     detected = 0 if a.cpu else gpu_count()
+    extra_args = []
+    if a.rehearse_shared_gpu:
+        if not detected:
+            log("--rehearse-shared-gpu needs a GPU")
+            return 2
+        # every agent GPU index maps to physical GPU 0; no warm slots (one per physical GPU)
+        os.environ["HIP_VISIBLE_DEVICES"] = ",".join(["0"] * N)
+        os.environ["PDO_WARM_SLOTS"] = "0"
+        a.no_warm_slots = True
+        os.environ.setdefault("PDO_HANG_DUMP_S", "60")  # rank stacks in the pod logs (launch/run.py)
+        extra_args = ["--backend", "gloo"]
+        detected = N
     if detected and detected < N:
         log(f"--gpus {N} but only {detected} GPU(s) visible")
         return 2
@@ -245,7 +266,7 @@ def orchestrate(a):
         os.environ["PDO_WARM_SLOTS"] = "0"  # read by the agent when it starts the zygote
     out = {}
     try:
-        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode))
+        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode), extra_args)
         try:
             trials = []
             for t in range(a.ready_trials):
@@ -322,7 +343,8 @@ def orchestrate(a):
                "value": round(rate, 1), "unit": "tokens/s", **common,
                "data": "synthetic (on-device random tokens), random-init weights",
                "config": {"model": a.model, "global_batch": a.micro_batch * N, "micro_batch_per_gpu": a.micro_batch,
-                          "seq_len": a.seq, "parallelism": f"dp{N}", "launch": launch,
+                          "seq_len": a.seq, "parallelism": f"dp{N}" + ("-shared-gpu-gloo" if a.rehearse_shared_gpu else ""),
+                          "launch": launch,
                           "grad_reduce": rs[0].get("grad_reduce"), "buckets": rs[0].get("buckets"), "ops": a.ops,
                           "device": dev},
                **extra,

@@ -329,6 +329,12 @@ def main(argv=None) -> int:
     jenv = JobEnv.from_env()
     jenv.check_supported()
     log(f"role={jenv.role} id={jenv.trainer_id} mode={jenv.mode} elastic={jenv.elastic} workload={args.workload}")
+    hang_dump = float(os.environ.get("PDO_HANG_DUMP_S", "0") or 0)
+    if hang_dump > 0:
+        # hang diagnostics: every thread's Python stack to the pod log every N s
+        # (a rank stuck in a collective shows where; no debugger attached)
+        import faulthandler
+        faulthandler.dump_traceback_later(hang_dump, repeat=True, file=sys.stderr)
     if jenv.mode == "PS" or args.workload in ("wide_deep", "deepfm") and jenv.pserver_endpoints:
         return run_ps(args, jenv)
     if (jenv.elastic or args.elastic) and not args.worker:
