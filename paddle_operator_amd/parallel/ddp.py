@@ -66,6 +66,14 @@ class BucketedDDP:
         self._seen = set()
         self._hooks = []
         self._staged = False
+        # gloo on GPU tensors (the shared-GPU rehearsal, PDO_DIST_BACKEND=gloo):
+        # one bucket in flight at a time.  Dozens of queued async gloo all-reduces
+        # on CUDA tensors collapsed to ~30 MB/s at 3 ranks (22 s per GPT-2-medium
+        # step vs 2.4 GB/s for one-at-a-time all-reduces, bench.py
+        # --rehearse-shared-gpu) and stalled outright at 4.  RCCL keeps the
+        # overlapped pipeline: its collectives are stream-ordered kernels.
+        self._serial = (self.enabled and flat.device.type == "cuda" and dist.is_initialized()
+                        and dist.get_backend(group) == "gloo")
         if self.enabled:
             for s in flat.slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._hook))
@@ -155,6 +163,8 @@ class BucketedDDP:
             _cast_scale(buf, st, 1.0 / self.world)
             buf = st
             self._staged = True
+        if self._serial and self._works:
+            self._works[-1].wait()
         w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._works.append(w)
 
