@@ -1,4 +1,4 @@
-"""Data parallelism over the HIP training path on one MI355X (2 ranks, gloo).
+"""Data parallelism over the HIP training path on one MI355X (2 and 4 ranks, gloo).
 
 RCCL refuses two ranks on one GPU, so the collective here is gloo over the
 same BucketedDDP code; everything else is the production GPU path: bf16 flat
@@ -73,20 +73,24 @@ def _port():
     return p
 
 
-def test_ddp_two_ranks_hip_path_matches_full_batch(tmp_path, cuda):
-    mp.start_processes(_worker, args=(2, _port(), str(tmp_path)), nprocs=2, start_method="spawn")
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_ranks_hip_path_matches_full_batch(tmp_path, cuda, world):
+    """world 4 also pins the one-bucket-in-flight rule for gloo on GPU tensors
+    (BucketedDDP._serial): queued async gloo CUDA all-reduces stalled at 4 ranks."""
+    mp.start_processes(_worker, args=(world, _port(), str(tmp_path)), nprocs=world, start_method="spawn")
     ref_path = str(tmp_path / "ref.pt")
     p = mp.get_context("spawn").Process(target=_grads, args=(0, 1, _port(), ref_path, 64 << 20))
     p.start()
     p.join(300)
     assert p.exitcode == 0
     ref = torch.load(ref_path, weights_only=True)
-    g0 = torch.load(tmp_path / "g0.pt", weights_only=True)
-    g1 = torch.load(tmp_path / "g1.pt", weights_only=True)
+    gs = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(world)]
+    g0 = gs[0]
     bad = []
     for n, r in ref.items():
-        if not torch.equal(g0[n], g1[n]):
-            bad.append(f"{n}: ranks disagree (max |g0-g1| {(g0[n] - g1[n]).abs().max().item():.3g})")
+        for k, gk in enumerate(gs[1:], 1):
+            if not torch.equal(g0[n], gk[n]):
+                bad.append(f"{n}: ranks 0/{k} disagree (max diff {(g0[n] - gk[n]).abs().max().item():.3g})")
         err = ((g0[n] - r).abs().max() / r.abs().max().clamp_min(1e-8)).item()
         if not err < 3e-2:
             bad.append(f"{n}: rel err {err:.3g} (|ref| {r.abs().max().item():.3g}, |ddp| {g0[n].abs().max().item():.3g})")
