@@ -193,10 +193,13 @@ void Server::stop() {
     }
     return;
   }
+  // wake the acceptor (shutdown makes its accept4 fail), join it, THEN close:
+  // closing first would let the acceptor read fd_ concurrently (TSan) and call
+  // accept4 on a descriptor number the process may already have reused
   ::shutdown(fd_, SHUT_RDWR);
+  if (acceptor_.joinable()) acceptor_.join();
   ::close(fd_);
   fd_ = -1;
-  if (acceptor_.joinable()) acceptor_.join();
   {
     std::lock_guard<std::mutex> g(conn_mu_);
     for (int cfd : conn_fds_) ::shutdown(cfd, SHUT_RDWR);
@@ -206,10 +209,11 @@ void Server::stop() {
 }
 
 void Server::accept_loop() {
+  const int lfd = fd_;  // fixed for the acceptor's lifetime (stop() closes it after the join)
   while (running_) {
     sockaddr_in sa{};
     socklen_t len = sizeof sa;
-    int cfd = ::accept4(fd_, (sockaddr*)&sa, &len, SOCK_CLOEXEC);
+    int cfd = ::accept4(lfd, (sockaddr*)&sa, &len, SOCK_CLOEXEC);
     if (cfd < 0) {
       if (!running_) break;
       if (errno == EINTR) continue;
