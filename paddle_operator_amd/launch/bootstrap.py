@@ -62,6 +62,32 @@ def _wait_port(host: str, port: int, timeout_s: float, poll: float = 0.002) -> b
     return False
 
 
+_STORE = []  # keeps rank 0's store (and its listening socket) alive for the job
+
+
+def _bound_store(host: str, port: int, world: int, timeout_s: int):
+    """Rank 0's c10d TCPStore listening on ``host`` only.
+
+    c10d binds its store to the wildcard address.  On Kubernetes every pod has
+    its own network namespace, but the local backend's exec agent runs pods as
+    processes with one loopback IP each, so two concurrent jobs' rank 0 both
+    wanting ``PADDLE_PORT + 1`` collided (EADDRINUSE).  A socket bound to the
+    pod's own address and handed over as ``master_listen_fd`` keeps them apart.
+    Returns None when ``host`` is not a local address (a service name or
+    ClusterIP): then c10d's default wildcard store is used."""
+    try:
+        ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        ls.bind((socket.gethostbyname(host), port))
+        ls.listen(1024)
+    except OSError:
+        return None
+    store = dist.TCPStore(host, port, world, True, datetime.timedelta(seconds=timeout_s),
+                          wait_for_workers=False, master_listen_fd=ls.fileno())
+    _STORE.append((store, ls))
+    return store
+
+
 def _env_int(k, d):
     return int(os.environ.get(k, str(d)))
 
@@ -98,11 +124,17 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
             kw["store"] = dist.HashStore()
         else:
             host, port = os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"])
-            if rank != 0:
+            # explicit stores on every rank (an init_method URL would put the
+            # process group's keys under a "default_pg" prefix on one side only)
+            to = datetime.timedelta(seconds=timeout_s)
+            if rank == 0:
+                kw["store"] = (_bound_store(host, port, world, timeout_s)
+                               or dist.TCPStore(host, port, world, True, to, wait_for_workers=False))
+            else:
                 # c10d's client connect retries back off to ~1 s; ranks forked
                 # in the same ms as rank 0 would otherwise sleep through its bind
                 _wait_port(host, port, timeout_s)
-            kw["init_method"] = f"tcp://{host}:{port}"
+                kw["store"] = dist.TCPStore(host, port, world, False, to)
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         t_comm = time.time()

@@ -224,3 +224,37 @@ def test_heter_ps_mode(tmp_path):
         d = records(tmp_path / f"t{i}.log", "PDO_DONE")[0]
         assert d["last_loss"] < d["first_loss"] - 0.05, d
         assert d["heter_stats"][0]["heter_steps"] >= 60  # this trainer's steps (at least) ran on the heter worker
+
+
+_STORE_JOB = r"""
+import os, sys, time
+sys.path.insert(0, sys.argv[1])
+import torch, torch.distributed as dist
+from paddle_operator_amd.launch import bootstrap
+b = bootstrap.init(time.time(), backend="gloo", timeout_s=60)
+t = torch.ones(1) * (b.rank + 1)
+dist.all_reduce(t)
+assert t.item() == 3.0, t
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_concurrent_jobs_same_store_port_distinct_pod_ips():
+    """Two 2-rank jobs whose rank 0s share MASTER_PORT on different loopback pod
+    IPs (the local backend's exec agent): rank 0's store binds its own address
+    (bootstrap._bound_store), so neither job fails with EADDRINUSE."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for ip in ("127.0.0.21", "127.0.0.22"):
+        for rank in (0, 1):
+            env = dict(os.environ, MASTER_ADDR=ip, MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                       LOCAL_RANK="0", OMP_NUM_THREADS="1", PDO_PIN_CPUS="0")
+            procs.append(subprocess.Popen([sys.executable, "-c", _STORE_JOB, root], env=env,
+                                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), "\n---\n".join(outs)
