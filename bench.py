@@ -93,6 +93,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-warm-slots", action="store_true",
                     help="zygote without GPU-warm slots (every rank inits HIP + RCCL from scratch)")
     ap.add_argument("--cpu", action="store_true", help="ranks on CPU (gloo) even if GPUs are present")
+    ap.add_argument("--gpu-visibility", choices=["all", "isolate"], default="all",
+                    help="node agent GPU exposure: all = every rank sees the node's GPUs and selects its own "
+                         "(PDO_GPU_IDS, as torchrun-style launches; RCCL sees xGMI peers as local devices); "
+                         "isolate = HIP_VISIBLE_DEVICES per pod, as a Kubernetes device plugin")
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
@@ -261,6 +265,9 @@ def orchestrate(a):
         log(f"--gpus {N} but only {detected} GPU(s) visible")
         return 2
     gpus = N if detected else 0  # the job asks for N amd.com/gpu; the node offers exactly those
+    if gpus:
+        # read by the in-process agent (csrc/core/agent.cpp) and its warm launcher
+        os.environ["PDO_GPU_VISIBILITY"] = "isolate" if a.rehearse_shared_gpu else a.gpu_visibility
     sandbox = tempfile.mkdtemp(prefix="pdo-bench-")
     if a.no_warm_slots:
         os.environ["PDO_WARM_SLOTS"] = "0"  # read by the agent when it starts the zygote
@@ -323,7 +330,8 @@ def orchestrate(a):
         "dtype": "bf16",
     }
     launch = (f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}, "
-              f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}")
+              f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}, "
+              f"gpu_visibility={os.environ.get('PDO_GPU_VISIBILITY', 'isolate') if gpus else 'cpu'}")
     extra = {
         "baseline_metric": BASELINE_METRIC,
         "ready_p50_s": out["ready"]["p50"] if out.get("ready") else None,

@@ -257,7 +257,14 @@ bool Agent::build_env(const Rt& rt, const Value& pod, const Value& c, std::vecto
     set(name, "");
   }
   // device + sandbox env (the device plugin's job on a real node)
-  if (!rt.gpus.empty()) set("HIP_VISIBLE_DEVICES", visible_ids(rt.gpus));
+  // PDO_GPU_VISIBILITY=all (node-agent setting): the pod sees every GPU of the
+  // node and gets its own ids in PDO_GPU_IDS (bootstrap selects the device),
+  // as torchrun-style launches do — RCCL then knows its peers as local devices
+  // for xGMI P2P.  Default: HIP_VISIBLE_DEVICES isolation, as a device plugin.
+  if (!rt.gpus.empty()) {
+    const char* vis = getenv("PDO_GPU_VISIBILITY");
+    set(vis && std::string(vis) == "all" ? "PDO_GPU_IDS" : "HIP_VISIBLE_DEVICES", visible_ids(rt.gpus));
+  }
   set("PDO_POD_IP", rt.ip);
   set("PDO_NODE_NAME", opt_.node.name);
   set("PDO_SANDBOX", rt.sandbox);

@@ -98,14 +98,18 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
     rank = _env_int("RANK", 0)
     world = _env_int("WORLD_SIZE", 1)
     local = _env_int("LOCAL_RANK", 0)
-    topology.pin_to_gpu(local)  # before HIP init: uses sysfs only
+    # PDO_GPU_IDS (agent with PDO_GPU_VISIBILITY=all): every GPU is visible and
+    # this pod's own ids are listed; else HIP_VISIBLE_DEVICES isolation → index
+    ids = [int(x) for x in os.environ.get("PDO_GPU_IDS", "").split(",") if x.strip().isdigit()]
+    index = ids[local] if local < len(ids) else local
+    topology.pin_to_gpu(index)  # before HIP init: uses sysfs only
     gpu = torch.cuda.is_available()
     if backend is None:
         backend = "nccl" if gpu else "gloo"
     if gpu:
-        torch.cuda.set_device(local)  # hipSetDevice
+        torch.cuda.set_device(index)  # hipSetDevice
         torch.cuda.init()
-        dev = torch.device("cuda", local)
+        dev = torch.device("cuda", index)
     else:
         dev = torch.device("cpu")
     t_dev = time.time()

@@ -87,7 +87,7 @@ def warm_device_of(req: dict, key: tuple) -> Optional[str]:
     """The GPU id a request may take a warm slot for, or None (cold fork)."""
     env = req.get("env") or {}
     argv = req.get("argv") or []
-    dev = env.get("HIP_VISIBLE_DEVICES", "")
+    dev = env.get("HIP_VISIBLE_DEVICES", "") or env.get("PDO_GPU_IDS", "")
     if not dev or "," in dev or env.get("PDO_WARM_SLOT", "1") == "0":
         return None
     # elastic agents fork+exec their workers: never from a HIP-initialised process
@@ -174,20 +174,22 @@ def _become_rank(req, fds, warm=False):
         os._exit(rc)
 
 
-def _warm_gpu() -> dict:
+def _warm_gpu(index: int = 0) -> dict:
     """HIP init + a 1-rank RCCL communicator built and destroyed (loads RCCL's
-    device code into this process), on the slot's one visible GPU."""
+    device code into this process) on device ``index``: 0 = the slot's one
+    visible GPU, or the GPU's own index when every GPU is visible
+    (PDO_GPU_VISIBILITY=all)."""
     import torch
     import torch.distributed as dist
 
     from ..utils import topology
     t0 = time.time()
-    topology.pin_to_gpu(0)
+    topology.pin_to_gpu(index)
     if not torch.cuda.is_available():  # a GPU node with no usable HIP device: nothing to warm
         return {"device": "none"}
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(index)
     torch.cuda.init()
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", index)
     t1 = time.time()
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=dev)
     t = torch.ones(1, device=dev)
@@ -210,8 +212,12 @@ def _slot_main(dev: str, sock: socket.socket, listener: socket.socket):
         for sig in (signal.SIGTERM, signal.SIGCHLD):
             signal.signal(sig, signal.SIG_DFL)
         os.environ.pop("CUDA_VISIBLE_DEVICES", None)
-        os.environ["HIP_VISIBLE_DEVICES"] = dev
-        info = _warm_gpu()
+        if os.environ.get("PDO_GPU_VISIBILITY") == "all":
+            os.environ.pop("HIP_VISIBLE_DEVICES", None)
+            info = _warm_gpu(int(dev))
+        else:
+            os.environ["HIP_VISIBLE_DEVICES"] = dev
+            info = _warm_gpu()
         info["pid"] = os.getpid()
         sock.sendall(f"READY {json.dumps(info)}\n".encode())
         req, fds = _recv_request(sock)

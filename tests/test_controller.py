@@ -574,3 +574,30 @@ def test_elastic_member_rejoins_after_lease_loss(tmp_path):
         assert len(gens) >= 2  # the world re-formed around the new lease
     finally:
         cl.stop()
+
+
+@pytest.mark.parametrize("visibility", ["isolate", "all"])
+def test_exec_agent_gpu_visibility_modes(tmp_path, monkeypatch, visibility):
+    """Default: each pod sees only its GPUs (HIP_VISIBLE_DEVICES, as a device
+    plugin).  PDO_GPU_VISIBILITY=all on the agent: every GPU stays visible and
+    the pod's own ids come in PDO_GPU_IDS (launch/bootstrap.py selects it) — the
+    torchrun-style layout bench.py uses so RCCL sees its xGMI peers as local
+    devices."""
+    if visibility == "all":
+        monkeypatch.setenv("PDO_GPU_VISIBILITY", "all")
+    else:
+        monkeypatch.delenv("PDO_GPU_VISIBILITY", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), nodes=[{"name": "n0", "gpus": 2}])
+    c = {"name": "paddle", "image": "busybox", "command": ["sh", "-c", "env | grep -E '^(PDO_GPU_IDS|HIP_VISIBLE_DEVICES)=' | sort"],
+         "resources": {"limits": {T.AMD_GPU: 1}}}
+    cl.create(T.paddlejob("vis", worker={"replicas": 2, "template": {"spec": {"containers": [c]}}},
+                          clean_pod_policy="Never"))
+    try:
+        assert cl.wait_phase("vis", T.Phase.Completed, timeout=60), cl.job("vis")["status"]
+        seen = sorted(open(os.path.join(cl.sandbox(f"vis-worker-{i}"), "paddle.log")).read().strip() for i in range(2))
+        key = "PDO_GPU_IDS" if visibility == "all" else "HIP_VISIBLE_DEVICES"
+        assert seen == [f"{key}=0", f"{key}=1"], seen
+    finally:
+        cl.stop()
