@@ -307,7 +307,7 @@ def orchestrate(a):
         finally:
             L.stop()
         if a.compat_trials:
-            C = Launcher("compat", False, gpus, os.path.join(sandbox, "compat"))
+            C = Launcher("compat", False, gpus, os.path.join(sandbox, "compat"), extra_args)
             try:
                 ct = [C.ready_trial(f"compat-{t}", N, a.timeout) for t in range(a.compat_trials)]
             finally:
