@@ -49,7 +49,8 @@ def main():
     M, C = a.tokens, 1024
     shapes = [("qkv_fwd", 3 * C, C, "bias"), ("proj_fwd", C, C, "plain"), ("fc1_fwd", 4 * C, C, "gelu"),
               ("fc2_fwd", C, 4 * C, "plain"), ("qkv_dx", C, 3 * C, "plain"), ("proj_dx", C, C, "plain"),
-              ("fc1_dx", C, 4 * C, "plain"), ("fc2_dx", 4 * C, C, "dgelu"), ("lm_dx", C, 50304, "plain")]
+              ("fc1_dx", C, 4 * C, "plain"), ("fc2_dx", 4 * C, C, "dgelu"), ("lm_dx", C, 50304, "plain"),
+              ("wide_plain", 4 * C, C, "plain")]  # fc1_fwd / fc2_dx GEMM without an epilogue
     if a.shapes:
         keep = set(a.shapes.split(","))
         shapes = [s for s in shapes if s[0] in keep]
