@@ -32,6 +32,8 @@
 // ds_read_b128 lane group touches land on 16 distinct bank slots.  The DMA
 // writes LDS linearly (1 KiB = 8 rows per wave-instruction) and applies the
 // swizzle on the per-lane global source address.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
                                                            const bf16* __restrict__ bias, bf16* __restrict__ Y,
-                                                           int ldy, float* __restrict__ dbias_part) {
+                                                           int ldy, float* __restrict__ dbias_part, int group_m) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * 256 * BK];  // [buf][A|B][256][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -61,7 +63,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
     id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
-  const int tn = id % tiles_n, tm = id / tiles_n;
+  // grouped tile order: consecutive ids walk group_m tile rows, then the next
+  // tile column, so the 32 tiles an XCD runs at once form a group_m × (32 /
+  // group_m) block and share fewer A/B panels in that XCD's 4 MiB L2 (row-major,
+  // group_m = 1: 2 rows × 16 columns on the [65536, 4096] shapes = 18 panels)
+  int tn, tm;
+  {
+    const int tiles_m = M / BM, per_group = group_m * tiles_n;
+    const int g = id / per_group, first_m = g * group_m;
+    const int gsz = min(tiles_m - first_m, group_m), r = id - g * per_group;
+    tm = first_m + r % gsz;
+    tn = r / gsz;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- LDS-DMA sources.  Wave w fills 8-row blocks b = w + 4i (i = 0..7) of
@@ -370,13 +383,20 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;
   if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
+  static const int group_m = [] {
+    const char* e = getenv("PDO_NT_GROUP_M");
+    // 8: tools/gpu_group_m.sh on the GPT-2 NT shapes (row-major = 1: wide K = 1024 GEMM
+    // 501 -> 451 us, fc2 dX ⊙ GELU' 642 -> 607, qkv 433 -> 419; 16 is slower; bit-identical)
+    const int g = e ? atoi(e) : 8;
+    return g >= 1 ? g : 1;
+  }();
   auto launch = [&](auto gpg, auto bar, auto bufld) {
     constexpr int G = decltype(gpg)::value, R = decltype(bar)::value, L = decltype(bufld)::value;
     switch (epi) {
-      case 0: gemm_nt4_kernel<0, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-      case 1: gemm_nt4_kernel<1, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-      case 2: gemm_nt4_kernel<2, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
-      case 3: gemm_nt4_kernel<3, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+      case 0: gemm_nt4_kernel<0, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 1: gemm_nt4_kernel<1, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 2: gemm_nt4_kernel<2, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 3: gemm_nt4_kernel<3, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       default: return -4;
     }
     return 0;
