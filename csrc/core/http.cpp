@@ -659,15 +659,18 @@ void parse_head(const std::string& text, Head* h) {
   }
 }
 
-// one attempt on connection `c`; *sent_nothing = the server answered nothing
-// at all (a stale keep-alive connection: safe to retry on a fresh one)
+// one attempt on connection `c`.  *unsent = the request could not be written
+// (never reached the server: always safe to send again); *no_answer = it was
+// written but the server answered nothing at all (a stale keep-alive connection
+// — or a server that applied it and then dropped the connection)
 ClientResponse exchange(Conn& c, const std::string& req, const std::function<bool(const std::string&)>* on_line,
-                        bool* sent_nothing, bool* reusable) {
+                        bool* unsent, bool* no_answer, bool* reusable) {
   ClientResponse out;
-  *sent_nothing = false;
+  *unsent = false;
+  *no_answer = false;
   *reusable = false;
   if (!c.wr(req)) {
-    *sent_nothing = true;
+    *unsent = true;
     out.error = "send failed";
     return out;
   }
@@ -677,7 +680,7 @@ ClientResponse exchange(Conn& c, const std::string& req, const std::function<boo
   while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos) {
     ssize_t r = c.rd(tmp, sizeof tmp);
     if (r <= 0) {
-      *sent_nothing = buf.empty();
+      *no_answer = buf.empty();
       out.error = "no response";
       return out;
     }
@@ -785,9 +788,12 @@ ClientResponse do_request(const std::string& method, const std::string& url, con
     } else {
       c->set_timeout(opt.timeout_s);
     }
-    bool nothing = false, reusable = false;
-    out = exchange(*c, req, on_line, &nothing, &reusable);
-    if (out.status == 0 && reused && nothing) continue;  // the server dropped an idle connection
+    bool unsent = false, no_answer = false, reusable = false;
+    out = exchange(*c, req, on_line, &unsent, &no_answer, &reusable);
+    // a reused connection the server had already dropped: resend on a fresh one
+    // only when the request never left, or repeating it is harmless
+    const bool idem = opt.idempotent || method == "GET" || method == "HEAD" || method == "OPTIONS";
+    if (out.status == 0 && reused && (unsent || (no_answer && idem))) continue;
     if (pooled && reusable) pool_put(std::move(c));
     return out;
   }

@@ -104,6 +104,12 @@ struct ClientOptions {
   std::string ca_pem, cert_pem, key_pem;     // or PEM text (kubeconfig *-data): never written to disk
   bool insecure_skip_verify = false;
   bool keep_alive = true;  // reuse connections to the same server (not for streams)
+  // a request whose repetition is harmless: when a reused keep-alive connection
+  // returns nothing after the request was written, it is sent again on a fresh
+  // connection.  Default: GET / HEAD / OPTIONS only — an empty read does not prove
+  // the server never applied a POST / PUT / DELETE (it may have, then reset).
+  // A request that could not be written at all is always retried.
+  bool idempotent = false;
 };
 
 ClientResponse request(const std::string& method, const std::string& url, const std::string& body = "",

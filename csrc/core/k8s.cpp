@@ -177,51 +177,80 @@ void Informer::stop() {
   if (th_.joinable()) th_.join();
 }
 
+bool apply_watch_event(const std::string& line, store::Store* cache, const std::string& kind, std::string* rv,
+                       bool* gone) {
+  const KindInfo* k = kind_by_name(kind);
+  Value ev;
+  try {
+    ev = Value::parse(line);
+  } catch (const std::exception&) {
+    return true;  // a torn or foreign line: skip it, keep the stream
+  }
+  const std::string type = ev.get("type").str();
+  Value obj = ev.get("object");
+  if (type == "ERROR") {
+    // metav1.Status: 410 Expired / Gone = the resourceVersion was compacted away
+    const int code = (int)obj.get("code").as_int();
+    *gone = code == 410 || obj.get("reason").str() == "Expired" || obj.get("reason").str() == "Gone";
+    return false;
+  }
+  const std::string orv = obj.at_path("metadata.resourceVersion").str();
+  if (!orv.empty()) *rv = orv;
+  if (type == "BOOKMARK") return true;  // only the resourceVersion moves
+  if (type != "ADDED" && type != "MODIFIED" && type != "DELETED") return true;
+  if (k) api::set_type_meta(obj, k->group_version, k->kind);
+  if (type == "DELETED")
+    cache->mirror_delete(kind, obj.at_path("metadata.namespace").str(), obj.at_path("metadata.name").str());
+  else
+    cache->mirror_put(kind, obj);
+  return true;
+}
+
 void Informer::run() {
   const KindInfo* k = kind_by_name(kind_);
+  std::string rv;
+  bool need_list = true;
   while (running_) {
-    std::string rv;
-    try {
-      Value l = api_->list(kind_, ns_, &rv);
-      std::vector<Value> items;
-      for (auto& o : l.get("items").arr()) {
-        Value x = o;
-        api::set_type_meta(x, k->group_version, k->kind);
-        items.push_back(x);
-      }
-      cache_->mirror_replace(kind_, ns_, items);
-      synced_ = true;
-    } catch (const std::exception& e) {
-      log::error("informer", "list failed", {{"kind", kind_}, {"error", e.what()}});
-      for (int i = 0; i < 20 && running_; ++i) usleep(100000);
-      continue;
-    }
-    // watch until the stream ends (timeout / 410 Gone) or we stop
-    const std::string url = api_->config().server + collection_path(*k, ns_) +
-                            "?watch=true&allowWatchBookmarks=true&timeoutSeconds=300&resourceVersion=" + rv;
-    bool gone = false;
-    auto opts = api_->config().client(330);
-    http::stream_lines("GET", url, "", [&](const std::string& line) {
-      if (!running_) return false;
+    if (need_list) {
       try {
-        Value ev = Value::parse(line);
-        const std::string type = ev.get("type").str();
-        Value obj = ev.get("object");
-        if (type == "ERROR") {
-          gone = obj.get("code").as_int() == 410;
-          return false;
+        Value l = api_->list(kind_, ns_, &rv);
+        std::vector<Value> items;
+        for (auto& o : l.get("items").arr()) {
+          Value x = o;
+          api::set_type_meta(x, k->group_version, k->kind);
+          items.push_back(x);
         }
-        if (type == "BOOKMARK") return true;
-        api::set_type_meta(obj, k->group_version, k->kind);
-        if (type == "DELETED")
-          cache_->mirror_delete(kind_, obj.at_path("metadata.namespace").str(), obj.at_path("metadata.name").str());
-        else
-          cache_->mirror_put(kind_, obj);
-      } catch (const std::exception&) {
+        cache_->mirror_replace(kind_, ns_, items);
+        synced_ = true;
+        need_list = false;
+        ++lists_;
+      } catch (const std::exception& e) {
+        log::error("informer", "list failed", {{"kind", kind_}, {"error", e.what()}});
+        for (int i = 0; i < 20 && running_; ++i) usleep(100000);
+        continue;
+      }
+    }
+    // watch from rv until the stream ends: a clean end (server-side timeout)
+    // re-watches from the last resourceVersion seen — BOOKMARKs included —
+    // an ERROR event or a failed watch request relists (client-go's reflector)
+    const std::string url = api_->config().server + collection_path(*k, ns_) +
+                            "?watch=true&allowWatchBookmarks=true&timeoutSeconds=" + std::to_string(watch_timeout_s) +
+                            "&resourceVersion=" + http::url_encode(rv);
+    bool gone = false, ended_by_event = false;
+    auto opts = api_->config().client(watch_timeout_s + 30);
+    ++watches_;
+    auto r = http::stream_lines("GET", url, "", [&](const std::string& line) {
+      if (!running_) return false;
+      if (!apply_watch_event(line, cache_, kind_, &rv, &gone)) {
+        ended_by_event = true;
+        return false;
       }
       return true;
     }, opts);
-    (void)gone;  // either way: relist
+    if (ended_by_event || r.status != 200) {
+      need_list = true;
+      if (!gone && running_) usleep(200000);  // an unexpected error: back off before relisting
+    }
   }
 }
 

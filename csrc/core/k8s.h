@@ -61,6 +61,9 @@ class Informer {
   void start();
   void stop();
   bool synced() const { return synced_; }
+  int lists() const { return lists_; }      // LISTs issued (initial + relists)
+  int watches() const { return watches_; }  // WATCH requests issued
+  int watch_timeout_s = 300;
 
  private:
   void run();
@@ -68,8 +71,16 @@ class Informer {
   store::Store* cache_;
   std::string kind_, ns_;
   std::atomic<bool> running_{false}, synced_{false};
+  std::atomic<int> lists_{0}, watches_{0};
   std::thread th_;
 };
+
+// one line of a watch stream (a watch.Event JSON) applied to the mirrored cache.
+// *rv follows every event's metadata.resourceVersion, BOOKMARKs included.
+// Returns false on an ERROR event (the stream is over), with *gone = 410
+// Expired / Gone (the resourceVersion was compacted: relist).
+bool apply_watch_event(const std::string& line, store::Store* cache, const std::string& kind, std::string* rv,
+                       bool* gone);
 
 class LeaderElector {
  public:

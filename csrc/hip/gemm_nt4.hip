@@ -35,6 +35,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 #include "kernels.h"
@@ -44,9 +45,69 @@ namespace pdo {
 namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
+
+// f(integral_constant<int, I>) for I = 0 .. N-1, expanded at compile time: a
+// 128-slot MFMA schedule is too large for `#pragma unroll` (hipcc gives up and
+// indexes the accumulators at run time); here every slot's index is a constant
+template <typename Fn, int... I>
+__device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 = 32 KiB
 
-template <int EPI, int EPG, int BAR, int BUFLD>
+// ---- register-epilogue helpers (SCHED 1)
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 join(u32x2 a, u32x2 b) {
+  return __builtin_bit_cast(bf16x8, u32x4{a[0], a[1], b[0], b[1]});
+}
+__device__ __forceinline__ u32x2 pack4(f32x4 v) {  // 4 fp32 → 4 bf16 (round to nearest even)
+  const bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  return __builtin_bit_cast(u32x2, b);
+}
+__device__ __forceinline__ void swap32(u32x2& x, u32x2& y) {  // x's upper 32 lanes ↔ y's lower 32
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x[d], y[d], false, false);
+    x[d] = r[0];
+    y[d] = r[1];
+  }
+}
+__device__ __forceinline__ void swap16(u32x2& x, u32x2& y) {  // x's odd 16-lane rows ↔ y's even rows
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+    x[d] = r[0];
+    y[d] = r[1];
+  }
+}
+// 4×4 block transpose across the lane groups q = lane >> 4: in, b[j] holds the
+// columns 16j + 4q .. +3 of the lane's row; out, b[q'] holds 16q + 4q' .. +3,
+// i.e. the lane owns 16 contiguous columns of block q
+__device__ __forceinline__ void transpose_blocks(u32x2 (&b)[4]) {
+  swap32(b[0], b[2]);
+  swap32(b[1], b[3]);
+  swap16(b[0], b[1]);
+  swap16(b[2], b[3]);
+}
+
+// SCHED 0: one barrier per k-tile, tile t+1's DMA issued during tile t (lead
+//          ≈ 0.6 tile), described at the top of the file.
+// SCHED 1: three barriers per k-tile and an operand-split refill — the schedule
+//          of hipBLASLt's gfx950 MT256x256x64 loop (profiles/r3_gemm_nt4_sched.md).
+//          Tile t's buffer is released operand by operand as the waves finish
+//          reading it: after barrier 1 (every wave's last A read of it, the k
+//          32-63 fragments) its A half is refilled with tile t+2, after barrier 2
+//          its B half.  Barrier 3 (vmcnt = this tile's own t+2 pieces still in
+//          flight) publishes tile t+1, whose k 0-31 fragments are then read
+//          under the last quarter of tile t's MFMAs.  Every DMA piece has
+//          ≈ 1.3-1.6 tiles of lead instead of ≈ 0.6.
+template <int EPI, int EPG, int BAR, int BUFLD, int SCHED = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
@@ -177,6 +238,101 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   f32x4 acc[8][8];  // first written by mma0 in tile 0's block 0
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
+  if constexpr (SCHED == 1) {
+    // fragment i of A (rows wm·128 + 16i + (l & 15)) / B, k half kk, from buffer BUF
+    auto rdA = [&](auto buf_tag, int kk, int i) -> bf16x8 {
+      constexpr int BUF = decltype(buf_tag)::value;
+      return *reinterpret_cast<const bf16x8*>(lds + BUF * 2 * OPB + (kk ? oA1 : oA0) + i * 2048);
+    };
+    auto rdB = [&](auto buf_tag, int kk, int j) -> bf16x8 {
+      constexpr int BUF = decltype(buf_tag)::value;
+      return *reinterpret_cast<const bf16x8*>(lds + BUF * 2 * OPB + (kk ? oB1 : oB0) + j * 2048);
+    };
+    // F0 (k 0-31) reads of a tile in the order its first MFMA run consumes them:
+    // B fragment 0 (the run's stationary operand), A 0-7, then B 1-7
+    auto rdF0 = [&](auto buf_tag, int q) {
+      if (q == 0) fb0[0] = rdB(buf_tag, 0, 0);
+      else if (q <= 8) fa0[q - 1] = rdA(buf_tag, 0, q - 1);
+      else fb0[q - 8] = rdB(buf_tag, 0, q - 8);
+    };
+    // ---- prologue: tiles 0 and 1 in flight, wait for tile 0, its F0 fragments
+    {
+      const Src s0 = srcs(0);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
+      const Src s1 = srcs(1);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) dma(s1, B1{}, p);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rdF0(B0{}, q);
+
+    // slot s = MFMA index in the tile (128); run r = s >> 3 keeps B fragment
+    // (r & 7) stationary over A fragments 0-7, k half s >> 6.
+    //   s  0-14 (even)  F1 A reads           s 23        lgkmcnt(0), barrier 1
+    //   s 24-45 (÷3)    A pieces of t+2      s 25-46 (÷3) F1 B reads
+    //   s 51            lgkmcnt(0), barrier 2
+    //   s 52-87 (÷5)    B pieces of t+2      s 93        vmcnt(t+2 pieces), barrier 3
+    //   s 94-124 (even) F0 reads of t+1 (other buffer)
+    auto tile3 = [&](int t, auto buf_tag, auto first_tag, auto more_tag, auto load_tag) {
+      constexpr int BUF = decltype(buf_tag)::value;
+      constexpr bool FIRST = decltype(first_tag)::value;
+      constexpr bool MORE = decltype(more_tag)::value;
+      constexpr bool LOAD = decltype(load_tag)::value;
+      using NB = std::integral_constant<int, BUF ^ 1>;
+      using SB = std::integral_constant<int, BUF>;
+      Src sn2{};
+      if constexpr (LOAD) sn2 = srcs(t + 2);
+      static_for<128>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        constexpr int i = s & 7, j = (s >> 3) & 7;
+        if constexpr (s < 64) {
+          if constexpr (FIRST) mma0(acc[i][j], fb0[j], fa0[i]);
+          else mma(acc[i][j], fb0[j], fa0[i]);
+        } else {
+          mma(acc[i][j], fb1[j], fa1[i]);
+        }
+        if constexpr (s < 16 && (s & 1) == 0) fa1[s >> 1] = rdA(SB{}, 1, s >> 1);
+        if constexpr (LOAD && s == 23) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (LOAD && s >= 24 && s < 48 && (s - 24) % 3 == 0) dma(sn2, SB{}, (s - 24) / 3);
+        if constexpr (s >= 25 && s < 49 && (s - 25) % 3 == 0) fb1[(s - 25) / 3] = rdB(SB{}, 1, (s - 25) / 3);
+        if constexpr (LOAD && s == 51) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (LOAD && s >= 52 && s < 92 && (s - 52) % 5 == 0) dma(sn2, SB{}, 8 + (s - 52) / 5);
+        if constexpr (MORE && s == 93) {
+          // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in flight)
+          if constexpr (LOAD) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (MORE && s >= 94 && s < 126 && (s & 1) == 0) rdF0(NB{}, (s - 94) >> 1);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    // nk is even and ≥ 4 (host contract)
+    tile3(0, B0{}, T_{}, T_{}, T_{});
+    tile3(1, B1{}, F_{}, T_{}, T_{});
+    for (int t = 2; t < nk - 2; t += 2) {
+      tile3(t, B0{}, F_{}, T_{}, T_{});
+      tile3(t + 1, B1{}, F_{}, T_{}, T_{});
+    }
+    tile3(nk - 2, B0{}, F_{}, T_{}, F_{});
+    tile3(nk - 1, B1{}, F_{}, F_{}, F_{});
+  } else {
   // ---- prologue: tile 0 → buffer 0, F0 of tile 0
   {
     const Src s0 = srcs(0);
@@ -281,6 +437,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   }
   tile(nk - 2, B0{}, T_{}, F_{}, T_{}, F_{});
   tile(nk - 1, B1{}, F_{}, F_{}, F_{}, F_{});
+  }  // SCHED
 
   // ---- epilogue ----
   // The accumulators leave the accumulator file through explicit
@@ -297,6 +454,115 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
                  : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
     return v;
   };
+  if constexpr (SCHED == 1) {
+    // ---- register epilogue: no LDS round trip, no barrier.  Per 16-row block
+    // i and 4-block column group h, the 4 lanes {r, r+16, r+32, r+48} hold a
+    // 4×4 matrix of 4-column pieces; transpose_blocks leaves each lane 16
+    // contiguous columns (two 16-B stores).  The stores of a tile leave while
+    // the workgroup drains, so the next tile's DMA prologue starts without the
+    // LDS staging pass (2 barriers, 128 KiB of LDS writes + reads).
+    const int q = lane >> 4, rr = lane & 15;
+    auto rowp = [&](int i) { return (size_t)(m0 + wm * 128 + 16 * i + rr); };
+    auto colb = [&](int h) { return n0 + wn * 128 + 16 * (4 * h + q); };  // first of the lane's 16 columns
+    bf16x8 pre[EPI == 3 ? 32 : 1];
+    if constexpr (EPI == 3) {
+      // pre-activation rows first: their latency hides behind the transposes
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            pre[(i * 2 + h) * 2 + c] = *reinterpret_cast<const bf16x8*>(Y + rowp(i) * ldy + colb(h) + 8 * c);
+    }
+    f32x8 bv[EPI >= 2 ? 4 : 1];
+    if constexpr (EPI >= 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) bv[h * 2 + c] = to_f32(*reinterpret_cast<const bf16x8*>(bias + colb(h) + 8 * c));
+    }
+    f32x8 colp[EPI == 3 ? 4 : 1];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) colp[u] = f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    }
+    f32x2 m1 = {-1.f, -1.f};
+    asm volatile("" : "+v"(m1));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u32x2 b[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          f32x4 a = rd_acc(acc[i][4 * h + jj]);
+          if constexpr (EPI == 1) {
+            const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * 128 + 16 * (4 * h + jj) + 4 * q);
+            a += f32x4{(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
+          }
+          b[jj] = pack4(a);
+        }
+        transpose_blocks(b);
+        const bf16x8 v[2] = {join(b[0], b[1]), join(b[2], b[3])};
+        bf16* crow = C + rowp(i) * ldc + colb(h);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          if constexpr (EPI <= 1) {
+            *reinterpret_cast<bf16x8*>(crow + 8 * c) = v[c];
+          } else if constexpr (EPI == 2) {
+            *reinterpret_cast<bf16x8*>(crow + 8 * c) = v[c];
+            const f32x8 x = to_f32(v[c]) + bv[h * 2 + c];
+            f32x8 y;
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const f32x2 g = gelu_sig2(f32x2{x[e], x[e + 1]});
+              y[e] = g[0];
+              y[e + 1] = g[1];
+            }
+            *reinterpret_cast<bf16x8*>(Y + rowp(i) * ldy + colb(h) + 8 * c) = to_bf16(y);
+          } else {
+            const f32x8 x = to_f32(pre[(i * 2 + h) * 2 + c]) + bv[h * 2 + c];
+            const f32x8 dy = to_f32(v[c]);
+            f32x8 d;
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const f32x2 g = f32x2{dy[e], dy[e + 1]} * gelu_sig_grad2(f32x2{x[e], x[e + 1]}, m1);
+              d[e] = g[0];
+              d[e + 1] = g[1];
+            }
+            colp[h * 2 + c] += d;
+            *reinterpret_cast<bf16x8*>(crow + 8 * c) = to_bf16(d);
+          }
+        }
+      }
+    }
+    if constexpr (EPI == 3) {
+      // fp32 column partials: the 16 row lanes of a column group reduce in
+      // fours (xor 1, 2); partial row 4·wm + (rr >> 2) of this M-tile's 8
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float s = colp[u][e];
+          s += __shfl_xor(s, 1);
+          s += __shfl_xor(s, 2);
+          colp[u][e] = s;
+        }
+      if ((rr & 3) == 0) {
+        float* prow = dbias_part + (size_t)(8 * tm + 4 * wm + (rr >> 2)) * N;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const f32x8 s = colp[h * 2 + c];
+            *reinterpret_cast<f32x4*>(prow + colb(h) + 8 * c) = f32x4{s[0], s[1], s[2], s[3]};
+            *reinterpret_cast<f32x4*>(prow + colb(h) + 8 * c + 4) = f32x4{s[4], s[5], s[6], s[7]};
+          }
+      }
+    }
+    return;
+  }
   // acc[i][j][e] = C[m][n], m = wm·128 + 16i + (l&15), n = wn·128 + 16j + 4(l>>4) + e.
   // Staged through LDS as bf16 [256][256] (chunk c of row m at c ^ (m & 31))
   // and written back as whole 512-B rows, 16 B per lane.
@@ -390,13 +656,14 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
     const int g = e ? atoi(e) : 8;
     return g >= 1 ? g : 1;
   }();
-  auto launch = [&](auto gpg, auto bar, auto bufld) {
+  auto launch = [&](auto gpg, auto bar, auto bufld, auto sched) {
     constexpr int G = decltype(gpg)::value, R = decltype(bar)::value, L = decltype(bufld)::value;
+    constexpr int S = decltype(sched)::value;
     switch (epi) {
-      case 0: gemm_nt4_kernel<0, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
-      case 1: gemm_nt4_kernel<1, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
-      case 2: gemm_nt4_kernel<2, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
-      case 3: gemm_nt4_kernel<3, G, R, L><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 0: gemm_nt4_kernel<0, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 1: gemm_nt4_kernel<1, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 2: gemm_nt4_kernel<2, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 3: gemm_nt4_kernel<3, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       default: return -4;
     }
     return 0;
@@ -412,12 +679,14 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   // 0 = barrier after block-1 group 11, the first 4 DMA pieces of tile t+2 after it, the rest one per
   // block-0 group, B-stationary MFMA order (each group's 4 MFMAs share SrcA; default: 1-4 % faster
   // than the A-stationary order of variant 4 on qkv_fwd / proj_dx, bit-identical)
+  // 5 = SCHED 1 (three barriers, operand-split refill)
   switch (variant) {
-    case 1: return launch(I1{}, I7{}, I0{});
-    case 2: return launch(I2{}, I7{}, I0{});   // every piece of tile t+2 right after tile t's barrier
-    case 3: return launch(I4{}, I11{}, I0{});  // the same, 4 per group after a later barrier
-    case 4: return launch(I1{}, I11{}, I0{});  // variant 0 with the A-stationary order
-    default: return launch(I1{}, I11{}, I2{});
+    case 1: return launch(I1{}, I7{}, I0{}, I0{});
+    case 2: return launch(I2{}, I7{}, I0{}, I0{});   // every piece of tile t+2 right after tile t's barrier
+    case 3: return launch(I4{}, I11{}, I0{}, I0{});  // the same, 4 per group after a later barrier
+    case 4: return launch(I1{}, I11{}, I0{}, I0{});  // variant 0 with the A-stationary order
+    case 5: return launch(I1{}, I11{}, I2{}, I1{});
+    default: return launch(I1{}, I11{}, I2{}, I0{});
   }
   return 0;
 }

@@ -4,11 +4,16 @@
 //   cmake -DPDO_SANITIZE=address,undefined …   /  -DPDO_SANITIZE=thread …
 // (the reference runs no race detector; pdo runs these and the
 // multi-worker controller stress below under TSan in CI.)
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <cstdio>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -16,6 +21,7 @@
 #include "builders.h"
 #include "cluster.h"
 #include "http.h"
+#include "k8s.h"
 #include "kvclient.h"
 #include "kvstore.h"
 #include "planner.h"
@@ -258,6 +264,318 @@ static void test_websocket_and_keepalive() {
   srv.stop();
 }
 
+// ---------------------------------------------------------------- raw-socket fixtures
+// A scripted TCP server with no pdo HTTP code in it: connection n is handed to
+// script(n, fd).  Used to replay hand-built kube-apiserver responses
+// (csrc/tests/fixtures/k8s) and to misbehave in ways the pdo server never does.
+#ifndef PDO_FIXTURE_DIR
+#define PDO_FIXTURE_DIR "csrc/tests/fixtures"
+#endif
+
+static std::string fixture(const std::string& rel) {
+  FILE* f = fopen((std::string(PDO_FIXTURE_DIR) + "/" + rel).c_str(), "rb");
+  if (!f) {
+    fprintf(stderr, "missing fixture %s\n", rel.c_str());
+    ++g_fail;
+    return "";
+  }
+  std::string s;
+  char buf[4096];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+  fclose(f);
+  while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
+  return s;
+}
+
+struct RawServer {
+  int lfd = -1, port = 0;
+  std::thread th;
+  std::atomic<bool> stop{false};
+  std::vector<std::string> requests;  // request heads in arrival order
+  std::mutex mu;
+  explicit RawServer(std::function<void(RawServer&, int n, int fd)> script) {
+    lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    ::bind(lfd, (sockaddr*)&a, sizeof a);
+    ::listen(lfd, 16);
+    socklen_t len = sizeof a;
+    getsockname(lfd, (sockaddr*)&a, &len);
+    port = ntohs(a.sin_port);
+    th = std::thread([this, script] {
+      for (int n = 0; !stop; ++n) {
+        pollfd p{lfd, POLLIN, 0};
+        if (::poll(&p, 1, 50) != 1) {
+          --n;
+          continue;
+        }
+        int fd = ::accept(lfd, nullptr, nullptr);
+        if (fd < 0) break;
+        script(*this, n, fd);
+        ::close(fd);
+      }
+    });
+  }
+  ~RawServer() {
+    stop = true;
+    th.join();
+    ::close(lfd);
+  }
+  std::string url() const { return "http://127.0.0.1:" + std::to_string(port); }
+  // one request (head + Content-Length body); "" when the peer closed
+  std::string read_request(int fd) {
+    std::string buf;
+    char tmp[4096];
+    size_t he;
+    while ((he = buf.find("\r\n\r\n")) == std::string::npos) {
+      ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+      if (r <= 0) return "";
+      buf.append(tmp, (size_t)r);
+    }
+    size_t cl = 0, p = buf.find("Content-Length: ");
+    if (p != std::string::npos && p < he) cl = (size_t)atol(buf.c_str() + p + 16);
+    while (buf.size() < he + 4 + cl) {
+      ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+      if (r <= 0) break;
+      buf.append(tmp, (size_t)r);
+    }
+    std::lock_guard<std::mutex> g(mu);
+    requests.push_back(buf.substr(0, buf.find("\r\n")));
+    return buf;
+  }
+  static void send_all(int fd, const std::string& s) {
+    size_t off = 0;
+    while (off < s.size()) {
+      ssize_t w = ::send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+      if (w <= 0) return;
+      off += (size_t)w;
+    }
+  }
+  static void respond(int fd, int code, const std::string& reason, const std::string& body, bool keep) {
+    send_all(fd, "HTTP/1.1 " + std::to_string(code) + " " + reason +
+                     "\r\nContent-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) +
+                     (keep ? "\r\nConnection: keep-alive" : "\r\nConnection: close") + "\r\n\r\n" + body);
+  }
+  // a watch response: chunked, one chunk per line (as the apiserver flushes events)
+  static void stream(int fd, const std::string& jsonl, bool terminate) {
+    send_all(fd, "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n");
+    size_t s = 0;
+    while (s < jsonl.size()) {
+      size_t e = jsonl.find('\n', s);
+      if (e == std::string::npos) e = jsonl.size();
+      const std::string line = jsonl.substr(s, e - s) + "\n";
+      char hex[16];
+      snprintf(hex, sizeof hex, "%zx", line.size());
+      send_all(fd, std::string(hex) + "\r\n" + line + "\r\n");
+      s = e + 1;
+    }
+    if (terminate) send_all(fd, "0\r\n\r\n");
+  }
+};
+
+// a reused keep-alive connection whose server reads a POST and then
+// closes without replying must NOT replay the POST on a fresh connection (it may
+// have been applied); a GET in the same situation is retried.
+static void test_keepalive_retry_only_idempotent() {
+  std::atomic<int> posts{0}, gets{0};
+  RawServer srv([&](RawServer& s, int n, int fd) {
+    if (n == 0) {  // GET answered with keep-alive, then the POST read and dropped
+      s.read_request(fd);
+      RawServer::respond(fd, 200, "OK", "{}", true);
+      if (s.read_request(fd).rfind("POST", 0) == 0) ++posts;
+      return;  // close without a reply
+    }
+    if (n == 1) {  // a fresh connection: GET, keep-alive; then a GET read and dropped
+      s.read_request(fd);
+      RawServer::respond(fd, 200, "OK", "{}", true);
+      if (s.read_request(fd).rfind("GET", 0) == 0) ++gets;
+      return;
+    }
+    std::string r = s.read_request(fd);  // the retried GET (or a replayed POST: counted)
+    if (r.rfind("POST", 0) == 0) ++posts;
+    if (r.rfind("GET", 0) == 0) ++gets;
+    RawServer::respond(fd, 200, "OK", "{\"retried\":true}", false);
+  });
+  pdo::http::ClientOptions o;
+  o.timeout_s = 5;
+  CHECK(pdo::http::request("GET", srv.url() + "/a", "", o).status == 200);
+  auto p = pdo::http::request("POST", srv.url() + "/lease/grant", "{\"TTL\":5}", o);
+  CHECK(p.status == 0 && !p.error.empty());  // surfaced to the caller, not replayed
+  CHECK(pdo::http::request("GET", srv.url() + "/b", "", o).status == 200);
+  auto g = pdo::http::request("GET", srv.url() + "/c", "", o);
+  CHECK(g.status == 200 && g.body.find("retried") != std::string::npos);
+  CHECK(posts == 1);
+  CHECK(gets == 2);
+}
+
+// Status bodies of a real apiserver → the controller's ApiError codes
+// (AlreadyExists is "create raced, already there", Conflict is "re-read and retry")
+static void test_k8s_status_fixtures() {
+  const std::string exists = fixture("k8s/status_409_already_exists.json");
+  const std::string conflict = fixture("k8s/status_409_conflict.json");
+  const std::string notfound = fixture("k8s/status_404_not_found.json");
+  const std::string invalid = fixture("k8s/status_422_invalid.json");
+  RawServer srv([&](RawServer& s, int, int fd) {
+    const std::string r = s.read_request(fd);
+    if (r.rfind("POST", 0) == 0 && r.find("paddlejobs") != std::string::npos)
+      RawServer::respond(fd, 409, "Conflict", exists, false);
+    else if (r.rfind("PUT", 0) == 0 && r.find("/status") != std::string::npos)
+      RawServer::respond(fd, 409, "Conflict", conflict, false);
+    else if (r.rfind("PUT", 0) == 0)
+      RawServer::respond(fd, 422, "Unprocessable Entity", invalid, false);
+    else
+      RawServer::respond(fd, 404, "Not Found", notfound, false);
+  });
+  pdo::k8s::Config c;
+  c.server = srv.url();
+  pdo::k8s::RestApi api(c);
+  Value j = job("resnet", 0, 2);
+  auto code_of = [](const std::function<void()>& f) {
+    try {
+      f();
+    } catch (const pdo::store::ApiError& e) {
+      return (int)e.code;
+    }
+    return -1;
+  };
+  CHECK(code_of([&] { api.create("PaddleJob", j); }) == (int)pdo::store::ApiError::AlreadyExists);
+  CHECK(code_of([&] { api.update_status("PaddleJob", j); }) == (int)pdo::store::ApiError::Conflict);
+  CHECK(code_of([&] { api.update("PaddleJob", j); }) == (int)pdo::store::ApiError::Invalid);
+  CHECK(code_of([&] { api.get("Pod", "default", "resnet-worker-7"); }) == (int)pdo::store::ApiError::NotFound);
+  // the request paths the apiserver routes on
+  std::lock_guard<std::mutex> g(srv.mu);
+  CHECK(srv.requests.size() == 4);
+  if (srv.requests.size() == 4) {
+    CHECK(srv.requests[0] == "POST /apis/batch.paddlepaddle.org/v1/namespaces/default/paddlejobs HTTP/1.1");
+    CHECK(srv.requests[1] == "PUT /apis/batch.paddlepaddle.org/v1/namespaces/default/paddlejobs/resnet/status HTTP/1.1");
+    CHECK(srv.requests[3] == "GET /api/v1/namespaces/default/pods/resnet-worker-7 HTTP/1.1");
+  }
+}
+
+// the informer against a scripted LIST / WATCH sequence: a watch that ends
+// cleanly resumes from the BOOKMARK's resourceVersion (no relist); an ERROR 410
+// Expired event relists; every event lands in the mirrored cache
+static void test_k8s_watch_fixtures() {
+  const std::string l100 = fixture("k8s/podlist_rv100.json"), l200 = fixture("k8s/podlist_rv200.json");
+  const std::string w100 = fixture("k8s/watch_rv100.jsonl"), w150 = fixture("k8s/watch_rv150_expired.jsonl");
+  std::atomic<int> lists{0};
+  RawServer srv([&](RawServer& s, int, int fd) {
+    const std::string r = s.read_request(fd);
+    const std::string head = r.substr(0, r.find("\r\n"));
+    if (head.find("watch=true") == std::string::npos) {
+      RawServer::respond(fd, 200, "OK", lists++ == 0 ? l100 : l200, false);
+    } else if (head.find("resourceVersion=100") != std::string::npos) {
+      RawServer::stream(fd, w100, true);  // server-side timeout: the stream just ends
+    } else if (head.find("resourceVersion=150") != std::string::npos) {
+      RawServer::stream(fd, w150, true);
+    } else {
+      usleep(20000);
+      RawServer::stream(fd, "", true);  // quiet watches from rv 200 on
+    }
+  });
+  pdo::k8s::Config c;
+  c.server = srv.url();
+  pdo::k8s::RestApi api(c);
+  pdo::store::Store cache;
+  pdo::k8s::Informer inf(&api, &cache, "Pod", "default");
+  inf.watch_timeout_s = 5;
+  inf.start();
+  for (int i = 0; i < 300 && inf.lists() < 2; ++i) usleep(10000);
+  for (int i = 0; i < 100 && inf.watches() < 4; ++i) usleep(10000);
+  inf.stop();
+  std::vector<std::string> reqs;
+  {
+    std::lock_guard<std::mutex> g(srv.mu);
+    reqs = srv.requests;
+  }
+  CHECK(reqs.size() >= 5);
+  if (reqs.size() >= 5) {
+    CHECK(reqs[0].find("watch=true") == std::string::npos);
+    CHECK(reqs[1].find("watch=true") != std::string::npos && reqs[1].find("resourceVersion=100") != std::string::npos);
+    CHECK(reqs[2].find("resourceVersion=150") != std::string::npos);  // resumed from the BOOKMARK
+    CHECK(reqs[3].find("watch=true") == std::string::npos);           // 410 Expired → relist
+    CHECK(reqs[4].find("resourceVersion=200") != std::string::npos);
+  }
+  CHECK(inf.lists() == 2);
+  // after the relist only worker-0 (with the relisted label) remains; worker-1
+  // was ADDED then DELETED by the watches
+  auto pods = cache.list("Pod");
+  CHECK(pods.size() == 1);
+  if (pods.size() == 1) {
+    CHECK(pods[0].at_path("metadata.name").str() == "resnet-worker-0");
+    CHECK(pods[0].at_path("metadata.labels.relisted").str() == "yes");
+    CHECK(pods[0].get("kind").str() == "Pod");
+  }
+  // the event function on its own: BOOKMARK moves rv only, ERROR 410 ends the stream
+  pdo::store::Store c2;
+  std::string rv = "100";
+  bool gone = false;
+  size_t s = 0;
+  int applied = 0;
+  while (s < w100.size()) {
+    size_t e = w100.find('\n', s);
+    if (e == std::string::npos) e = w100.size();
+    applied += pdo::k8s::apply_watch_event(w100.substr(s, e - s), &c2, "Pod", &rv, &gone);
+    s = e + 1;
+  }
+  CHECK(applied == 3 && rv == "150" && !gone && c2.list("Pod").size() == 2);
+  CHECK(!pdo::k8s::apply_watch_event(w150.substr(w150.find('\n') + 1), &c2, "Pod", &rv, &gone) && gone);
+  CHECK(pdo::k8s::apply_watch_event("not json", &c2, "Pod", &rv, &gone));  // a torn line is skipped
+}
+
+// pods/exec over WebSocket against hand-assembled server frames (RFC 6455
+// framing, unmasked; v5.channel.k8s.io): a fragmented stdout message, a ping
+// mid-stream (must be answered), a 16-bit-length stderr frame, the channel-3
+// Status of a command that exited 3, then a close frame
+static void test_k8s_exec_v5_fixture() {
+  const std::string status = fixture("k8s/exec_status_exit3.json");
+  std::atomic<bool> got_pong{false};
+  RawServer srv([&](RawServer& s, int, int fd) {
+    const std::string r = s.read_request(fd);
+    size_t k = r.find("Sec-WebSocket-Key: ");
+    const std::string key = r.substr(k + 19, r.find("\r\n", k) - k - 19);
+    RawServer::send_all(fd, "HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+                            "Sec-WebSocket-Accept: " + pdo::http::ws_accept_key(key) +
+                                "\r\nSec-WebSocket-Protocol: v5.channel.k8s.io\r\n\r\n");
+    auto frame = [](unsigned char b0, const std::string& payload) {
+      std::string f(1, (char)b0);
+      if (payload.size() < 126) {
+        f.push_back((char)payload.size());
+      } else {
+        f.push_back((char)126);
+        f.push_back((char)(payload.size() >> 8));
+        f.push_back((char)(payload.size() & 0xff));
+      }
+      return f + payload;
+    };
+    RawServer::send_all(fd, frame(0x82, std::string(1, '\x01')));          // stream init (channel byte only)
+    RawServer::send_all(fd, frame(0x02, std::string("\x01") + "hel"));      // binary, FIN = 0
+    RawServer::send_all(fd, frame(0x89, "hb"));                             // ping between fragments
+    RawServer::send_all(fd, frame(0x80, "lo\n"));                           // continuation, FIN = 1
+    RawServer::send_all(fd, frame(0x82, std::string("\x02") + std::string(300, 'e')));
+    RawServer::send_all(fd, frame(0x82, std::string("\x03") + status));
+    RawServer::send_all(fd, frame(0x88, std::string("\x03\xe8", 2)));      // close 1000
+    // the client's pong (masked, opcode 0xA) arrives before its close
+    char buf[512];
+    ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+    if (n >= 2 && ((unsigned char)buf[0] & 0x0f) == 0x0a) got_pong = true;
+    usleep(20000);
+  });
+  pdo::http::ClientOptions o;
+  o.timeout_s = 5;
+  auto r = pdo::http::ws_exec(srv.url() + "/api/v1/namespaces/default/pods/p/exec?container=c&command=sh", o);
+  CHECK(r.protocol == "v5.channel.k8s.io");
+  CHECK(r.out == "hello\n");
+  CHECK(r.err == std::string(300, 'e'));
+  CHECK(!r.ok && r.exit_code == 3);
+  CHECK(r.error.find("exit code 3") != std::string::npos);
+  CHECK(got_pong);
+}
+
 static void test_yaml() {
   const char* y = R"(apiVersion: v1
 clusters:
@@ -323,6 +641,10 @@ int main() {
   test_workqueue();
   test_kv_and_http();
   test_websocket_and_keepalive();
+  test_keepalive_retry_only_idempotent();
+  test_k8s_status_fixtures();
+  test_k8s_watch_fixtures();
+  test_k8s_exec_v5_fixture();
   test_yaml();
   test_cluster_sim_multiworker();
   test_cluster_without_controller();

@@ -88,7 +88,7 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
         ref = hip.gemm_nt(a, b, bias)
         ref_p, ref_y = hip.gemm_nt_gelu(a, b, bias)
         ref_dx, ref_db = hip.gemm_nt_dgelu(a, b, pre, bias)
-        for impl in (1, 2, 3, 4):
+        for impl in (1, 2, 3, 4, 5, 6):
             hip.gemm_nt_impl(impl)
             assert torch.equal(hip.gemm_nt(a, b, bias), ref), impl
             p, y = hip.gemm_nt_gelu(a, b, bias)
@@ -101,3 +101,24 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
         torch.testing.assert_close(ref.float(), exact, rtol=2e-2, atol=6e-2)
     finally:
         hip.gemm_nt_impl(prev)
+
+
+@pytest.mark.parametrize("M,N,K,impl", [(65536, 4096, 1024, 1), (65536, 4096, 1024, 6),
+                                        (3328, 1024, 3072, 1), (3328, 1024, 3072, 6)])
+def test_nt4_production_shapes_vs_fp32(hip, M, N, K, impl):
+    """Production-size grids: M = 65536 (4096 tiles: XCD remap over every tile,
+    grouped order across 32 groups of 8 tile rows) and M = 3328 (13 tile rows,
+    tiles_m % 8 != 0: the last group is short), full output against fp32."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
+    bias = torch.empty(N, device="cuda", dtype=torch.bfloat16).uniform_(-0.1, 0.1, generator=g)
+    prev = hip.gemm_nt_impl(impl)
+    try:
+        c = hip.gemm_nt(a, b, bias)
+    finally:
+        hip.gemm_nt_impl(prev)
+    ref = torch.addmm(bias.float(), a.float(), b.float().t())
+    err = (c.float() - ref).abs()
+    tol = 1e-2 + 8e-3 * ref.abs()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.4f} at {int(err.argmax())}"

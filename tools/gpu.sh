@@ -1,0 +1,75 @@
+#!/bin/bash
+# The one gpurun driver: every GPU step is a subcommand, run under its own time
+# limit, chained with && so the first failure (fault, abort, timeout) ends the call.
+#
+#   gpurun --timeout 900 -- bash tools/gpu.sh NAME STEP [STEP ...]
+#
+# Outputs go to gpurun_out/NAME/.  A STEP is one shell word (quote it when it
+# has arguments); the arguments after ':' are split on spaces:
+#   tests[:K]           pytest -m gpu (-k K when given)
+#   smoke               __graft_entry__.smoke()
+#   'bench:ARGS'        bench.py --gpus 1 --steps 20 --warmup 5 (ARGS replace the defaults)
+#   'probe:SCRIPT ARGS' python tools/SCRIPT ARGS      (stdout -> NAME/probe_SCRIPT.log)
+#   'prof:SCRIPT ARGS'  rocprofv3 --kernel-trace --stats of python tools/SCRIPT ARGS,
+#                       summarised by tools/prof_summary.py (-> NAME/prof_SCRIPT.md)
+#   'pmc:CTRS SCRIPT ARGS'  one rocprofv3 --pmc pass (CTRS joined by '+') over tools/SCRIPT
+#   step                prof of the GPT-2-medium training step (tools/train_probe.py)
+#   env:K=V             export K=V for the following steps
+set -o pipefail
+NAME=${1:?name}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$NAME; mkdir -p "$O"
+export TMPDIR=/tmp
+cd "$R" || exit 1
+PMC_PASS=0
+say() { echo "[gpu.sh $(date +%H:%M:%S)] $*"; }
+
+run_step() {
+  local step=$1 kind=${1%%:*} arg=""
+  [[ $step == *:* ]] && arg=${step#*:}
+  read -r -a A <<< "$arg"
+  case $kind in
+    env) export "$arg"; say "env $arg" ;;
+    tests)
+      local k=(); [[ -n $arg ]] && k=(-k "$arg")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
+        > "$O/pytest_gpu.log" 2>&1 || { tail -60 "$O/pytest_gpu.log"; return 1; }
+      tail -3 "$O/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+        || { tail -40 "$O/smoke.log"; return 1; }
+      tail -2 "$O/smoke.log" ;;
+    bench)
+      local b=(--gpus 1 --steps 20 --warmup 5); [[ -n $arg ]] && b=("${A[@]}")
+      timeout -k 10 600 python bench.py "${b[@]}" > "$O/bench.json" 2> "$O/bench.err" \
+        || { tail -60 "$O/bench.err"; return 1; }
+      cat "$O/bench.json" ;;
+    probe)
+      local s=${A[0]}
+      timeout -k 10 600 python -u "tools/$s" "${A[@]:1}" > "$O/probe_${s%.py}.log" 2>&1 \
+        || { tail -40 "$O/probe_${s%.py}.log"; return 1; }
+      cat "$O/probe_${s%.py}.log" ;;
+    prof|step)
+      local s=${A[0]:-train_probe.py} rest=("${A[@]:1}")
+      [[ $kind == step ]] && { s=train_probe.py; rest=(--dist --steps 7 --warmup 2); }
+      local d=$O/prof_${s%.py}
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 "$R/tools/$s" "${rest[@]}" ) \
+        > "$O/prof_${s%.py}.log" 2>&1 || { tail -30 "$O/prof_${s%.py}.log"; return 1; }
+      local db; db=$(find "$d" -name '*.db' | head -1)
+      local steps=1; [[ $kind == step ]] && steps=7
+      python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/prof_${s%.py}.md" && rm -rf "$d"
+      tail -5 "$O/prof_${s%.py}.log"; head -45 "$O/prof_${s%.py}.md" ;;
+    pmc)
+      PMC_PASS=$((PMC_PASS + 1))
+      local ctr=${A[0]//+/ } s=${A[1]} p=$O/pmc${PMC_PASS}_${A[1]%.py}
+      ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d "$p" -o run -- python3 "$R/tools/$s" "${A[@]:2}" ) \
+        > "$p.log" 2>&1 || { tail -30 "$p.log"; return 1; }
+      python3 tools/pmc_summary.py $(find "$p" -name "*.db") > "$p.md" 2>&1 && rm -rf "$p"; head -60 "$p.md" ;;
+    *) say "unknown step $step"; return 2 ;;
+  esac
+}
+
+for st in "$@"; do
+  say "step $st"
+  run_step "$st" || { say "step $st failed"; exit 1; }
+done
+say "done"
