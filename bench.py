@@ -86,8 +86,14 @@ def parse_args(argv=None):
                     help="per-rank batch (default 64 sequences for gpt2, 256 images for resnet50)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--ready-trials", type=int, default=10)
-    ap.add_argument("--compat-trials", type=int, default=0,
-                    help="extra ready trials in the reference-equivalent compat mode")
+    ap.add_argument("--compat-trials", type=int, default=3,
+                    help="ready trials in the reference-equivalent compat mode (the record's compat_ready)")
+    ap.add_argument("--train-ready-trials", type=int, default=5,
+                    help="ready trials of the headline workload itself (GPT-2 / ResNet ranks: model built on "
+                         "the GPU and its initial weights broadcast, then ready) — the record's ready_train")
+    ap.add_argument("--b2b-trials", type=int, default=5,
+                    help="noop ready trials created back to back, without waiting for the node's warm slots "
+                         "to re-warm (the record's ready_b2b)")
     ap.add_argument("--mode", default="fast", choices=["fast", "compat"])
     ap.add_argument("--no-zygote", action="store_true", help="cold interpreter per rank")
     ap.add_argument("--no-warm-slots", action="store_true",
@@ -97,6 +103,10 @@ def parse_args(argv=None):
                     help="node agent GPU exposure: all = every rank sees the node's GPUs and selects its own "
                          "(PDO_GPU_IDS, as torchrun-style launches; RCCL sees xGMI peers as local devices); "
                          "isolate = HIP_VISIBLE_DEVICES per pod, as a Kubernetes device plugin")
+    ap.add_argument("--pod-layout", choices=["per-gpu", "one-pod"], default=os.environ.get("PDO_POD_LAYOUT", "per-gpu"),
+                    help="per-gpu = N pods × 1 amd.com/gpu (the reference's layout, deploy/examples/resnet.yaml); "
+                         "one-pod = 1 pod × N amd.com/gpu running --nproc-per-pod N local ranks (the Kubernetes "
+                         "xGMI layout: under a device plugin only GPUs of one pod see each other)")
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
@@ -111,7 +121,7 @@ def parse_args(argv=None):
 class Launcher:
     """One in-process local backend; launches PaddleJobs and reads pdo-kv."""
 
-    def __init__(self, mode, zygote, gpus, sandbox, extra_args=()):
+    def __init__(self, mode, zygote, gpus, sandbox, extra_args=(), nproc=1):
         from paddle_operator_amd.controller import LocalCluster
         from paddle_operator_amd.kv.client import KVClient
 
@@ -120,6 +130,7 @@ class Launcher:
         self.sandbox = sandbox
         self.zygote = zygote
         self.extra_args = list(extra_args)
+        self.nproc = nproc  # ranks per pod (--nproc-per-pod; amd.com/gpu per pod)
         self.cl = LocalCluster(mode=mode, agent="exec", sandbox_root=sandbox,
                                nodes=[{"name": "node0", "gpus": gpus}],
                                kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote)
@@ -144,13 +155,16 @@ class Launcher:
         c = {"name": "paddle", "image": "pdo/launcher:rocm",
              "command": [os.path.join(REPO, "bin", "pdo-launch")] + list(args), "env": env}
         if self.gpus:
-            c["resources"] = {"limits": {T.AMD_GPU: 1}}
+            c["resources"] = {"limits": {T.AMD_GPU: self.nproc}}
         return c
 
     def launch(self, name, ranks, args, ops):
         from paddle_operator_amd.api import types as T
-        job = T.paddlejob(name, worker={"replicas": ranks,
-                                        "template": {"spec": {"containers": [self.container(list(args) + self.extra_args, ops)]}}},
+        args = list(args) + self.extra_args
+        if self.nproc > 1:
+            args += ["--nproc-per-pod", str(self.nproc)]
+        job = T.paddlejob(name, worker={"replicas": ranks // self.nproc,
+                                        "template": {"spec": {"containers": [self.container(args, ops)]}}},
                           clean_pod_policy="Always")
         t0 = time.time()
         self.cl.create(job)
@@ -196,10 +210,13 @@ class Launcher:
         self.cl.delete(T.KIND, name)
         self.cl.wait(lambda: self.cl.job(name) is None and not self.cl.pods(name), timeout=60)
 
-    def ready_trial(self, name, ranks, timeout):
-        if self.zygote and self.gpus and not self.cl.wait_warm(timeout=120):
+    def ready_trial(self, name, ranks, timeout, args=None, ops="torch", wait_warm=True):
+        """Create → the last rank's readiness record.  ``args``: the rank's
+        workload (default a noop rank); ``wait_warm``: start on an idle node
+        whose warm slots are all up (False: right after the previous job)."""
+        if wait_warm and self.zygote and self.gpus and not self.cl.wait_warm(timeout=120):
             log("warm slots not all up after 120 s; trial runs with what is there")
-        t0 = self.launch(name, ranks, ["--workload", "noop", "--exit-after-ready"], "torch")
+        t0 = self.launch(name, ranks, (args or ["--workload", "noop"]) + ["--exit-after-ready"], ops)
         rs = self.wait_records(name, "ready", ranks, timeout)
         self.finish(name)
         slow = max(rs, key=lambda r: r["t_ready"])
@@ -234,6 +251,18 @@ def _comm_summary(rs):
         return None
     out = {"ranks": len(cs), "allreduce_bytes": cs[0].get("allreduce_bytes"),
            "allreduce_busbw_GBps_min": min(c["allreduce_busbw_GBps"] for c in cs)}
+    # size sweep: the slowest rank per size (every rank times the same collectives)
+    sw = [c["allreduce_sweep"] for c in cs if c.get("allreduce_sweep")]
+    if sw:
+        out["allreduce_sweep"] = [{"bytes": p["bytes"], "busbw_GBps": min(s[i]["busbw_GBps"] for s in sw),
+                                   "us": max(s[i]["us"] for s in sw)} for i, p in enumerate(sw[0])]
+        best = max(p["busbw_GBps"] for p in out["allreduce_sweep"])
+        out["knee_bytes"] = next(p["bytes"] for p in out["allreduce_sweep"] if p["busbw_GBps"] >= 0.9 * best)
+    if cs[0].get("buckets"):
+        out["buckets"] = cs[0]["buckets"]
+    ipc = [c["ipc_gbps"] for c in cs if "ipc_gbps" in c]
+    if ipc:
+        out["ipc_gbps"] = ipc
     ex = [c["exposed_ms"] for c in cs if "exposed_ms" in c]
     if ex:
         out["exposed_ms_max"] = max(ex)
@@ -273,7 +302,8 @@ def orchestrate(a):
         os.environ["PDO_WARM_SLOTS"] = "0"  # read by the agent when it starts the zygote
     out = {}
     try:
-        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode), extra_args)
+        nproc = N if a.pod_layout == "one-pod" else 1
+        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode), extra_args, nproc)
         try:
             trials = []
             for t in range(a.ready_trials):
@@ -281,6 +311,11 @@ def orchestrate(a):
             out["ready"] = ready_stats(trials) if trials else None
             if trials:
                 log(f"ready p50 {out['ready']['p50']}s over {len(trials)} trials ({N} ranks)")
+            if a.b2b_trials and not a.ready_only:
+                bt = [L.ready_trial(f"b2b-{t}", N, a.timeout, wait_warm=False) for t in range(a.b2b_trials)]
+                out["ready_b2b"] = ready_stats(bt)
+                log(f"back-to-back ready p50 {out['ready_b2b']['p50']}s "
+                    f"(warm-slot fraction {out['ready_b2b']['warm_slot_fraction']})")
             if a.ready_only:
                 print(json.dumps({"metric": "job-start->all-ranks-ready p50", "unit": "s", "n_gpus": N,
                                   "mode": a.mode, "zygote": not a.no_zygote, "ready": out.get("ready"),
@@ -298,6 +333,12 @@ def orchestrate(a):
                 wl = ["--workload", "gpt2", "--model", a.model, "--batch", str(a.micro_batch), "--seq", str(a.seq)]
             else:
                 wl = ["--workload", "resnet50", "--batch", str(a.micro_batch)] + (["--tiny"] if a.tiny else [])
+            if a.train_ready_trials:
+                # ready-to-train: the headline workload's ranks, model built and weights broadcast
+                tt = [L.ready_trial(f"train-ready-{t}", N, a.timeout, args=list(wl), ops=a.ops)
+                      for t in range(a.train_ready_trials)]
+                out["ready_train"] = ready_stats(tt)
+                log(f"ready-to-train p50 {out['ready_train']['p50']}s over {len(tt)} {a.workload} jobs")
             wl += ["--steps", str(a.steps), "--warmup", str(a.warmup), "--bench", "--timeout", "600"]
             t0 = L.launch(name, N, wl, a.ops)
             rs = L.wait_records(name, "bench", N, a.timeout)
@@ -307,7 +348,7 @@ def orchestrate(a):
         finally:
             L.stop()
         if a.compat_trials:
-            C = Launcher("compat", False, gpus, os.path.join(sandbox, "compat"), extra_args)
+            C = Launcher("compat", False, gpus, os.path.join(sandbox, "compat"), extra_args, nproc)
             try:
                 ct = [C.ready_trial(f"compat-{t}", N, a.timeout) for t in range(a.compat_trials)]
             finally:
@@ -329,13 +370,18 @@ def orchestrate(a):
         "vs_baseline": None,  # BASELINE.json publishes no number ("published": {})
         "dtype": "bf16",
     }
-    launch = (f"PaddleJob worker.replicas={N}, planner={a.mode}, zygote={not a.no_zygote}, "
+    pods = N if a.pod_layout == "per-gpu" else 1
+    launch = (f"PaddleJob worker.replicas={pods} x {N // pods} GPU, planner={a.mode}, zygote={not a.no_zygote}, "
               f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}, "
               f"gpu_visibility={os.environ.get('PDO_GPU_VISIBILITY', 'isolate') if gpus else 'cpu'}")
     extra = {
         "baseline_metric": BASELINE_METRIC,
         "ready_p50_s": out["ready"]["p50"] if out.get("ready") else None,
         "ready": out.get("ready"),
+        # the headline workload's own create → every rank past its initial weight broadcast
+        "ready_train": out.get("ready_train"),
+        # noop jobs created back to back (warm slots may still be re-warming)
+        "ready_b2b": out.get("ready_b2b"),
         "compat_ready": out.get("compat_ready"),
         "job_ready_s": round(out["bench_ready_s"], 3),
         "final_loss": rs[0].get("loss"),
@@ -352,7 +398,7 @@ def orchestrate(a):
                "data": "synthetic (on-device random tokens), random-init weights",
                "config": {"model": a.model, "global_batch": a.micro_batch * N, "micro_batch_per_gpu": a.micro_batch,
                           "seq_len": a.seq, "parallelism": f"dp{N}" + ("-shared-gpu-gloo" if a.rehearse_shared_gpu else ""),
-                          "launch": launch,
+                          "launch": launch, "pod_layout": f"{pods}x{N // pods}",
                           "grad_reduce": rs[0].get("grad_reduce"), "buckets": rs[0].get("buckets"), "ops": a.ops,
                           "device": dev},
                **extra,
@@ -365,6 +411,7 @@ def orchestrate(a):
                "data": "synthetic (on-device random 224x224 images and labels), random-init weights",
                "config": {"model": "resnet50", "global_batch": a.micro_batch * N, "micro_batch_per_gpu": a.micro_batch,
                           "resolution": 224, "parallelism": f"dp{N}", "launch": launch,
+                          "pod_layout": f"{pods}x{N // pods}",
                           "grad_reduce": rs[0].get("grad_reduce"), "buckets": rs[0].get("buckets"), "device": dev},
                **extra}
     print(json.dumps(rec), flush=True)

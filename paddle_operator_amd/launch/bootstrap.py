@@ -62,7 +62,7 @@ def _wait_port(host: str, port: int, timeout_s: float, poll: float = 0.002) -> b
     return False
 
 
-_STORE = []  # keeps rank 0's store (and its listening socket) alive for the job
+_STORE = []  # keeps rank 0's store (it owns the listening socket) alive for the job
 
 
 def _bound_store(host: str, port: int, world: int, timeout_s: int):
@@ -82,9 +82,17 @@ def _bound_store(host: str, port: int, world: int, timeout_s: int):
         ls.listen(1024)
     except OSError:
         return None
-    store = dist.TCPStore(host, port, world, True, datetime.timedelta(seconds=timeout_s),
-                          wait_for_workers=False, master_listen_fd=ls.fileno())
-    _STORE.append((store, ls))
+    # the descriptor's ownership moves to c10d's server: detached, the Python
+    # socket object can never close it a second time (a number the process
+    # may meanwhile have reused for something else)
+    fd = ls.detach()
+    try:
+        store = dist.TCPStore(host, port, world, True, datetime.timedelta(seconds=timeout_s),
+                              wait_for_workers=False, master_listen_fd=fd)
+    except BaseException:
+        os.close(fd)
+        raise
+    _STORE.append(store)
     return store
 
 
@@ -192,7 +200,7 @@ def ipc_probe_run(dev: torch.device, nbytes: int = 64 << 20) -> dict:
 
 def report_ready(b: Bootstrapped, job_key: str, kv_endpoints: str = "", extra: Optional[dict] = None):
     b.t_ready = time.time()
-    rec = {"rank": b.rank, "world": b.world, "t_start": b.t_start, "t_pg": b.t_pg, "t_ready": b.t_ready,
+    rec = {"rank": b.rank, "world": b.world, "local_rank": b.local_rank, "t_start": b.t_start, "t_pg": b.t_pg, "t_ready": b.t_ready,
            "host": socket.gethostname(), "pid": os.getpid(), "backend": b.backend}
     if os.environ.get("PDO_ELASTIC_GEN"):
         rec["gen"] = os.environ["PDO_ELASTIC_GEN"]

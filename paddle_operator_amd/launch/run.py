@@ -35,7 +35,10 @@ def parse_args(argv=None):
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--tiny", action="store_true", help="tiny model variant (CPU tests)")
     ap.add_argument("--backend", default=None, help="nccl (RCCL) | gloo; default by device")
-    ap.add_argument("--nproc-per-pod", type=int, default=1)
+    ap.add_argument("--nproc-per-pod", type=int, default=int(os.environ.get("PDO_NPROC_PER_POD", "1") or 1),
+                    help="ranks this pod runs, one per GPU it was given (amd.com/gpu: N): RANK = "
+                         "PADDLE_TRAINER_ID·N + local, WORLD_SIZE = PADDLE_TRAINERS_NUM·N.  One pod with all of a "
+                         "node's GPUs is the xGMI layout: RCCL sees every peer GPU in one IPC namespace")
     ap.add_argument("--ckpt-dir", default=os.environ.get("PDO_CKPT_DIR", ""))
     ap.add_argument("--ckpt-every", type=int, default=0)
     ap.add_argument("--ipc-probe", action="store_true", help="hipIpc handle exchange + xGMI copy probe")
@@ -70,7 +73,7 @@ def run_collective(args, jenv) -> int:
     from ..utils import checkpoint as ckpt
     from ..utils import trace
 
-    if "RANK" not in os.environ or not args.worker:
+    if os.environ.get("PDO_LOCAL_CHILD") != "1" and ("RANK" not in os.environ or not args.worker):
         os.environ.update(jenv.torch_env(0, args.nproc_per_pod))
     b = bootstrap.init(T_START, backend=args.backend, timeout_s=args.timeout, ipc_probe=args.ipc_probe)
     dev = b.device
@@ -220,9 +223,13 @@ def _comm_diag(trainer, fence, dev, step_s, nosync_steps=3, iters=10):
     * ``exposed_ms``: timed step minus the same step with the gradient
       all-reduce switched off (``BucketedDDP.no_sync``) — the part of the
       bucketed RCCL traffic the backward did not hide;
-    * ``allreduce_busbw_GBps``: one bucket-sized (64 MiB on GPU) bf16
-      all-reduce, ring bus bandwidth = bytes · 2(n−1)/n / time — what xGMI
-      delivers to this job's communicator.
+    * ``buckets``: the job's bucket count and sizes (bytes);
+    * ``allreduce_sweep``: bf16 all-reduce busbw at 4 … 256 MiB (1 … 8 MiB on
+      CPU) — the knee ``utils/topology.py bucket_bytes_for`` is tuned from
+      (``knee_bytes``: the smallest size within 90 % of the best busbw);
+      ``allreduce_busbw_GBps`` keeps the 64 MiB point;
+    * ``ipc_gbps``: hipIpc handle exchange + a 64 MiB peer copy per same-node
+      pair (the xGMI link the bootstrap probe sees), GPU only.
 
     The no-sync steps leave the ranks' weights different; the job ends here."""
     import torch
@@ -243,20 +250,108 @@ def _comm_diag(trainer, fence, dev, step_s, nosync_steps=3, iters=10):
         out["step_ms"] = round(step_s * 1e3, 3)
         out["nosync_step_ms"] = round(ns * 1e3, 3)
         out["exposed_ms"] = round((step_s - ns) * 1e3, 3)
-    nbytes = (64 << 20) if dev.type == "cuda" else (4 << 20)
-    buf = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=dev)
-    for _ in range(3):
-        dist.all_reduce(buf)
-    fence()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        dist.all_reduce(buf)
-    fence()
-    t = (time.perf_counter() - t0) / iters
-    out["allreduce_bytes"] = nbytes
-    out["allreduce_us"] = round(t * 1e6, 1)
-    out["allreduce_busbw_GBps"] = round(nbytes * 2 * (n - 1) / n / t / 1e9, 1)
+    flat = getattr(trainer, "flat", None)
+    if flat is not None and getattr(flat, "buckets", None):
+        esz = flat.params.element_size()
+        out["buckets"] = {"count": len(flat.buckets), "bytes": [int(bk.numel * esz) for bk in flat.buckets]}
+    sizes_mib = (4, 8, 16, 32, 64, 128, 256) if dev.type == "cuda" else (1, 2, 4, 8)
+    buf = torch.ones((max(sizes_mib) << 20) // 2, dtype=torch.bfloat16, device=dev)
+    sweep = []
+    for mib in sizes_mib:
+        view = buf[: (mib << 20) // 2]
+        reps = iters if mib <= 64 else max(3, iters // 2)
+        for _ in range(2):
+            dist.all_reduce(view)
+        fence()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(view)
+        fence()
+        t = (time.perf_counter() - t0) / reps
+        sweep.append({"bytes": mib << 20, "us": round(t * 1e6, 1),
+                      "busbw_GBps": round((mib << 20) * 2 * (n - 1) / n / t / 1e9, 1)})
+    del buf
+    out["allreduce_sweep"] = sweep
+    best = max(p["busbw_GBps"] for p in sweep)
+    out["knee_bytes"] = next(p["bytes"] for p in sweep if p["busbw_GBps"] >= 0.9 * best)
+    ref = next((p for p in sweep if p["bytes"] == 64 << 20), sweep[-1])
+    out["allreduce_bytes"] = ref["bytes"]
+    out["allreduce_us"] = ref["us"]
+    out["allreduce_busbw_GBps"] = ref["busbw_GBps"]
+    if dev.type == "cuda":
+        try:
+            from .bootstrap import ipc_probe_run
+            out["ipc_gbps"] = ipc_probe_run(dev)
+        except Exception as e:  # diagnostics never fail the bench
+            out["ipc_gbps"] = f"unavailable: {e}"
     return out
+
+
+def spawn_local(args, jenv, argv) -> int:
+    """--nproc-per-pod N: the pod's entry process becomes a supervisor of N
+    local ranks, forked before anything in this process touches HIP.  Local
+    rank i gets RANK = PADDLE_TRAINER_ID·N + i, LOCAL_RANK = i and device i of
+    the pod's GPUs (HIP_VISIBLE_DEVICES under a device plugin, or PDO_GPU_IDS
+    when the agent exposes every GPU — launch/bootstrap.py picks it), so all N
+    devices stay visible to every rank and RCCL connects them peer to peer over
+    xGMI.  SIGTERM/SIGINT are forwarded; the first rank to fail takes the
+    others down (torchrun's behaviour) and its status is the pod's.
+    Replaces what ``paddle.distributed.launch`` does per pod in the reference's
+    images (deploy/examples/resnet.yaml:14-19)."""
+    import signal
+    if "torch" in sys.modules:
+        import torch
+        if torch.cuda.is_initialized():  # forking a HIP-initialised process is not allowed
+            raise RuntimeError("--nproc-per-pod: HIP already initialised in the pod's entry process")
+    n = args.nproc_per_pod
+    gpus = os.environ.get("PDO_GPU_IDS") or os.environ.get("HIP_VISIBLE_DEVICES") or ""
+    ids = [x for x in gpus.split(",") if x.strip()]
+    if ids and len(ids) < n:
+        raise RuntimeError(f"--nproc-per-pod {n} but the pod was given {len(ids)} GPU(s) ({gpus})")
+    kids = {}
+    for i in range(n):
+        env = jenv.torch_env(i, n)
+        pid = os.fork()
+        if pid == 0:
+            os.setpgid(0, 0)
+            os.environ.update(env)
+            os.environ["PDO_LOCAL_CHILD"] = "1"
+            try:
+                _hang_dump()
+                rc = run_collective(args, jenv)
+            except SystemExit as e:
+                rc = e.code if isinstance(e.code, int) else 1
+            except BaseException:
+                import traceback
+                traceback.print_exc()
+                rc = 1
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(int(rc or 0))
+        kids[pid] = i
+    log(f"pod {jenv.trainer_id}: {n} local ranks {env['WORLD_SIZE']}-world, pids {list(kids)}")
+
+    def forward(signum, frame):
+        for p in kids:
+            try:
+                os.killpg(p, signum)
+            except ProcessLookupError:
+                pass
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    while kids:
+        pid, status = os.wait()
+        i = kids.pop(pid, None)
+        if i is None:
+            continue
+        code = os.waitstatus_to_exitcode(status)
+        code = 128 - code if code < 0 else code
+        if code and not rc:
+            rc = code
+            log(f"local rank {i} exited {code}: stopping the other {len(kids)}")
+            forward(signal.SIGTERM, None)
+    return rc
 
 
 def run_ps(args, jenv) -> int:
@@ -323,19 +418,28 @@ def run_ps(args, jenv) -> int:
     return 0
 
 
-def main(argv=None) -> int:
-    args = parse_args(argv)
-    from .env import JobEnv
-    jenv = JobEnv.from_env()
-    jenv.check_supported()
-    log(f"role={jenv.role} id={jenv.trainer_id} mode={jenv.mode} elastic={jenv.elastic} workload={args.workload}")
+def _hang_dump():
     hang_dump = float(os.environ.get("PDO_HANG_DUMP_S", "0") or 0)
     if hang_dump > 0:
         # hang diagnostics: every thread's Python stack to the pod log every N s
         # (a rank stuck in a collective shows where; no debugger attached)
         import faulthandler
         faulthandler.dump_traceback_later(hang_dump, repeat=True, file=sys.stderr)
-    if jenv.mode == "PS" or args.workload in ("wide_deep", "deepfm") and jenv.pserver_endpoints:
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    from .env import JobEnv
+    jenv = JobEnv.from_env()
+    jenv.check_supported()
+    log(f"role={jenv.role} id={jenv.trainer_id} mode={jenv.mode} elastic={jenv.elastic} workload={args.workload}")
+    ps = jenv.mode == "PS" or args.workload in ("wide_deep", "deepfm") and jenv.pserver_endpoints
+    if args.nproc_per_pod > 1 and not ps and os.environ.get("PDO_LOCAL_CHILD") != "1":
+        if jenv.elastic or args.elastic:
+            raise NotImplementedError("--nproc-per-pod > 1 with an elastic job: one rank per pod there")
+        return spawn_local(args, jenv, argv)  # before any thread or HIP call in this process
+    _hang_dump()
+    if ps:
         return run_ps(args, jenv)
     if (jenv.elastic or args.elastic) and not args.worker:
         from .elastic import run_agent

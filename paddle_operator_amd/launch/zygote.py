@@ -77,6 +77,18 @@ def preload():
 WARM_PREFIXES = ("HIP_", "HSA_", "ROCR_", "GPU_", "NCCL_", "RCCL_", "PYTORCH_", "TORCH_", "AMD_", "LD_", "CUDA_")
 WARM_IGNORE = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
 SLOT_RETRIES = 3
+# a request parked behind a still-warming slot is cold-forked after this long
+# (≈ the cold start it was parked to avoid): a slot stuck in HIP or RCCL init
+# must never hold a pod's launch hostage (PDO_SLOT_PARK_S)
+SLOT_PARK_S = float(os.environ.get("PDO_SLOT_PARK_S", "2.5"))
+# a slot still warming after this long is killed and counted as a failure
+SLOT_WARM_MAX_S = float(os.environ.get("PDO_SLOT_WARM_MAX_S", "60"))
+# when the replacement slot for a GPU is forked: "handoff" = as soon as a job
+# takes the warm slot (the next job on that GPU starts warm; the replacement's
+# HIP context and 1-rank communicator stay resident beside the job, see
+# "mem_mb" in the status table), "exit" = once that job's rank exits (no
+# second context on the GPU while the job runs)
+SLOT_RESPAWN = os.environ.get("PDO_SLOT_RESPAWN", "handoff")
 
 
 def runtime_key(env: Dict[str, str]) -> tuple:
@@ -92,6 +104,9 @@ def warm_device_of(req: dict, key: tuple) -> Optional[str]:
         return None
     # elastic agents fork+exec their workers: never from a HIP-initialised process
     if "--elastic" in argv or "--worker" in argv or env.get("PADDLE_ELASTIC_JOB_ID") or env.get("PADDLE_ELASTIC_NP"):
+        return None
+    # a pod supervising several local ranks forks them: never from a warm slot
+    if "--nproc-per-pod" in argv or int(env.get("PDO_NPROC_PER_POD", "1") or 1) > 1:
         return None
     return dev if runtime_key(env) == key else None
 
@@ -156,6 +171,9 @@ def _become_rank(req, fds, warm=False):
         sys.argv = ["pdo-launch"] + argv
         sys.stdout = os.fdopen(1, "w", buffering=1, closefd=False)
         sys.stderr = os.fdopen(2, "w", buffering=1, closefd=False)
+        hold = float(os.environ.get("PDO_RANK_HOLD_S", "0") or 0)
+        if hold > 0:  # tests: a rank that stays alive this long before it runs
+            time.sleep(hold)
         from paddle_operator_amd.launch import run
         run.T_START = float(req.get("t_start") or time.time())
         rc = int(run.main(argv) or 0)
@@ -190,6 +208,7 @@ def _warm_gpu(index: int = 0) -> dict:
     torch.cuda.set_device(index)
     torch.cuda.init()
     dev = torch.device("cuda", index)
+    free0, total = torch.cuda.mem_get_info(dev)
     t1 = time.time()
     dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=dev)
     t = torch.ones(1, device=dev)
@@ -197,7 +216,12 @@ def _warm_gpu(index: int = 0) -> dict:
     torch.cuda.synchronize(dev)
     dist.destroy_process_group()
     del t
-    return {"hip_s": round(t1 - t0, 4), "rccl_s": round(time.time() - t1, 4)}
+    free1, _ = torch.cuda.mem_get_info(dev)
+    # device memory this warm process holds while it waits (HIP context + RCCL
+    # code objects); mem_get_info is device-wide, so this is an upper bound
+    # when other processes allocate on the GPU meanwhile
+    return {"hip_s": round(t1 - t0, 4), "rccl_s": round(time.time() - t1, 4),
+            "mem_mb": round((total - free1) / 2**20, 1), "mem_mb_before_rccl": round((total - free0) / 2**20, 1)}
 
 
 def _slot_main(dev: str, sock: socket.socket, listener: socket.socket):
@@ -212,7 +236,13 @@ def _slot_main(dev: str, sock: socket.socket, listener: socket.socket):
         for sig in (signal.SIGTERM, signal.SIGCHLD):
             signal.signal(sig, signal.SIG_DFL)
         os.environ.pop("CUDA_VISIBLE_DEVICES", None)
-        if os.environ.get("PDO_GPU_VISIBILITY") == "all":
+        test_mode = os.environ.get("PDO_SLOT_TEST", "")
+        if test_mode == "hang":  # CPU tests: a slot stuck in its warm-up
+            while True:
+                time.sleep(3600)
+        if test_mode == "cpu":  # CPU tests: a slot that warms nothing
+            info = {"device": "none"}
+        elif os.environ.get("PDO_GPU_VISIBILITY") == "all":
             os.environ.pop("HIP_VISIBLE_DEVICES", None)
             info = _warm_gpu(int(dev))
         else:
@@ -264,8 +294,9 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
     slots: Dict[str, _Slot] = {}       # device -> its (single) warm slot
     slot_pids: Dict[int, _Slot] = {}
     slot_fails: Dict[str, int] = {}
-    pending: Dict[str, list] = {}      # device -> [(conn, req, fds)] waiting for a warming slot
-    served = {"warm": 0, "cold": 0}
+    pending: Dict[str, list] = {}      # device -> [(conn, req, fds, t_park)] waiting for a warming slot
+    rank_dev: Dict[int, str] = {}      # rank pid -> GPU whose slot it took (SLOT_RESPAWN = exit)
+    served = {"warm": 0, "cold": 0, "park_timeouts": 0, "warm_timeouts": 0}
 
     def log(msg):
         print(f"[pdo-zygote] {msg}", flush=True)
@@ -324,19 +355,53 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
         slot_pids.pop(sl.pid, None)
         served["warm"] += 1
         attach(sl.pid, conn)
-        spawn_slot(sl.dev)  # the replacement warms while this job runs
+        if SLOT_RESPAWN == "exit":
+            rank_dev[sl.pid] = sl.dev  # the replacement is forked when this rank exits
+        else:
+            spawn_slot(sl.dev)  # the replacement warms while this job runs
 
     def flush_pending(dev):
-        for conn, req, fds in pending.pop(dev, []):
+        for conn, req, fds, _ in pending.pop(dev, []):
             sl = slots.get(dev)
             if sl is not None and sl.ready:
                 handoff(sl, conn, req, fds)
             else:
                 cold(conn, req, fds)
 
+    def expire(now):
+        """Cold-fork requests parked past SLOT_PARK_S; kill slots warming past
+        SLOT_WARM_MAX_S (counted in slot_fails; the reaper respawns up to
+        SLOT_RETRIES)."""
+        for dev in list(pending):
+            keep = []
+            for ent in pending[dev]:
+                if now - ent[3] > SLOT_PARK_S:
+                    served["park_timeouts"] += 1
+                    log(f"request parked {now - ent[3]:.1f}s behind warming slot gpu {dev}; cold fork")
+                    cold(*ent[:3])
+                else:
+                    keep.append(ent)
+            if keep:
+                pending[dev] = keep
+            else:
+                pending.pop(dev)
+        for sl in list(slots.values()):
+            if not sl.ready and now - sl.t_spawn > SLOT_WARM_MAX_S:
+                served["warm_timeouts"] += 1
+                log(f"slot gpu {sl.dev} pid {sl.pid} still warming after {now - sl.t_spawn:.0f}s; killed")
+                slot_fails[sl.dev] = slot_fails.get(sl.dev, 0) + 1
+                try:
+                    os.killpg(sl.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                drop_slot(sl)
+                flush_pending(sl.dev)
+
     def status_table():
         return {"pid": os.getpid(), "served": served,
-                "slots": {d: {"pid": sl.pid, "ready": sl.ready, **sl.info} for d, sl in slots.items()},
+                "slots": {d: {"pid": sl.pid, "ready": sl.ready, "t_spawn": sl.t_spawn, **sl.info}
+                          for d, sl in slots.items()},
+                "respawn": SLOT_RESPAWN, "park_s": SLOT_PARK_S,
                 "devices": list(warm_devices or []), "failed": slot_fails}
 
     for dev in warm_devices or []:
@@ -367,8 +432,8 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                 sl = slots.get(dev) if dev is not None else None
                 if sl is not None and sl.ready:
                     handoff(sl, conn, req, fds)
-                elif sl is not None:  # warming: waiting is never slower than a cold start
-                    pending.setdefault(dev, []).append((conn, req, fds))
+                elif sl is not None:  # warming: wait for it, but at most SLOT_PARK_S (expire)
+                    pending.setdefault(dev, []).append((conn, req, fds, time.time()))
                 else:
                     cold(conn, req, fds)
             elif isinstance(skey.data, tuple):  # a slot's control socket
@@ -408,8 +473,9 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                         os.killpg(pid, signal.SIGKILL)
                     except (ProcessLookupError, PermissionError):
                         pass
+        expire(time.time())
         # reap
-        while children:
+        while children or slot_pids:
             try:
                 pid, status = os.waitpid(-1, os.WNOHANG)
             except ChildProcessError:
@@ -425,6 +491,8 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                 spawn_slot(sl.dev)
                 continue
             conn = children.pop(pid, None)
+            if pid in rank_dev:
+                spawn_slot(rank_dev.pop(pid))
             code = os.waitstatus_to_exitcode(status)
             code = 128 - code if code < 0 else code
             if conn is not None:

@@ -126,13 +126,24 @@ class GPT2(nn.Module):
 
     @torch.no_grad()
     def reset_parameters(self, seed: int = 1234):
-        g = torch.Generator().manual_seed(seed)
+        """N(0, 0.02) weights (residual projections scaled by 1/sqrt(2·layers)).
+
+        Parameters already on a GPU (the trainer builds the model under
+        ``torch.device("cuda")``) are drawn in place by the device's generator:
+        no host RNG over 355 M values and no host→device copy — the largest term
+        of a GPT-2-medium rank's create→ready time (2.6 s in BENCH_r02, ≈2 s of
+        it CPU randn).  On CPU the host generator keeps the reference stream."""
+        dev = next(self.parameters()).device
+        g = torch.Generator(device=dev).manual_seed(seed)
         std = 0.02
         proj_std = 0.02 / math.sqrt(2 * self.cfg.n_layer)
         for name, p in self.named_parameters():
             if p.dim() == 2:
                 s = proj_std if (name.endswith("proj.weight") and "blocks" in name) else std
-                p.copy_(torch.randn(p.shape, generator=g) * s)
+                if dev.type == "cpu":
+                    p.copy_(torch.randn(p.shape, generator=g) * s)
+                else:
+                    p.normal_(0.0, s, generator=g)
         self.wte[self.cfg.vocab_size:].zero_()
 
     def forward(self, idx, targets=None):

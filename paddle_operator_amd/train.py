@@ -81,7 +81,12 @@ class GPT2Trainer:
             from .utils.tuning import enable_tuned_gemms
             enable_tuned_gemms()
         torch.manual_seed(seed)
-        model = GPT2(cfg)
+        if self.device.type == "cuda":
+            # built and initialised on the device (models/gpt2.py reset_parameters)
+            with torch.device(self.device):
+                model = GPT2(cfg)
+        else:
+            model = GPT2(cfg)
         model.to(device=self.device, dtype=dtype)
         self.model = model
         if bucket_mb is None:

@@ -250,7 +250,15 @@ def bucket_bytes_for(world: int, grad_bytes: int, links_per_gpu: int = 7) -> int
     quarter of the gradient so at least four buckets overlap the backward.
     At world 1 there is nothing to reduce: one bucket.  Pinned by
     tests/test_ddp.py::test_bucket_policy; the 1-GPU RCCL size sweep is
-    ``bin/pdo-allreduce-bench`` (profiles/rccl_allreduce_1gpu_r2.md)."""
+    ``bin/pdo-allreduce-bench`` (profiles/rccl_allreduce_1gpu_r2.md).
+
+    Tuning source: every multi-GPU ``bench.py --gpus N`` record carries
+    ``comm.allreduce_sweep`` (busbw of the job's own communicator at 4-256 MiB,
+    slowest rank) and ``comm.knee_bytes`` (the smallest size within 90 % of the
+    best busbw), next to ``comm.buckets`` (what this policy chose) and
+    ``comm.exposed_ms``.  Once a driver SCALE record exists, the per-world
+    bucket is set to that ``knee_bytes`` (still capped at a quarter of the
+    gradient); until then this stays the link-model heuristic."""
     if world <= 1:
         return max(grad_bytes, 1 << 20)
     b = (1 << 20) * world * links_per_gpu

@@ -16,7 +16,9 @@
 """
 import json
 import os
+import subprocess
 import sys
+import time
 
 import pytest
 
@@ -227,3 +229,67 @@ def test_config5_elastic_4_8_4_with_pod_kill_gpu_accounting():
         assert sum(e["reason"] == "Scaled" for e in cl.events()) >= 2
     finally:
         cl.stop()
+
+
+# ----------------------------------------------------------------------------- multi-GPU pods
+def test_two_pods_nproc_per_pod_2_world_4(tmp_path):
+    """2 replicas × --nproc-per-pod 2 through the operator: each pod's entry
+    process supervises two local ranks (RANK = trainer_id·2 + local), one world
+    of 4 over gloo — the layout of one pod per node holding all its GPUs
+    (amd.com/gpu: 8, --nproc-per-pod 8), where RCCL reaches every peer over xGMI."""
+    base = free_port_block(50)
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), port_range=(base, base + 40))
+    cont = {"name": "paddle", "image": "pdo/launcher:rocm",
+            "command": [sys.executable, "-m", "paddle_operator_amd.launch", "--workload", "gpt2", "--tiny",
+                        "--steps", "3", "--log-every", "1", "--seq", "128", "--nproc-per-pod", "2",
+                        "--backend", "gloo"],
+            "env": [{"name": "PYTHONPATH", "value": REPO}, {"name": "OMP_NUM_THREADS", "value": "1"},
+                    {"name": "PDO_OPS", "value": "torch"}]}
+    cl.create(T.paddlejob("np2", worker={"replicas": 2, "template": {"spec": {"containers": [cont]}}},
+                          intranet="Host", clean_pod_policy="Never"))
+
+    def log(pod):
+        d = cl.sandbox(pod)
+        p = os.path.join(d, "paddle.log") if d else ""
+        return open(p).read() if p and os.path.exists(p) else ""
+
+    def recs(pod, tag):
+        return [json.loads(l[len(tag) + 1:]) for l in log(pod).splitlines() if l.startswith(tag + " ")]
+
+    try:
+        ok = cl.wait_phase("np2", T.Phase.Completed, timeout=300)
+        assert ok, (cl.job("np2")["status"], log("np2-worker-0")[-3000:], log("np2-worker-1")[-3000:])
+        for i in range(2):
+            ready = sorted(recs(f"np2-worker-{i}", "PDO_READY"), key=lambda r: r["rank"])
+            assert [r["rank"] for r in ready] == [2 * i, 2 * i + 1], ready
+            assert [r["local_rank"] for r in ready] == [0, 1]
+            assert all(r["world"] == 4 and r["backend"] == "gloo" for r in ready)
+            assert len({r["pid"] for r in ready}) == 2  # two processes in one pod
+            done = recs(f"np2-worker-{i}", "PDO_DONE")
+            assert len(done) == 2 and all(d["steps"] == 3 and d["world"] == 4 for d in done)
+        st = cl.job("np2")["status"]
+        assert st["mode"] == T.Mode.Collective and st["worker"]["succeeded"] == 2
+    finally:
+        cl.stop()
+
+
+def test_nproc_per_pod_local_rank_failure_takes_pod_down(tmp_path):
+    """A local rank that fails ends its siblings and fails the pod (its status
+    is the pod's), so the job goes Failed instead of hanging in a collective."""
+    from paddle_operator_amd.launch.env import JobEnv
+    env = JobEnv.from_env({"PADDLE_TRAINER_ID": "1", "PADDLE_TRAINERS_NUM": "2",
+                           "PADDLE_TRAINER_ENDPOINTS": "10.0.0.1:2379,10.0.0.2:2379"})
+    assert env.torch_env(1, 4) == {"RANK": "5", "WORLD_SIZE": "8", "LOCAL_RANK": "1", "LOCAL_WORLD_SIZE": "4",
+                                   "MASTER_ADDR": "10.0.0.1", "MASTER_PORT": "2380"}
+    base = free_port_block(10)
+    e = dict(os.environ, PYTHONPATH=REPO, PADDLE_TRAINER_ID="0", PADDLE_TRAINERS_NUM="1",
+             PADDLE_TRAINER_ENDPOINTS=f"127.0.0.1:{base}", POD_IP="127.0.0.1", PADDLE_PORT=str(base),
+             TRAINING_ROLE="TRAINER", PDO_OPS="torch", OMP_NUM_THREADS="1")
+    # world 2 in one pod, but a bogus workload model makes every local rank fail at start
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "paddle_operator_amd.launch", "--workload", "gpt2",
+                        "--model", "no-such-model", "--nproc-per-pod", "2", "--backend", "gloo", "--timeout", "60"],
+                       env=e, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert time.time() - t0 < 200
+    assert "local ranks" in r.stdout

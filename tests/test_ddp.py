@@ -86,7 +86,8 @@ def _bench_env():
 
 
 BENCH_ARGS = ["--model", "gpt2-tiny", "--micro-batch", "2", "--seq", "64", "--steps", "2", "--warmup", "1",
-              "--ready-trials", "2", "--cpu", "--ops", "torch"]
+              "--ready-trials", "2", "--cpu", "--ops", "torch", "--compat-trials", "1", "--train-ready-trials", "2",
+              "--b2b-trials", "2"]
 
 
 def _json_line(out):
@@ -101,11 +102,17 @@ def _check_record(rec, n):
         assert k in rec, k
     assert rec["n_gpus"] == n and rec["steps"] == 2 and rec["warmup"] == 1 and rec["value"] > 0
     assert rec["config"]["parallelism"] == f"dp{n}" and rec["config"]["global_batch"] == 2 * n
-    assert "PaddleJob" in rec["config"]["launch"]
+    assert "PaddleJob" in rec["config"]["launch"] and rec["config"]["pod_layout"] in (f"{n}x1", f"1x{n}")
     assert rec["ready"]["trials"] == 2 and 0 < rec["ready_p50_s"] < 60
+    assert rec["ready_train"]["trials"] == 2 and rec["ready_b2b"]["trials"] == 2
+    assert rec["compat_ready"]["trials"] == 1 and rec["compat_ready"]["p50"] > 0
     if n > 1:  # communication evidence measured after the timed region (launch/run.py _comm_diag)
         c = rec["comm"]
         assert c["ranks"] == n and c["allreduce_busbw_GBps_min"] > 0 and "exposed_ms_max" in c, c
+        sw = c["allreduce_sweep"]
+        assert [p["bytes"] >> 20 for p in sw] == [1, 2, 4, 8] and all(p["busbw_GBps"] > 0 for p in sw), sw
+        assert c["knee_bytes"] in [p["bytes"] for p in sw]
+        assert c["buckets"]["count"] >= 1 and all(b > 0 for b in c["buckets"]["bytes"])
     else:
         assert rec["comm"] is None
     tokens = 2 * 64 * n * 2  # micro-batch × seq × world × steps
@@ -126,6 +133,17 @@ def test_bench_launched_two_ranks_without_torchrun():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check_record(_json_line(r.stdout), 2)
+
+
+def test_bench_one_pod_layout_two_ranks():
+    """--pod-layout one-pod: one PaddleJob pod running --nproc-per-pod 2 local
+    ranks (the Kubernetes xGMI layout); the record says which layout ran."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--pod-layout", "one-pod"] + BENCH_ARGS, cwd=REPO,
+                       env=_bench_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    _check_record(rec, 2)
+    assert rec["config"]["pod_layout"] == "1x2" and "replicas=1 x 2" in rec["config"]["launch"]
 
 
 @pytest.mark.slow
