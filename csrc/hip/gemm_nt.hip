@@ -27,6 +27,8 @@
 //              GEMM with the bias-GELU backward pass fused
 // Rounding matches the unfused path bit for bit: the GEMM result is rounded to
 // bf16 before the activation math, as when it made an HBM round trip.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -232,7 +234,12 @@ int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
 
 int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
 
-static int g_impl = 1;  // 4-wave mainloop, variant 0 (tools/nt4_probe.py)
+// 1 = 4-wave mainloop, variant 0 (tools/nt4_probe.py); PDO_NT_IMPL overrides
+// (A/B in the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=8 PDO_NT_IMPL=1')
+static int g_impl = [] {
+  const char* e = getenv("PDO_NT_IMPL");
+  return e && *e ? atoi(e) : 1;
+}();
 void gemm_nt_set_impl(int impl) { g_impl = impl; }
 int gemm_nt_get_impl() { return g_impl; }
 

@@ -59,7 +59,7 @@ __device__ __forceinline__ void static_for(Fn&& f) {
 }
 constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 = 32 KiB
 
-// ---- register-epilogue helpers (SCHED 1)
+// ---- register-epilogue helpers (SCHED & 2)
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -98,7 +98,7 @@ __device__ __forceinline__ void transpose_blocks(u32x2 (&b)[4]) {
 
 // SCHED 0: one barrier per k-tile, tile t+1's DMA issued during tile t (lead
 //          ≈ 0.6 tile), described at the top of the file.
-// SCHED 1: three barriers per k-tile and an operand-split refill — the schedule
+// SCHED & 1: three barriers per k-tile and an operand-split refill — the schedule
 //          of hipBLASLt's gfx950 MT256x256x64 loop (profiles/r3_gemm_nt4_sched.md).
 //          Tile t's buffer is released operand by operand as the waves finish
 //          reading it: after barrier 1 (every wave's last A read of it, the k
@@ -107,6 +107,7 @@ __device__ __forceinline__ void transpose_blocks(u32x2 (&b)[4]) {
 //          flight) publishes tile t+1, whose k 0-31 fragments are then read
 //          under the last quarter of tile t's MFMAs.  Every DMA piece has
 //          ≈ 1.3-1.6 tiles of lead instead of ≈ 0.6.
+// SCHED & 2: the register epilogue (below) instead of the LDS-staged one.
 template <int EPI, int EPG, int BAR, int BUFLD, int SCHED = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   f32x4 acc[8][8];  // first written by mma0 in tile 0's block 0
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
-  if constexpr (SCHED == 1) {
+  if constexpr (SCHED & 1) {
     // fragment i of A (rows wm·128 + 16i + (l & 15)) / B, k half kk, from buffer BUF
     auto rdA = [&](auto buf_tag, int kk, int i) -> bf16x8 {
       constexpr int BUF = decltype(buf_tag)::value;
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
                  : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
     return v;
   };
-  if constexpr (SCHED == 1) {
+  if constexpr (SCHED & 2) {
     // ---- register epilogue: no LDS round trip, no barrier.  Per 16-row block
     // i and 4-block column group h, the 4 lanes {r, r+16, r+32, r+48} hold a
     // 4×4 matrix of 4-column pieces; transpose_blocks leaves each lane 16
@@ -671,6 +672,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
   using I4 = std::integral_constant<int, 4>;
   using I7 = std::integral_constant<int, 7>;
   using I11 = std::integral_constant<int, 11>;
@@ -679,14 +681,17 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   // 0 = barrier after block-1 group 11, the first 4 DMA pieces of tile t+2 after it, the rest one per
   // block-0 group, B-stationary MFMA order (each group's 4 MFMAs share SrcA; default: 1-4 % faster
   // than the A-stationary order of variant 4 on qkv_fwd / proj_dx, bit-identical)
-  // 5 = SCHED 1 (three barriers, operand-split refill)
+  // 5 = SCHED 1 (three barriers, operand-split refill; default), 6 = the same with
+  // the register epilogue (profiles/r3_gemm_nt4_sched.md: slower on the wide-N
+  // shapes, e.g. qkv_fwd 360 -> 395 us; kept for the record and the tests)
   switch (variant) {
     case 1: return launch(I1{}, I7{}, I0{}, I0{});
     case 2: return launch(I2{}, I7{}, I0{}, I0{});   // every piece of tile t+2 right after tile t's barrier
     case 3: return launch(I4{}, I11{}, I0{}, I0{});  // the same, 4 per group after a later barrier
     case 4: return launch(I1{}, I11{}, I0{}, I0{});  // variant 0 with the A-stationary order
-    case 5: return launch(I1{}, I11{}, I2{}, I1{});
-    default: return launch(I1{}, I11{}, I2{}, I0{});
+    case 6: return launch(I1{}, I11{}, I2{}, I3{});
+    case 7: return launch(I1{}, I11{}, I2{}, I0{});  // the round-2 default (SCHED 0)
+    default: return launch(I1{}, I11{}, I2{}, I1{});
   }
   return 0;
 }

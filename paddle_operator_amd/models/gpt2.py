@@ -50,8 +50,11 @@ class GPT2Config:
             "gpt2-medium": dict(n_embd=1024, n_layer=24, n_head=16),
             "gpt2-large": dict(n_embd=1280, n_layer=36, n_head=20),
             "gpt2-xl": dict(n_embd=1600, n_layer=48, n_head=25),
-            # tiny config for CPU tests / smoke
+            # tiny config for CPU tests
             "gpt2-tiny": dict(n_embd=128, n_layer=2, n_head=2, n_positions=256, vocab_size=1000),
+            # GPU smoke: the smallest width whose GEMMs (K = 256, 1024) enter the
+            # hand-written gemm_nt4 / gemm_dw4 kernels, not their fallbacks
+            "gpt2-smoke": dict(n_embd=256, n_layer=2, n_head=4, n_positions=512, vocab_size=4000),
         }
         return GPT2Config(**table[name])
 

@@ -260,7 +260,7 @@ def _weight_grad(w, dy2, x2):
         # a gradient tensor for autograd to accumulate (the tied LM head / embedding
         # weight): HIP dW GEMM where its shape contract holds (incl. the 50304-row
         # vocabulary's half-height tile row: 5.42 vs 6.41 ms alone, tools/lm_dw_probe.py;
-        # in the step 159.08 / 159.20 vs 159.24 / 159.44 ms, tools/gpu_so_ab.sh)
+        # in the step 159.08 / 159.20 vs 159.24 / 159.44 ms, tools/gpu.sh soab)
         if (_HIP_DW[0] and dy2.is_cuda and dy2.dtype == torch.bfloat16 and dy2.is_contiguous()
                 and x2.is_contiguous()):
             g = torch.empty(Fo, K, device=dy2.device, dtype=dy2.dtype)
@@ -510,7 +510,7 @@ class _NTMLPFn(torch.autograd.Function):
 
 
 # fc1 forward with the fused GELU epilogue (gemm_nt): off by default.  In the
-# GPT-2-medium step (tools/gpu_ab_probe.sh PDO_NT_GELU=0/1, same box, 2 rounds)
+# GPT-2-medium step (tools/gpu.sh 'stepab:PDO_NT_GELU=0 PDO_NT_GELU=1', same box, 2 rounds)
 # it ran 152.25 / 152.80 ms vs 152.74 / 153.21 ms for hipBLASLt + bias_gelu_fwd:
 # the probe's 46 µs per call does not survive cold operands.  PDO_NT_GELU=1 on.
 _NT_GELU = [os.environ.get("PDO_NT_GELU", "0") == "1"]

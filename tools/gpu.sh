@@ -14,6 +14,10 @@
 #                       summarised by tools/prof_summary.py (-> NAME/prof_SCRIPT.md)
 #   'pmc:CTRS SCRIPT ARGS'  one rocprofv3 --pmc pass (CTRS joined by '+') over tools/SCRIPT
 #   step                prof of the GPT-2-medium training step (tools/train_probe.py)
+#   'stepab:C1 C2 ..'   in-process GPT-2-medium step under each env config Ci (K=V[;K=V..]),
+#                       2 interleaved rounds (STEPS, default 20)
+#   'soab:SCRIPT ARGS'  A/B built extensions: every ab/*.so in turn over the tree's
+#                       _pdo_hip.so, python tools/SCRIPT ARGS with each, 2 rounds; restored after
 #   env:K=V             export K=V for the following steps
 set -o pipefail
 NAME=${1:?name}; shift
@@ -64,6 +68,28 @@ run_step() {
       ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d "$p" -o run -- python3 "$R/tools/$s" "${A[@]:2}" ) \
         > "$p.log" 2>&1 || { tail -30 "$p.log"; return 1; }
       python3 tools/pmc_summary.py $(find "$p" -name "*.db") > "$p.md" 2>&1 && rm -rf "$p"; head -60 "$p.md" ;;
+    stepab)
+      local round cfg
+      for round in 1 2; do
+        for cfg in "${A[@]}"; do
+          ( IFS=';'; for kv in $cfg; do export "$kv"; done
+            timeout -k 10 300 python tools/train_probe.py --dist --steps "${STEPS:-20}" --warmup 3 ) \
+            > "$O/stepab.json" 2> "$O/stepab.err" || { tail -30 "$O/stepab.err"; return 1; }
+          echo "$round [$cfg] $(tail -1 "$O/stepab.json")"
+        done
+      done ;;
+    soab)
+      local so=paddle_operator_amd/_pdo_hip.so round v out rc=0
+      cp "$so" "$O/.tree_hip.so"
+      for round in 1 2; do
+        for v in ab/*.so; do
+          cp "$v" "$so"
+          out=$(timeout -k 10 300 python "tools/${A[0]}" "${A[@]:1}" 2> "$O/soab.err") || { rc=1; tail -20 "$O/soab.err"; break 2; }
+          echo "$round $(basename "$v" .so) $out"
+        done
+      done
+      cp "$O/.tree_hip.so" "$so"; rm -f "$O/.tree_hip.so"
+      return $rc ;;
     *) say "unknown step $step"; return 2 ;;
   esac
 }
