@@ -509,11 +509,13 @@ class _NTMLPFn(torch.autograd.Function):
         return dx, dw1, db1, dw2
 
 
-# fc1 forward with the fused GELU epilogue (gemm_nt): off by default.  In the
-# GPT-2-medium step (tools/gpu.sh 'stepab:PDO_NT_GELU=0 PDO_NT_GELU=1', same box, 2 rounds)
-# it ran 152.25 / 152.80 ms vs 152.74 / 153.21 ms for hipBLASLt + bias_gelu_fwd:
-# the probe's 46 µs per call does not survive cold operands.  PDO_NT_GELU=1 on.
-_NT_GELU = [os.environ.get("PDO_NT_GELU", "0") == "1"]
+# fc1 forward with the fused GELU epilogue (gemm_nt): on by default since the
+# three-barrier gemm_nt4 schedule (round 3).  GPT-2-medium step, one box, 2
+# interleaved rounds (tools/gpu.sh 'stepab:...', profiles/r3_gemm_nt4_sched.md):
+# 151.02 / 151.14 ms with hipBLASLt + bias_gelu_fwd, 150.76 / 150.79 fused.
+# (Round 2, on the one-barrier schedule, it was 0.5 ms slower: off then.)
+# PDO_NT_GELU=0 restores the library GEMM + the HIP bias-GELU kernel.
+_NT_GELU = [os.environ.get("PDO_NT_GELU", "1") != "0"]
 
 
 # fc2 input gradient with the fused GELU' epilogue (gemm_nt) where its shape
