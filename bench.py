@@ -311,6 +311,12 @@ def orchestrate(a):
             out["ready"] = ready_stats(trials) if trials else None
             if trials:
                 log(f"ready p50 {out['ready']['p50']}s over {len(trials)} trials ({N} ranks)")
+            if L.zygote and gpus:
+                # the warm slots' resident footprint (HIP context + RCCL code), per GPU
+                st = L.cl.zygote_status()
+                out["warm_slots"] = {node: {d: {k: sl.get(k) for k in ("mem_mb", "mem_mb_before_rccl", "warm_s")}
+                                            for d, sl in (z or {}).get("slots", {}).items()}
+                                     for node, z in st.items()}
             if a.b2b_trials and not a.ready_only:
                 bt = [L.ready_trial(f"b2b-{t}", N, a.timeout, wait_warm=False) for t in range(a.b2b_trials)]
                 out["ready_b2b"] = ready_stats(bt)
@@ -382,6 +388,7 @@ def orchestrate(a):
         "ready_train": out.get("ready_train"),
         # noop jobs created back to back (warm slots may still be re-warming)
         "ready_b2b": out.get("ready_b2b"),
+        "warm_slots": out.get("warm_slots"),
         "compat_ready": out.get("compat_ready"),
         "job_ready_s": round(out["bench_ready_s"], 3),
         "final_loss": rs[0].get("loss"),

@@ -34,6 +34,7 @@
 // every 8 rows, so its fragment addresses are per-lane constants plus
 // ds_read immediates (toff_v; 1.6 % on the forward, bitwise-identical output).
 #include <math.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -64,6 +65,23 @@ __device__ __forceinline__ f32x16 zero16() {
 #pragma unroll
   for (int i = 0; i < 16; ++i) z[i] = 0.f;
   return z;
+}
+
+__device__ __forceinline__ f32x16 bcast16(float v) {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = v;
+  return z;
+}
+
+// operand prescale: x ← bf16(c · x), once per workgroup on the register-resident
+// operand, so every score MFMA yields c2·q·k directly (log2-domain logits) and
+// the softmax needs no per-score multiply.  Rounds c·x to bf16 once (the score's
+// relative error grows from 2^-9 to ≈ 1.4 · 2^-9).
+template <int N>
+__device__ __forceinline__ void prescale(bf16x8 (&v)[N], float c) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = to_bf16(to_f32(v[i]) * c);
 }
 
 // row fragment: lane reads row (rbase + lane&31), chunk (2ks + lane>>5)
@@ -283,10 +301,14 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
   retire(qf);
+  prescale(qf, c2);
 
   const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
   f32x16 o0 = zero16(), o1 = zero16();
-  float m = -INFINITY, l = 0.f;
+  // m: running max in log2 units; nm16 = −m in every register is the score
+  // MFMAs' initial accumulator, so they produce s' = c2·q·k − m directly
+  float m = 0.f, l = 0.f;
+  f32x16 nm16 = zero16();
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
@@ -307,7 +329,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
     }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
-      f32x16 s0 = zero16(), s1 = zero16();
+      f32x16 s0 = nm16, s1 = nm16;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
@@ -323,27 +345,35 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
           s1[r] = c + 32 > d ? -INFINITY : s1[r];
         }
       }
+      // tile max of s' (relative to m): only a growth past 2^8 rescales
+      // (defer-max, cdna_hip_programming.md T13); the first tile sets m
       float tmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-      tmax = xhalf_max(tmax) * c2;
-      const bool grow = tmax > m + 8.f;
-      if (__any(grow)) {
-        const float mn = grow ? fmaxf(m, tmax) : m;
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
-        m = mn;
+      tmax = xhalf_max(tmax);
+      if (t == 0) {  // every query has key 0 unmasked here: tmax is finite
+        m = tmax;
+        s0 -= tmax;
+        s1 -= tmax;
+        nm16 = bcast16(-m);
+      } else if (__any(tmax > 8.f)) {
+        const float d = tmax > 8.f ? tmax : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        m += d;
         l *= alpha;
         o0 *= alpha;
         o1 *= alpha;
+        s0 -= d;
+        s1 -= d;
+        nm16 = bcast16(-m);
       }
-      const float nm = -m;
       f32x2 ls2 = {0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        s0[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c2, nm));
-        s0[r + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r + 1], c2, nm));
-        s1[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c2, nm));
-        s1[r + 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r + 1], c2, nm));
+        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
         ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
       }
       l += ls2[0] + ls2[1];
@@ -380,6 +410,172 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
 }
 
 // ============================================================================
+// forward, two 32-query blocks per wave (PDO_ATTN_FWD=2): workgroup = 4 waves =
+// 256 queries.  Every K fragment (ds_read_b128) and V fragment (transposed
+// reads) feeds two MFMAs instead of one, and each wave carries two independent
+// softmax chains per tile for the scheduler to interleave with the other
+// block's MFMAs.  2 waves per SIMD (≤ 256 VGPRs) instead of 3.
+// ============================================================================
+struct FwdBlock {
+  f32x16 o0, o1;  // output accumulators
+  float m, l;     // running max (log2 units; −m broadcast is the score MFMAs' initial C) and sum
+};
+
+__global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                         float* __restrict__ lse, int B, int S, int H, float c2) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int nqb = S / 256;
+  const int bh = blockIdx.x % (B * H);
+  const int qb = nqb - 1 - blockIdx.x / (B * H);  // heaviest query blocks first
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+
+  const int qw0 = qb * 256 + w * 64;  // first query of this wave (block 0; block 1 = +32)
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qf[u][ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)(qw0 + 32 * u + li) * rs + 16 * ks + 8 * hh);
+  retire(qf[0]);
+  retire(qf[1]);
+  prescale(qf[0], c2);
+  prescale(qf[1], c2);
+
+  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
+  FwdBlock blk[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    blk[u].o0 = zero16();
+    blk[u].o1 = zero16();
+    blk[u].m = 0.f;
+    blk[u].l = 0.f;
+  }
+  const int ntiles = (qb * 256 + 256) / TROWS;
+
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store_v(sv, smem + TROWS * HD, tid);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
+    const bf16* Vt = Kt + TROWS * HD;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    }
+    const int key0 = t * TROWS;
+    if (key0 <= qw0 + 63) {
+      const bool do0 = key0 <= qw0 + 31;  // block 0 has a key of this tile at or before its queries
+      f32x16 s[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) s[u][0] = s[u][1] = bcast16(-blk[u].m);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 k0 = row_frag(Kt, 0, ks, lane), k1 = row_frag(Kt, 32, ks, lane);
+        if (do0) {
+          s[0][0] = mfma(k0, qf[0][ks], s[0][0]);
+          s[0][1] = mfma(k1, qf[0][ks], s[0][1]);
+        }
+        s[1][0] = mfma(k0, qf[1][ks], s[1][0]);
+        s[1][1] = mfma(k1, qf[1][ks], s[1][1]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 0 && !do0) continue;
+        FwdBlock& k = blk[u];
+        f32x16& s0 = s[u][0];
+        f32x16& s1 = s[u][1];
+        const int qfirst = qw0 + 32 * u;
+        if (key0 + TROWS - 1 > qfirst) {  // diagonal tile (wave-uniform)
+          const int d = qfirst + li - key0 - 4 * hh;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = (r & 3) + 8 * (r >> 2);
+            s0[r] = c > d ? -INFINITY : s0[r];
+            s1[r] = c + 32 > d ? -INFINITY : s1[r];
+          }
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+        tmax = xhalf_max(tmax);
+        if (t == 0) {
+          k.m = tmax;
+          s0 -= tmax;
+          s1 -= tmax;
+        } else if (__any(tmax > 8.f)) {
+          const float dm = tmax > 8.f ? tmax : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-dm);
+          k.m += dm;
+          k.l *= alpha;
+          k.o0 *= alpha;
+          k.o1 *= alpha;
+          s0 -= dm;
+          s1 -= dm;
+        }
+        f32x2 ls2 = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+          s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+          s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+          ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+        }
+        k.l += ls2[0] + ls2[1];
+      }
+      const bf16* V0 = Vt + vb0;
+      const bf16* V1 = Vt + vb1;
+#define PV_STEP(KA, KB, PR)                                           \
+  {                                                                   \
+    const bf16x8 va0 = tr_frag_v<KA>(V0), va1 = tr_frag_v<KA>(V1);    \
+    const bf16x8 vb0_ = tr_frag_v<KB>(V0), vb1_ = tr_frag_v<KB>(V1);  \
+    if (do0) {                                                        \
+      const bf16x8 pa = pack8(s[0][0], PR), pb = pack8(s[0][1], PR);  \
+      blk[0].o0 = mfma(va0, pa, blk[0].o0);                           \
+      blk[0].o1 = mfma(va1, pa, blk[0].o1);                           \
+      blk[0].o0 = mfma(vb0_, pb, blk[0].o0);                          \
+      blk[0].o1 = mfma(vb1_, pb, blk[0].o1);                          \
+    }                                                                 \
+    const bf16x8 pa = pack8(s[1][0], PR), pb = pack8(s[1][1], PR);    \
+    blk[1].o0 = mfma(va0, pa, blk[1].o0);                             \
+    blk[1].o1 = mfma(va1, pa, blk[1].o1);                             \
+    blk[1].o0 = mfma(vb0_, pb, blk[1].o0);                            \
+    blk[1].o1 = mfma(vb1_, pb, blk[1].o1);                            \
+  }
+      PV_STEP(0, 32, 0)
+      PV_STEP(16, 48, 1)
+#undef PV_STEP
+    }
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store_v(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = qw0 + 32 * u + li;
+    const float lt = xhalf_sum(blk[u].l);
+    const float inv = 1.f / lt;
+    bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
+    store_acc_rows(orow, blk[u].o0, 0, hh, inv);
+    store_acc_rows(orow, blk[u].o1, 32, hh, inv);
+    if (hh == 0) lse[(size_t)bh * S + q] = (blk[u].m + log2f(lt)) * LN2;
+  }
+}
+
+// ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
@@ -400,7 +596,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
   const bf16* kbase = qbase + (size_t)H * HD;
   const bf16* vbase = qbase + (size_t)2 * H * HD;
   const bf16* dobase = dout + (size_t)b * S * ors + (size_t)h * HD;
-  const float* lse2_bh = delta + (size_t)B * H * S + (size_t)bh * S;  // lse·log2e, written by the dQ kernel
+  const float* lse2_bh = delta + (size_t)B * H * S + (size_t)bh * S;  // −lse·log2e, written by the dQ kernel
   const float* del_bh = delta + (size_t)bh * S;
   (void)lse;
   (void)nkb;
@@ -414,6 +610,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
   }
   retire(kf);
   retire(vf);
+  prescale(kf, c2);  // s' = q·bf16(c2·k): log2-domain logits straight from the MFMA
   f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
   const int qt0 = (kb * 128) / TROWS;
   const int nqt = S / TROWS;
@@ -454,28 +651,39 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
       for (int qs = 0; qs < 2; ++qs) {
         const int qb0 = q0 + 32 * qs;
         if (qb0 + 31 < wave_kmin) continue;  // all queries before this wave's keys
-        f32x16 sacc = zero16(), dpacc = zero16();
+        // rows r: q = qb0 + (r&3) + 8(r>>2) + 4hh.  The accumulators start at the
+        // rows' −lse·log2e and −delta (stored negated by the dQ kernel): the chains
+        // end at s' = c2·q·k − lse·log2e and dp' = dO·v − delta
+        f32x16 sacc, dpacc;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qr = 32 * qs + 8 * g + 4 * hh;
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(L2 + qr);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + qr);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sacc[4 * g + e] = l4[e];
+            dpacc[4 * g + e] = d4[e];
+          }
+        }
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
           dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
         }
-        // rows r: q = qb0 + (r&3) + 8(r>>2) + 4hh.  The causal mask only touches the
-        // diagonal sub-tile (wave-uniform): a separate body keeps its compares and
-        // selects out of every other tile
+        // The causal mask only touches the diagonal sub-tile (wave-uniform): a
+        // separate body keeps its compares and selects out of every other tile
         auto softmax_grad = [&](auto masked) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int qr = 32 * qs + 8 * g + 4 * hh;
-            const f32x4 l4 = *reinterpret_cast<const f32x4*>(L2 + qr);
-            const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + qr);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const int r = 4 * g + e;
-              float p = __builtin_amdgcn_exp2f(sacc[r] * c2 - l4[e]);
+              float p = __builtin_amdgcn_exp2f(sacc[r]);
               if constexpr (decltype(masked)::value) p = (q0 + qr + e) < key ? 0.f : p;
               sacc[r] = p;
-              dpacc[r] = p * (dpacc[r] - d4[e]);
+              dpacc[r] = p * dpacc[r];
             }
           }
         };
@@ -559,13 +767,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
   const float dq_delta = xhalf_sum(dpart);
   if (hh == 0) {
-    delta[(size_t)bh * S + q] = dq_delta;
-    delta[(size_t)B * H * S + (size_t)bh * S + q] = lq;  // lse·log2e for the dK/dV kernel's DMA
+    // negated: the dK/dV kernel DMAs them straight into its accumulators' initial values
+    delta[(size_t)bh * S + q] = -dq_delta;
+    delta[(size_t)B * H * S + (size_t)bh * S + q] = -lq;  // −lse·log2e
   }
   retire(qf);
   retire(df);
   retire(lq);
   retire(dq_delta);
+  // (no operand prescale / row-constant accumulators here: the 16-register
+  // −lse block pushes this 3-waves-per-SIMD kernel into spills; the per-score
+  // FMA stays)
   f32x16 a0 = zero16(), a1 = zero16();
   const int ntiles = (qb * 128 + 128) / TROWS;
   const int wave_qmax = qb * 128 + w * 32 + 31;
@@ -598,7 +810,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         auto softmax_grad = [&](auto masked) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            float p = __builtin_amdgcn_exp2f(s[r] * c2 - lq);
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], c2, -lq));
             if constexpr (decltype(masked)::value) {
               const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
               p = kr > q ? 0.f : p;
@@ -640,6 +852,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
+  static const int variant = [] {
+    const char* e = getenv("PDO_ATTN_FWD");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (variant == 2 && S % 256 == 0) {
+    attn_fwd2_d64<<<B * H * (S / 256), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E);
+    return 0;
+  }
   const int grid = B * H * (S / 128);
   attn_fwd_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E);
   return 0;

@@ -521,7 +521,8 @@ def test_zygote_gpu_warm_slot_handoff(tmp_path):
         assert cl.wait_phase("w3", T.Phase.Completed, timeout=60)
         assert _ready_rec(cl, "w3", 0)["warm_slot"] is False
         st2 = cl.zygote_status()["node0"]
-        assert st2["served"] == {"warm": 1, "cold": 2} and st2["slots"]["0"]["pid"] == st1["slots"]["0"]["pid"]
+        assert {k: st2["served"][k] for k in ("warm", "cold")} == {"warm": 1, "cold": 2}
+        assert st2["slots"]["0"]["pid"] == st1["slots"]["0"]["pid"]
         # a long-running rank on a slot: the pod kill reaches it
         job("wk", ["--workload", "resnet50", "--tiny", "--steps", "100000"])
         assert cl.wait_phase("wk", T.Phase.Running, timeout=60)
