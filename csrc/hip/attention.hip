@@ -131,6 +131,27 @@ __device__ __forceinline__ void retire(const bf16x8 (&v)[N]) {
 }
 __device__ __forceinline__ void retire(float x) { asm volatile("" ::"v"(x)); }
 
+// Work order of the (b, h) × block grid.  order 0: heaviest blocks first across
+// every (b, h) — one pair's blocks run far apart in time, so each re-fetches the
+// pair's K/V (or Q/dO) tiles from beyond L2.  order 1: XCD-grouped — blocks
+// b and b + 8 share an XCD (round-robin dispatch), each XCD walks a contiguous
+// range of pairs and a pair's nb blocks consecutively (heaviest first), so its
+// tiles are fetched once into that XCD's L2 and read by all of them.  Speed
+// only, never correctness (any mapping is a bijection of the grid).
+// r = 0 is the heaviest block of the pair.
+__device__ __forceinline__ void attn_block(int order, int nb, int BH, int& bh, int& r) {
+  const int id = blockIdx.x;
+  if (order == 0) {
+    bh = id % BH;
+    r = id / BH;
+    return;
+  }
+  const int nwg = BH * nb, xcd = id & 7, slot = id >> 3, q = nwg >> 3, rem = nwg & 7;
+  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + slot;
+  bh = L / nb;
+  r = L - bh * nb;
+}
+
 // ----- global → register → LDS staging of a [64 rows][64] tile (256 threads) -----
 struct Stage {
   bf16x8 v[2];
@@ -284,12 +305,14 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
 }
 
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                     float* __restrict__ lse, int B, int S, int H, float c2) {
+                                                     float* __restrict__ lse, int B, int S, int H, float c2,
+                                                     int order) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
-  const int bh = blockIdx.x % (B * H);
-  const int qb = nqb - 1 - blockIdx.x / (B * H);  // heaviest query blocks first
+  int bh, r_;
+  attn_block(order, nqb, B * H, bh, r_);
+  const int qb = nqb - 1 - r_;  // heaviest query blocks first
   const int b = bh / H, h = bh % H;
   const size_t rs = (size_t)3 * H * HD;
   const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
@@ -410,6 +433,141 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
 }
 
 // ============================================================================
+// forward with an LDS-DMA ring (PDO_ATTN_FWD=3): the forward's structure, with
+// K / V tiles arriving by LDS-DMA two tiles ahead through 3 slots (the dK/dV
+// kernel's ring) instead of register staging one tile ahead — no staging
+// registers, no ds_write pass, and each tile's loads have ≈ 2 tiles of lead
+// ============================================================================
+__device__ __forceinline__ unsigned dma_voff_v(int lane, size_t row_stride) {
+  const int rr = lane >> 3;  // toff_v's swizzle sees row bit 1 only: one offset for every piece
+  return (unsigned)(((size_t)rr * row_stride + (size_t)(((lane & 7) ^ (((rr >> 1) & 1) << 2)) << 3)) * 2);
+}
+
+__global__ __launch_bounds__(256) void attn_fwd3_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                      float* __restrict__ lse, int B, int S, int H, float c2,
+                                                      int order) {
+  constexpr int SLOT = 2 * TROWS * HD;                                   // bf16 units: K then V (16 KiB)
+  __shared__ __attribute__((aligned(16))) bf16 smem[3 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int nqb = S / 128;
+  int bh, r_;
+  attn_block(order, nqb, B * H, bh, r_);
+  const int qb = nqb - 1 - r_;  // heaviest query blocks first
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+
+  const int q = qb * 128 + w * 32 + li;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
+  retire(qf);
+  prescale(qf, c2);
+
+  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = 0.f, l = 0.f;
+  f32x16 nm16 = zero16();
+  const int ntiles = (qb * 128 + 128) / TROWS;
+  const int wave_qmax = qb * 128 + w * 32 + 31;
+
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned vk0 = dma_voff(lane, rs, 0), vk1 = dma_voff(lane, rs, 1), vv = dma_voff_v(lane, rs);
+  auto issue = [&](int t, int slot) {  // this wave's 4 pieces (2 K, 2 V) of tile t
+    const unsigned base = lds0 + (unsigned)(slot * SLOT * 2);
+    dma_tile(kbase, rs, t * TROWS, wu, vk0, vk1, base);
+    dma_tile(vbase, rs, t * TROWS, wu, vv, vv, base + TROWS * HD * 2);
+  };
+  issue(0, 0);
+  if (ntiles > 1) issue(1, 1);
+  int sl = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles)
+      vm_wait<4>();  // this wave's pieces of tile t have landed (t + 1's 4 may still fly)
+    else
+      vm_wait<0>();
+    __syncthreads();  // ... and every other wave's; slot (sl + 2) % 3 (tile t - 1) is free again
+    if (t + 2 < ntiles) issue(t + 2, sl == 0 ? 2 : sl - 1);
+    const bf16* Kt = smem + sl * SLOT;
+    const bf16* Vt = Kt + TROWS * HD;
+    const int key0 = t * TROWS;
+    if (key0 <= wave_qmax) {
+      f32x16 s0 = nm16, s1 = nm16;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
+        s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
+      }
+      if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
+        const int d = q - key0 - 4 * hh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = (r & 3) + 8 * (r >> 2);
+          s0[r] = c > d ? -INFINITY : s0[r];
+          s1[r] = c + 32 > d ? -INFINITY : s1[r];
+        }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+      tmax = xhalf_max(tmax);
+      if (t == 0) {
+        m = tmax;
+        s0 -= tmax;
+        s1 -= tmax;
+        nm16 = bcast16(-m);
+      } else if (__any(tmax > 8.f)) {
+        const float d = tmax > 8.f ? tmax : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        m += d;
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+        s0 -= d;
+        s1 -= d;
+        nm16 = bcast16(-m);
+      }
+      f32x2 ls2 = {0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+      }
+      l += ls2[0] + ls2[1];
+      const bf16* V0 = Vt + vb0;
+      const bf16* V1 = Vt + vb1;
+      {
+        const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
+        o0 = mfma(tr_frag_v<0>(V0), p0, o0);
+        o1 = mfma(tr_frag_v<0>(V1), p0, o1);
+        o0 = mfma(tr_frag_v<32>(V0), p1, o0);
+        o1 = mfma(tr_frag_v<32>(V1), p1, o1);
+      }
+      {
+        const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
+        o0 = mfma(tr_frag_v<16>(V0), p0, o0);
+        o1 = mfma(tr_frag_v<16>(V1), p0, o1);
+        o0 = mfma(tr_frag_v<48>(V0), p1, o0);
+        o1 = mfma(tr_frag_v<48>(V1), p1, o1);
+      }
+    }
+    sl = sl == 2 ? 0 : sl + 1;
+  }
+  const float lt = xhalf_sum(l);
+  const float inv = 1.f / lt;
+  bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
+  store_acc_rows(orow, o0, 0, hh, inv);
+  store_acc_rows(orow, o1, 32, hh, inv);
+  if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
+}
+
+// ============================================================================
 // forward, two 32-query blocks per wave (PDO_ATTN_FWD=2): workgroup = 4 waves =
 // 256 queries.  Every K fragment (ds_read_b128) and V fragment (transposed
 // reads) feeds two MFMAs instead of one, and each wave carries two independent
@@ -422,12 +580,14 @@ struct FwdBlock {
 };
 
 __global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                         float* __restrict__ lse, int B, int S, int H, float c2) {
+                                                         float* __restrict__ lse, int B, int S, int H, float c2,
+                                                         int order) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 256;
-  const int bh = blockIdx.x % (B * H);
-  const int qb = nqb - 1 - blockIdx.x / (B * H);  // heaviest query blocks first
+  int bh, r_;
+  attn_block(order, nqb, B * H, bh, r_);
+  const int qb = nqb - 1 - r_;  // heaviest query blocks first
   const int b = bh / H, h = bh % H;
   const size_t rs = (size_t)3 * H * HD;
   const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
@@ -581,14 +741,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                          const float* __restrict__ lse, const float* __restrict__ delta,
                                                          bf16* __restrict__ dqkv, int B, int S, int H, float c2,
-                                                         float scale, float* __restrict__ dbias_part) {
+                                                         float scale, float* __restrict__ dbias_part, int order) {
   // ring of 3 slots × {Q [64][64] bf16, dO [64][64] bf16, lse·log2e [64] f32, delta [64] f32}
   constexpr int SLOT = 2 * TROWS * HD + 2 * TROWS * 2;  // bf16 units (16896 B)
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nkb = S / 128;
-  const int bh = blockIdx.x % (B * H);
-  const int kb = blockIdx.x / (B * H);  // lowest key blocks have the most query tiles: issue first
+  int bh, kb;
+  attn_block(order, nkb, B * H, bh, kb);  // lowest key blocks have the most query tiles: issue first
   const int b = bh / H, h = bh % H;
   const size_t rs = (size_t)3 * H * HD;
   const size_t ors = (size_t)H * HD;
@@ -599,7 +759,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
   const float* lse2_bh = delta + (size_t)B * H * S + (size_t)bh * S;  // −lse·log2e, written by the dQ kernel
   const float* del_bh = delta + (size_t)bh * S;
   (void)lse;
-  (void)nkb;
 
   const int key = kb * 128 + w * 32 + li;  // this lane's key (column of S / dP)
   bf16x8 kf[4], vf[4];
@@ -730,12 +889,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
-                                                       int H, float c2, float scale, float* __restrict__ dbias_part) {
+                                                       int H, float c2, float scale, float* __restrict__ dbias_part,
+                                                       int order) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
-  const int bh = blockIdx.x % (B * H);
-  const int qb = nqb - 1 - blockIdx.x / (B * H);
+  int bh, r_;
+  attn_block(order, nqb, B * H, bh, r_);
+  const int qb = nqb - 1 - r_;
   const int b = bh / H, h = bh % H;
   const size_t rs = (size_t)3 * H * HD;
   const size_t ors = (size_t)H * HD;
@@ -850,18 +1011,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
 }
 
+static int env_int(const char* k, int def) {
+  const char* e = getenv(k);
+  return e && *e ? atoi(e) : def;
+}
+static int attn_order() {
+  static const int o = env_int("PDO_ATTN_ORDER", 0);
+  return o;
+}
+
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
-  static const int variant = [] {
-    const char* e = getenv("PDO_ATTN_FWD");
-    return e && *e ? atoi(e) : 1;
-  }();
+  static const int variant = env_int("PDO_ATTN_FWD", 1);
+  if (variant == 3) {
+    attn_fwd3_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+    return 0;
+  }
   if (variant == 2 && S % 256 == 0) {
-    attn_fwd2_d64<<<B * H * (S / 256), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E);
+    attn_fwd2_d64<<<B * H * (S / 256), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
     return 0;
   }
   const int grid = B * H * (S / 128);
-  attn_fwd_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E);
+  attn_fwd_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   return 0;
 }
 
@@ -870,8 +1041,10 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part);
-  attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part);
+  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
+                                        attn_order());
+  attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
+                                          attn_order());
   return 0;
 }
 

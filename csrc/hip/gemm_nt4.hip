@@ -108,6 +108,19 @@ __device__ __forceinline__ void transpose_blocks(u32x2 (&b)[4]) {
 //          under the last quarter of tile t's MFMAs.  Every DMA piece has
 //          ≈ 1.3-1.6 tiles of lead instead of ≈ 0.6.
 // SCHED & 2: the register epilogue (below) instead of the LDS-staged one.
+// SCHED & 4: row-major accumulators (with SCHED & 1).  The MFMAs take A as
+//          SrcA, so a lane's 4 accumulator values of a 16×16 block are 4
+//          consecutive output ROWS; and B's tile rows sit permuted in LDS
+//          (physical row 128h + q holds row 128h + 8(q & 15) + (q >> 4)), so
+//          column c of block j is output column 8c + j: a lane holds 8
+//          consecutive columns of each of its rows across blocks j = 0-7.  The
+//          epilogue then stores 16 B per lane straight from the accumulators,
+//          4 rows × 256 B per instruction, no LDS round trip and no barrier (the
+//          layout of hipBLASLt's MT256x256x64 epilogue: 32 dwordx4 stores per
+//          wave).  The permutation costs nothing: it is the DMA source address
+//          (8-row lane stride, per-piece scalar base); the LDS image and the
+//          fragment reads are unchanged.
+// SCHED & 8: non-temporal C stores (keep the A / B panels in L2).
 template <int EPI, int EPG, int BAR, int BUFLD, int SCHED = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
@@ -147,10 +160,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   // piece costs scalar adds instead of 64-bit vector address arithmetic.
   const int rb = lane >> 3;
   const int csrc = (lane & 7) ^ (4 * (w & 1) + (lane >> 4));
-  const unsigned voffA = (unsigned)((rb * lda + csrc * 8) * 2), voffB = (unsigned)((rb * ldb + csrc * 8) * 2);
+  static_assert(!(SCHED & 4) || ((SCHED & 1) && !(BUFLD & 1)), "row-major accumulators: SCHED 1 mainloop, global_load_lds");
+  // SCHED & 4: physical B row 8(w + 4p) + q' (wave w, piece p, q' = l >> 3) holds
+  // row 128(p >> 2) + 64(w & 1) + (w >> 1) + 2(p & 3) + 8q' — lane stride 8 rows,
+  // piece stride 2 rows (and 128 for the second half); same swizzle (physical row)
+  const unsigned voffA = (unsigned)((rb * lda + csrc * 8) * 2);
+  const unsigned voffB = (SCHED & 4) ? (unsigned)((8 * rb * ldb + csrc * 8) * 2) : (unsigned)((rb * ldb + csrc * 8) * 2);
   const bf16* baseA = A + ((size_t)m0 + 8 * w) * lda;
-  const bf16* baseB = B + ((size_t)n0 + 8 * w) * ldb;
-  const unsigned stepAb = (unsigned)(64 * lda), stepBb = (unsigned)(64 * ldb);  // 32 rows, bytes
+  const bf16* baseB = (SCHED & 4) ? B + ((size_t)n0 + 64 * (w & 1) + (w >> 1)) * ldb : B + ((size_t)n0 + 8 * w) * ldb;
+  const unsigned stepAb = (unsigned)(64 * lda);                                                // 32 rows, bytes
+  const unsigned stepBb = (SCHED & 4) ? (unsigned)(4 * ldb) : (unsigned)(64 * ldb);            // 2 / 32 rows
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem + (unsigned)(w * 1024);
   // M0 is not saved around the DMA: nothing else in this kernel uses it (check
   // the .s for other M0 readers after editing); s_nop 0 = the SALU M0 write →
@@ -202,7 +221,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       else bld(voffB, rsB, ko + (p - 8) * sr.sb, base + OPB + (unsigned)(4096 * (p - 8)));
     } else {
       if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
-      else glds(voffB, reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+      else {
+        const int pp = p - 8;
+        const unsigned mul = (SCHED & 4) ? (unsigned)((pp & 3) + 64 * (pp >> 2)) : (unsigned)pp;
+        glds(voffB, reinterpret_cast<const bf16*>(sr.b + mul * sr.sb), base + OPB + (unsigned)(4096 * pp));
+      }
     }
   };
 
@@ -291,11 +314,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       static_for<128>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
         constexpr int i = s & 7, j = (s >> 3) & 7;
+        // SrcA / SrcB: B / A (column-major accumulators) or A / B (SCHED & 4)
         if constexpr (s < 64) {
-          if constexpr (FIRST) mma0(acc[i][j], fb0[j], fa0[i]);
-          else mma(acc[i][j], fb0[j], fa0[i]);
+          if constexpr (FIRST) {
+            if constexpr (SCHED & 4) mma0(acc[i][j], fa0[i], fb0[j]);
+            else mma0(acc[i][j], fb0[j], fa0[i]);
+          } else {
+            if constexpr (SCHED & 4) mma(acc[i][j], fa0[i], fb0[j]);
+            else mma(acc[i][j], fb0[j], fa0[i]);
+          }
         } else {
-          mma(acc[i][j], fb1[j], fa1[i]);
+          if constexpr (SCHED & 4) mma(acc[i][j], fa1[i], fb1[j]);
+          else mma(acc[i][j], fb1[j], fa1[i]);
         }
         if constexpr (s < 16 && (s & 1) == 0) fa1[s >> 1] = rdA(SB{}, 1, s >> 1);
         if constexpr (LOAD && s == 23) {
@@ -455,6 +485,75 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
                  : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
     return v;
   };
+  auto st16 = [](bf16* p, bf16x8 v) {
+    if constexpr (SCHED & 8) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+    else *reinterpret_cast<bf16x8*>(p) = v;
+  };
+  if constexpr (SCHED & 4) {
+    // ---- row epilogue: acc[i][j][e] = C[m][n], m = wm·128 + 16i + 4(l >> 4) + e,
+    // n = wn·128 + 8(l & 15) + j.  Per (i, e) a lane stores 8 consecutive
+    // columns; the 64 lanes cover 4 rows × 128 columns.  Same per-element math
+    // and roundings as the LDS-staged path below.
+    const int g4 = lane >> 4;
+    const int nb = n0 + wn * 128 + 8 * (lane & 15);
+    const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
+    bf16x8 pre[EPI == 3 ? 32 : 1];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
+    }
+    f32x8 bv8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI >= 1) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
+    f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    f32x2 m1 = {-1.f, -1.f};
+    asm volatile("" : "+v"(m1));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = rd_acc(acc[i][j]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x8 v = {a[0][e], a[1][e], a[2][e], a[3][e], a[4][e], a[5][e], a[6][e], a[7][e]};
+        const size_t m = mr + 16 * i + e;
+        bf16* crow = C + m * ldc + nb;
+        if constexpr (EPI <= 1) {
+          st16(crow, to_bf16(v + bv8));
+        } else if constexpr (EPI == 2) {
+          const bf16x8 o = to_bf16(v);
+          st16(crow, o);
+          const f32x8 x = to_f32(o) + bv8;
+          f32x8 y;
+#pragma unroll
+          for (int q = 0; q < 8; q += 2) {
+            const f32x2 gg = gelu_sig2(f32x2{x[q], x[q + 1]});
+            y[q] = gg[0];
+            y[q + 1] = gg[1];
+          }
+          st16(Y + m * ldy + nb, to_bf16(y));
+        } else {
+          const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
+          const f32x8 dy = to_f32(to_bf16(v));
+          f32x8 d;
+#pragma unroll
+          for (int q = 0; q < 8; q += 2) {
+            const f32x2 gg = f32x2{dy[q], dy[q + 1]} * gelu_sig_grad2(f32x2{x[q], x[q + 1]}, m1);
+            d[q] = gg[0];
+            d[q + 1] = gg[1];
+          }
+          colp += d;
+          st16(crow, to_bf16(d));
+        }
+      }
+    }
+    if constexpr (EPI == 3) {
+      // partial row 4·wm + (l >> 4) of this M-tile's 8: the rows 16i + 4(l >> 4) + e
+      float* prow = dbias_part + (size_t)(8 * tm + 4 * wm + g4) * N + nb;
+      *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
+      *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
+    }
+    return;
+  }
   if constexpr (SCHED & 2) {
     // ---- register epilogue: no LDS round trip, no barrier.  Per 16-row block
     // i and 4-block column group h, the 4 lanes {r, r+16, r+32, r+48} hold a
@@ -608,9 +707,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + r * 512 + ((c ^ (r & 31)) << 4));
     const size_t m = (size_t)(m0 + r);
     if constexpr (EPI <= 1) {
-      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+      st16(C + m * ldc + n, v);
     } else if constexpr (EPI == 2) {
-      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+      st16(C + m * ldc + n, v);
       const f32x8 x = to_f32(v) + bv8;
       f32x8 y;
 #pragma unroll
@@ -619,7 +718,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         y[e] = g[0];
         y[e + 1] = g[1];
       }
-      *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
+      st16(Y + m * ldy + n, to_bf16(y));
     } else {
       const f32x8 x = to_f32(pre[it]) + bv8;
       const f32x8 dy = to_f32(v);
@@ -631,7 +730,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         d[e + 1] = g[1];
       }
       colp += d;
-      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(d);
+      st16(C + m * ldc + n, to_bf16(d));
     }
   }
   if constexpr (EPI == 3) {
@@ -677,6 +776,8 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   using I7 = std::integral_constant<int, 7>;
   using I11 = std::integral_constant<int, 11>;
   using I13 = std::integral_constant<int, 13>;
+  using I5 = std::integral_constant<int, 5>;
+  using I9 = std::integral_constant<int, 9>;
   // schedule variants under A/B (tools/nt4_probe.py, profiles/r2_gemm_nt4.md):
   // 0 = barrier after block-1 group 11, the first 4 DMA pieces of tile t+2 after it, the rest one per
   // block-0 group, B-stationary MFMA order (each group's 4 MFMAs share SrcA; default: 1-4 % faster
@@ -691,6 +792,9 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
     case 4: return launch(I1{}, I11{}, I0{}, I0{});  // variant 0 with the A-stationary order
     case 6: return launch(I1{}, I11{}, I2{}, I3{});
     case 7: return launch(I1{}, I11{}, I2{}, I0{});  // the round-2 default (SCHED 0)
+    case 8: return launch(I1{}, I11{}, I2{}, I5{});   // row-major accumulators, direct row epilogue
+    case 9: return launch(I1{}, I11{}, I2{}, I13{});  // the same with non-temporal stores
+    case 10: return launch(I1{}, I11{}, I2{}, I9{});  // LDS-staged epilogue, non-temporal stores
     default: return launch(I1{}, I11{}, I2{}, I1{});
   }
   return 0;

@@ -167,7 +167,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.b = b
-        return F.linear(x, w, b)
+        return _fwd_gemm(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
@@ -226,6 +226,23 @@ def _splitk(tokens: int, m: int, n: int) -> int:
 
 _DX_TN = [os.environ.get("PDO_DX_TN", "1") != "0"]
 
+# Every forward-layout GEMM (y = x·Wᵀ (+ b): QKV / proj / fc2 forward, the
+# input-gradient GEMMs as F.linear(dY, Wᵀ), the LM head) on the hand-written
+# gemm_nt4 instead of hipBLASLt, where its shape contract holds (M, N % 256,
+# K % 128).  PDO_NT_ALL=0 keeps the library for the GEMMs without a fused epilogue.
+_NT_ALL = [os.environ.get("PDO_NT_ALL", "0") == "1"]
+
+
+def _fwd_gemm(x, w, b=None):
+    """F.linear(x, w, b) — on gemm_nt4 under _NT_ALL when the shapes allow."""
+    if (_NT_ALL[0] and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.is_contiguous() and w.is_contiguous() and (b is None or b.dtype == torch.bfloat16)):
+        x2 = x.reshape(-1, x.shape[-1])
+        m = _native.require_hip()
+        if m.gemm_nt_supported(x2.shape[0], w.shape[0], w.shape[1]):
+            return m.gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
+    return F.linear(x, w, b)
+
 
 def _input_grad(dy2, w):
     """dX = dY·W as the forward's GEMM form F.linear(dY, Wᵀ).
@@ -236,7 +253,7 @@ def _input_grad(dy2, w):
     HIP transpose (csrc/hip/transpose.hip) at the HBM rate — PyTorch's strided
     copy took ≈25 µs per projection weight, 2.4 ms per GPT-2-medium step."""
     if _DX_TN[0] and dy2.is_cuda:
-        return F.linear(dy2, transpose(w))
+        return _fwd_gemm(dy2, transpose(w))
     return dy2 @ w
 
 
@@ -449,7 +466,7 @@ class _GeluLinearFn(torch.autograd.Function):
         ctx.save_for_backward(hp2, h, w2)
         ctx.b1 = b1
         ctx.shape = hp.shape
-        return F.linear(h, w2).view(*hp.shape[:-1], w2.shape[0])
+        return _fwd_gemm(h, w2).view(*hp.shape[:-1], w2.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
@@ -488,7 +505,7 @@ class _NTMLPFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w1, hp, h, w2)
         ctx.b1 = b1
         ctx.shape = x.shape
-        return F.linear(h, w2).view(*x.shape[:-1], w2.shape[0])
+        return _fwd_gemm(h, w2).view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
@@ -591,7 +608,7 @@ class _QKVAttnFn(torch.autograd.Function):
     def forward(ctx, h, w, b, n_head):
         m = _native.require_hip()
         h2 = h.reshape(-1, h.shape[-1])
-        qkv = F.linear(h2, w, b).view(*h.shape[:-1], w.shape[0])
+        qkv = _fwd_gemm(h2, w, b).view(*h.shape[:-1], w.shape[0])
         o, lse = m.attn_fwd(qkv, n_head)
         ctx.save_for_backward(h2, w, qkv, o, lse)
         ctx.b = b

@@ -88,8 +88,10 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
         ref = hip.gemm_nt(a, b, bias)
         ref_p, ref_y = hip.gemm_nt_gelu(a, b, bias)
         ref_dx, ref_db = hip.gemm_nt_dgelu(a, b, pre, bias)
-        for impl in (1, 2, 3, 4, 5, 6, 7, 8):
+        for impl in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11):
             hip.gemm_nt_impl(impl)
+            # impls 9 / 10 feed the MFMAs A as SrcA (row-major accumulators): the
+            # products and their k order are the same, so they still match bitwise
             assert torch.equal(hip.gemm_nt(a, b, bias), ref), impl
             p, y = hip.gemm_nt_gelu(a, b, bias)
             assert torch.equal(p, ref_p) and torch.equal(y, ref_y), impl
@@ -103,8 +105,8 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
         hip.gemm_nt_impl(prev)
 
 
-@pytest.mark.parametrize("M,N,K,impl", [(65536, 4096, 1024, 1), (65536, 4096, 1024, 7),
-                                        (3328, 1024, 3072, 1), (3328, 1024, 3072, 7)])
+@pytest.mark.parametrize("M,N,K,impl", [(65536, 4096, 1024, 1), (65536, 4096, 1024, 7), (65536, 4096, 1024, 9),
+                                        (3328, 1024, 3072, 1), (3328, 1024, 3072, 7), (3328, 1024, 3072, 9)])
 def test_nt4_production_shapes_vs_fp32(hip, M, N, K, impl):
     """Production-size grids: M = 65536 (4096 tiles: XCD remap over every tile,
     grouped order across 32 groups of 8 tile rows) and M = 3328 (13 tile rows,
