@@ -227,19 +227,32 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
+// impl 0 = the 8-wave ring below, impl v + 1 = gemm_nt4 schedule variant v,
+// impl 13 (default) = per epilogue: the mirrored row-accumulator schedule
+// (variant 11), the unmirrored one (variant 9) for the GELU epilogue
+// (tools/nt4_probe.py, profiles/r3_gemm_nt4_rows.md).  PDO_NT_IMPL overrides
+// (A/B in the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=8 PDO_NT_IMPL=13')
+static int g_impl = [] {
+  const char* e = getenv("PDO_NT_IMPL");
+  return e && *e ? atoi(e) : 13;
+}();
+
+static int nt4_variant(int epi) {
+  if (g_impl == 13) return epi == 2 ? 9 : 11;
+  return g_impl - 1;
+}
+
+// N % 256 = 128 (the 50304-column LM head) only on the 4-wave row-accumulator variants
+static bool nt4_path(int K) { return g_impl >= 1 && K % 128 == 0 && K >= 256; }
+
 int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
-  return M > 0 && N > 0 && K >= 64 && M % BM == 0 && N % BN == 0 && K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+  const bool nok = N % BN == 0 || (N % BN == BN / 2 && nt4_path(K) && gemm_nt4_half_n(nt4_variant(0)) &&
+                                   gemm_nt4_half_n(nt4_variant(2)));
+  return M > 0 && N > 0 && K >= 64 && M % BM == 0 && nok && K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          ldc % 4 == 0 && lda >= K && ldb >= K && ldc >= N;
 }
 
 int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
-
-// 1 = 4-wave mainloop, variant 0 (tools/nt4_probe.py); PDO_NT_IMPL overrides
-// (A/B in the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=8 PDO_NT_IMPL=1')
-static int g_impl = [] {
-  const char* e = getenv("PDO_NT_IMPL");
-  return e && *e ? atoi(e) : 1;
-}();
 void gemm_nt_set_impl(int impl) { g_impl = impl; }
 int gemm_nt_get_impl() { return g_impl; }
 
@@ -249,8 +262,8 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
   if (epi != 0 && !bias) return -3;
   if ((epi == 2 || epi == 3) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
-  if (g_impl >= 1 && K % 128 == 0 && K >= 256)
-    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, g_impl - 1);
+  if (nt4_path(K))
+    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, nt4_variant(epi));
   const long long grid = (long long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;

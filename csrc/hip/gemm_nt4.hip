@@ -121,6 +121,9 @@ __device__ __forceinline__ void transpose_blocks(u32x2 (&b)[4]) {
 //          (8-row lane stride, per-piece scalar base); the LDS image and the
 //          fragment reads are unchanged.
 // SCHED & 8: non-temporal C stores (keep the A / B panels in L2).
+// SCHED & 16: with SCHED & 4, the mirror-image schedule — runs of 8 MFMAs share
+//          the SrcA operand (A fragment i) as hipBLASLt's loop does, and the
+//          operands trade places in the read / release / refill order.
 template <int EPI, int EPG, int BAR, int BUFLD, int SCHED = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int tiles_n = N / BN;
+  const int tiles_n = (N + BN - 1) / BN;  // SCHED & 4: N % 256 = 128 allowed (half-width last tile column)
   const int nwg = (M / BM) * tiles_n;
   int id = blockIdx.x;
   {  // bijective XCD remap: each XCD walks a contiguous range of tiles (shared A panels in its L2)
@@ -151,6 +154,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     tn = r / gsz;
   }
   const int m0 = tm * BM, n0 = tn * BN;
+  // half-width tile (only N - n0 = 128 columns exist): the B pieces of the upper
+  // half re-read the lower half's rows (in bounds), the wn = 1 waves store nothing
+  const bool halfn = (SCHED & 4) && n0 + BN > N;
 
   // ---- LDS-DMA sources.  Wave w fills 8-row blocks b = w + 4i (i = 0..7) of
   // both operands; lane l → row 8b + (l >> 3), LDS chunk l & 7, global chunk
@@ -223,7 +229,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
       else {
         const int pp = p - 8;
-        const unsigned mul = (SCHED & 4) ? (unsigned)((pp & 3) + 64 * (pp >> 2)) : (unsigned)pp;
+        const unsigned mul = (SCHED & 4) ? (unsigned)((pp & 3) + (halfn ? 0 : 64) * (pp >> 2)) : (unsigned)pp;
         glds(voffB, reinterpret_cast<const bf16*>(sr.b + mul * sr.sb), base + OPB + (unsigned)(4096 * pp));
       }
     }
@@ -263,6 +269,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
   if constexpr (SCHED & 1) {
+    constexpr bool MIR = (SCHED & 16) != 0;
+    static_assert(!MIR || (SCHED & 4), "the mirrored schedule feeds A as SrcA");
     // fragment i of A (rows wm·128 + 16i + (l & 15)) / B, k half kk, from buffer BUF
     auto rdA = [&](auto buf_tag, int kk, int i) -> bf16x8 {
       constexpr int BUF = decltype(buf_tag)::value;
@@ -274,10 +282,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     };
     // F0 (k 0-31) reads of a tile in the order its first MFMA run consumes them:
     // B fragment 0 (the run's stationary operand), A 0-7, then B 1-7
+    // (MIR: the mirror image — A fragment 0 stationary first, B 0-7, then A 1-7)
     auto rdF0 = [&](auto buf_tag, int q) {
-      if (q == 0) fb0[0] = rdB(buf_tag, 0, 0);
-      else if (q <= 8) fa0[q - 1] = rdA(buf_tag, 0, q - 1);
-      else fb0[q - 8] = rdB(buf_tag, 0, q - 8);
+      if constexpr (MIR) {
+        if (q == 0) fa0[0] = rdA(buf_tag, 0, 0);
+        else if (q <= 8) fb0[q - 1] = rdB(buf_tag, 0, q - 1);
+        else fa0[q - 8] = rdA(buf_tag, 0, q - 8);
+      } else {
+        if (q == 0) fb0[0] = rdB(buf_tag, 0, 0);
+        else if (q <= 8) fa0[q - 1] = rdA(buf_tag, 0, q - 1);
+        else fb0[q - 8] = rdB(buf_tag, 0, q - 8);
+      }
     };
     // ---- prologue: tiles 0 and 1 in flight, wait for tile 0, its F0 fragments
     {
@@ -313,7 +328,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       if constexpr (LOAD) sn2 = srcs(t + 2);
       static_for<128>([&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        constexpr int i = s & 7, j = (s >> 3) & 7;
+        // runs of 8 MFMAs share the B fragment j (MIR: the A fragment i, = SrcA)
+        constexpr int i = MIR ? (s >> 3) & 7 : s & 7, j = MIR ? s & 7 : (s >> 3) & 7;
         // SrcA / SrcB: B / A (column-major accumulators) or A / B (SCHED & 4)
         if constexpr (s < 64) {
           if constexpr (FIRST) {
@@ -327,20 +343,28 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           if constexpr (SCHED & 4) mma(acc[i][j], fa1[i], fb1[j]);
           else mma(acc[i][j], fb1[j], fa1[i]);
         }
-        if constexpr (s < 16 && (s & 1) == 0) fa1[s >> 1] = rdA(SB{}, 1, s >> 1);
+        // MIR swaps the operands' roles below: B's k 32-63 fragments first, B's
+        // half of the buffer released at barrier 1 and refilled first, A's at barrier 2
+        if constexpr (s < 16 && (s & 1) == 0) {
+          if constexpr (MIR) fb1[s >> 1] = rdB(SB{}, 1, s >> 1);
+          else fa1[s >> 1] = rdA(SB{}, 1, s >> 1);
+        }
         if constexpr (LOAD && s == 23) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (LOAD && s >= 24 && s < 48 && (s - 24) % 3 == 0) dma(sn2, SB{}, (s - 24) / 3);
-        if constexpr (s >= 25 && s < 49 && (s - 25) % 3 == 0) fb1[(s - 25) / 3] = rdB(SB{}, 1, (s - 25) / 3);
+        if constexpr (LOAD && s >= 24 && s < 48 && (s - 24) % 3 == 0) dma(sn2, SB{}, (MIR ? 8 : 0) + (s - 24) / 3);
+        if constexpr (s >= 25 && s < 49 && (s - 25) % 3 == 0) {
+          if constexpr (MIR) fa1[(s - 25) / 3] = rdA(SB{}, 1, (s - 25) / 3);
+          else fb1[(s - 25) / 3] = rdB(SB{}, 1, (s - 25) / 3);
+        }
         if constexpr (LOAD && s == 51) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (LOAD && s >= 52 && s < 92 && (s - 52) % 5 == 0) dma(sn2, SB{}, 8 + (s - 52) / 5);
+        if constexpr (LOAD && s >= 52 && s < 92 && (s - 52) % 5 == 0) dma(sn2, SB{}, (MIR ? 0 : 8) + (s - 52) / 5);
         if constexpr (MORE && s == 93) {
           // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in flight)
           if constexpr (LOAD) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -494,6 +518,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     // n = wn·128 + 8(l & 15) + j.  Per (i, e) a lane stores 8 consecutive
     // columns; the 64 lanes cover 4 rows × 128 columns.  Same per-element math
     // and roundings as the LDS-staged path below.
+    if (halfn && wn == 1) return;
     const int g4 = lane >> 4;
     const int nb = n0 + wn * 128 + 8 * (lane & 15);
     const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
@@ -743,9 +768,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 
 }  // namespace
 
+// the variants with row-major accumulators (SCHED & 4) take N % 256 = 128
+int gemm_nt4_half_n(int variant) { return variant == 8 || variant == 9 || variant == 11; }
+
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
              const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant) {
-  const long long grid = (long long)(M / BM) * (N / BN);
+  if (N % BN && !(N % BN == BN / 2 && gemm_nt4_half_n(variant))) return -2;
+  const long long grid = (long long)(M / BM) * ((N + BN - 1) / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;
   if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
@@ -795,6 +824,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
     case 8: return launch(I1{}, I11{}, I2{}, I5{});   // row-major accumulators, direct row epilogue
     case 9: return launch(I1{}, I11{}, I2{}, I13{});  // the same with non-temporal stores
     case 10: return launch(I1{}, I11{}, I2{}, I9{});  // LDS-staged epilogue, non-temporal stores
+    case 11: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 29>{});  // impl 10 + mirrored schedule
     default: return launch(I1{}, I11{}, I2{}, I1{});
   }
   return 0;

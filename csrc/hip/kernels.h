@@ -79,6 +79,8 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
 // gemm_nt4.hip: the same contract on the 4-wave / 128 × 128-per-wave mainloop
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
              const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant = 0);
+// the gemm_nt4 variants that also take N % 256 = 128 (half-width last tile column)
+int gemm_nt4_half_n(int variant);
 // which mainloop gemm_nt() runs: 0 = 8-wave ring (gemm_nt.hip), 1.. = 4-wave (gemm_nt4.hip)
 // schedule variant impl - 1
 void gemm_nt_set_impl(int impl);

@@ -12,7 +12,9 @@ MI355X-first rather than a transcription of any reference implementation:
 * residual add + LayerNorm are one kernel, bias + GELU is one kernel (with the
   bias gradient reduced inside the backward kernel), embedding gather + position
   add is one kernel;
-* all dense projections are plain hipBLASLt GEMMs (``torch.mm``) on bf16.
+* dense projections run on the hand-written gemm_nt4 / gemm_dw4 kernels where
+  a fused epilogue pays (ops.mlp, weight gradients) and on hipBLASLt or
+  gemm_nt4 (PDO_NT_ALL) otherwise.
 
 The reference operator has no model code at all; this workload
 is what a PaddleJob launches (``deploy/examples/resnet.yaml:14-19`` pattern).
@@ -20,7 +22,8 @@ is what a PaddleJob launches (``deploy/examples/resnet.yaml:14-19`` pattern).
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+import os
+from dataclasses import dataclass, field
 
 import torch
 import torch.nn as nn
@@ -36,7 +39,9 @@ class GPT2Config:
     n_layer: int = 24
     n_head: int = 16
     ln_eps: float = 1e-5
-    pad_vocab_to: int = 128
+    # 128: 50304 rows.  256 (PDO_PAD_VOCAB=256): 50432, full 256-wide tiles, so the
+    # LM head's forward / dX GEMMs enter gemm_nt4 and its dW gemm_dw4's full-height tiles
+    pad_vocab_to: int = field(default_factory=lambda: int(os.environ.get("PDO_PAD_VOCAB", "128")))
 
     @property
     def padded_vocab(self) -> int:

@@ -229,13 +229,17 @@ _DX_TN = [os.environ.get("PDO_DX_TN", "1") != "0"]
 # Every forward-layout GEMM (y = x·Wᵀ (+ b): QKV / proj / fc2 forward, the
 # input-gradient GEMMs as F.linear(dY, Wᵀ), the LM head) on the hand-written
 # gemm_nt4 instead of hipBLASLt, where its shape contract holds (M, N % 256,
-# K % 128).  PDO_NT_ALL=0 keeps the library for the GEMMs without a fused epilogue.
-_NT_ALL = [os.environ.get("PDO_NT_ALL", "0") == "1"]
+# K % 128, or N % 256 = 128 like the 50304-column LM head).  Default since the
+# row-accumulator schedules (profiles/r3_gemm_nt4_rows.md): no hipBLASLt kernel
+# in the step.  PDO_NT_ALL=0 keeps the library for the GEMMs without a fused
+# epilogue, 1 routes all of them, any larger value routes those with K ≤ it.
+_NT_ALL = [int(os.environ.get("PDO_NT_ALL", "1"))]
 
 
 def _fwd_gemm(x, w, b=None):
     """F.linear(x, w, b) — on gemm_nt4 under _NT_ALL when the shapes allow."""
-    if (_NT_ALL[0] and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+    if (_NT_ALL[0] and (_NT_ALL[0] == 1 or x.shape[-1] <= _NT_ALL[0])
+            and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.is_contiguous() and w.is_contiguous() and (b is None or b.dtype == torch.bfloat16)):
         x2 = x.reshape(-1, x.shape[-1])
         m = _native.require_hip()

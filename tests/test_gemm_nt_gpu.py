@@ -88,9 +88,9 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
         ref = hip.gemm_nt(a, b, bias)
         ref_p, ref_y = hip.gemm_nt_gelu(a, b, bias)
         ref_dx, ref_db = hip.gemm_nt_dgelu(a, b, pre, bias)
-        for impl in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11):
+        for impl in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13):
             hip.gemm_nt_impl(impl)
-            # impls 9 / 10 feed the MFMAs A as SrcA (row-major accumulators): the
+            # impls 9, 10 and 12 feed the MFMAs A as SrcA (row-major accumulators): the
             # products and their k order are the same, so they still match bitwise
             assert torch.equal(hip.gemm_nt(a, b, bias), ref), impl
             p, y = hip.gemm_nt_gelu(a, b, bias)
@@ -106,7 +106,8 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K,impl", [(65536, 4096, 1024, 1), (65536, 4096, 1024, 7), (65536, 4096, 1024, 9),
-                                        (3328, 1024, 3072, 1), (3328, 1024, 3072, 7), (3328, 1024, 3072, 9)])
+                                        (3328, 1024, 3072, 1), (3328, 1024, 3072, 7), (3328, 1024, 3072, 9),
+                                        (65536, 1024, 4096, 13), (3328, 50304, 1024, 13)])
 def test_nt4_production_shapes_vs_fp32(hip, M, N, K, impl):
     """Production-size grids: M = 65536 (4096 tiles: XCD remap over every tile,
     grouped order across 32 groups of 8 tile rows) and M = 3328 (13 tile rows,
@@ -124,3 +125,35 @@ def test_nt4_production_shapes_vs_fp32(hip, M, N, K, impl):
     err = (c.float() - ref).abs()
     tol = 1e-2 + 8e-3 * ref.abs()
     assert bool((err <= tol).all()), f"max err {err.max().item():.4f} at {int(err.argmax())}"
+
+
+@pytest.mark.parametrize("impl", [9, 10, 12, 13])
+def test_nt4_half_width_last_tile(hip, impl):
+    """N % 256 = 128 (the 50304-column LM head) on the row-accumulator variants:
+    the last tile column is half wide; its upper-half waves store nothing and
+    their B reads stay in bounds.  Plain, bias, GELU and dGELU epilogues vs fp32."""
+    M, N, K = 768, 640, 512
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.1, 0.1, generator=g)
+    bias = torch.empty(N, device="cuda", dtype=torch.bfloat16).uniform_(-0.1, 0.1, generator=g)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16).uniform_(-2, 2, generator=g)
+    prev = hip.gemm_nt_impl(impl)
+    try:
+        assert hip.gemm_nt_supported(M, N, K)
+        c = hip.gemm_nt(a, b, None)
+        cb = hip.gemm_nt(a, b, bias)
+        p, y = hip.gemm_nt_gelu(a, b, bias)
+        dx, db = hip.gemm_nt_dgelu(a, b, pre, bias)
+    finally:
+        hip.gemm_nt_impl(prev)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(cb.float(), ref + bias.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(p.float(), ref, rtol=1e-2, atol=1e-2)
+    x = p.float() + bias.float()
+    torch.testing.assert_close(y.float(), torch.nn.functional.gelu(x, approximate="tanh"), rtol=2e-2, atol=2e-2)
+    xp = (pre.float() + bias.float()).requires_grad_(True)
+    torch.nn.functional.gelu(xp, approximate="tanh").backward(ref.to(torch.bfloat16).float())
+    torch.testing.assert_close(dx.float(), xp.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=3e-2, atol=0.5)

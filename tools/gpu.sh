@@ -59,7 +59,7 @@ run_step() {
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 "$R/tools/$s" "${rest[@]}" ) \
         > "$O/prof_${s%.py}.log" 2>&1 || { tail -30 "$O/prof_${s%.py}.log"; return 1; }
       local db; db=$(find "$d" -name '*.db' | head -1)
-      local steps=1; [[ $kind == step ]] && steps=7
+      local steps=1; [[ $kind == step ]] && steps=9  # 2 warmup + 7 timed steps are all traced
       python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/prof_${s%.py}.md" && rm -rf "$d"
       tail -5 "$O/prof_${s%.py}.log"; head -45 "$O/prof_${s%.py}.md" ;;
     pmc)
