@@ -297,6 +297,18 @@ __device__ __forceinline__ int tr_base_v(int cbase, int lane) {
   return toff_v(r0, col >> 3) + (col & 7);
 }
 
+// PRIO: wave priority 1 while issuing a run of MFMAs, 0 for the softmax VALU
+// work, so the SIMD's arbiter keeps the matrix pipe fed from whichever of its
+// waves is in an MFMA phase while the others' exp / max / pack fill the gaps
+template <int PRIO>
+__device__ __forceinline__ void prio_hi() {
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+}
+template <int PRIO>
+__device__ __forceinline__ void prio_lo() {
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 template <int K0>
 __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Tlane + K0 * HD));
@@ -304,6 +316,7 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+template <int PRIO>
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int B, int S, int H, float c2,
                                                      int order) {
@@ -353,11 +366,13 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       f32x16 s0 = nm16, s1 = nm16;
+      prio_hi<PRIO>();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
         s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
       }
+      prio_lo<PRIO>();
       if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
         // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
         const int d = q - key0 - 4 * hh;
@@ -402,6 +417,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
       l += ls2[0] + ls2[1];
       const bf16* V0 = Vt + vb0;
       const bf16* V1 = Vt + vb1;
+      prio_hi<PRIO>();
       {
         const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
         o0 = mfma(tr_frag_v<0>(V0), p0, o0);
@@ -416,6 +432,7 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
         o0 = mfma(tr_frag_v<48>(V0), p1, o0);
         o1 = mfma(tr_frag_v<48>(V1), p1, o1);
       }
+      prio_lo<PRIO>();
     }
     if (more) {
       bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
@@ -738,6 +755,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__
 // ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
+template <int PRIO>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                          const float* __restrict__ lse, const float* __restrict__ delta,
                                                          bf16* __restrict__ dqkv, int B, int S, int H, float c2,
@@ -825,11 +843,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
             dpacc[4 * g + e] = d4[e];
           }
         }
+        prio_hi<PRIO>();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
           dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
         }
+        prio_lo<PRIO>();
         // The causal mask only touches the diagonal sub-tile (wave-uniform): a
         // separate body keeps its compares and selects out of every other tile
         auto softmax_grad = [&](auto masked) {
@@ -850,6 +870,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
           softmax_grad(std::true_type{});
         else
           softmax_grad(std::false_type{});
+        prio_hi<PRIO>();
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 pb = pack8(sacc, sst);
@@ -859,6 +880,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
           dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
           dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
         }
+        prio_lo<PRIO>();
       }
     }
     sl = sl == 2 ? 0 : sl + 1;
@@ -886,6 +908,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
 // ============================================================================
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
 // ============================================================================
+template <int PRIO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
@@ -963,11 +986,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
       for (int ksub = 0; ksub < 2; ++ksub) {
         f32x16 s = zero16(), dp = zero16();
+        prio_hi<PRIO>();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
           dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
         }
+        prio_lo<PRIO>();
         auto softmax_grad = [&](auto masked) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -983,12 +1008,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           softmax_grad(std::true_type{});
         else
           softmax_grad(std::false_type{});
+        prio_hi<PRIO>();
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 dsb = pack8(s, sst);
           a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
           a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
         }
+        prio_lo<PRIO>();
       }
     }
     if (more) {
@@ -1019,6 +1046,11 @@ static int attn_order() {
   static const int o = env_int("PDO_ATTN_ORDER", 0);
   return o;
 }
+// PDO_ATTN_PRIO bit 0: forward, bit 1: dQ, bit 2: dK/dV raise the wave priority around their MFMA runs
+static int attn_prio() {
+  static const int p = env_int("PDO_ATTN_PRIO", 0);
+  return p;
+}
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
@@ -1032,7 +1064,10 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
     return 0;
   }
   const int grid = B * H * (S / 128);
-  attn_fwd_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  if (attn_prio() & 1)
+    attn_fwd_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  else
+    attn_fwd_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   return 0;
 }
 
@@ -1041,10 +1076,18 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
-                                        attn_order());
-  attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
-                                          attn_order());
+  if (attn_prio() & 2)
+    attn_bwd_dq_d64<1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                             dbias_part, attn_order());
+  else
+    attn_bwd_dq_d64<0><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                             dbias_part, attn_order());
+  if (attn_prio() & 4)
+    attn_bwd_dkdv_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                               dbias_part, attn_order());
+  else
+    attn_bwd_dkdv_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                               dbias_part, attn_order());
   return 0;
 }
 

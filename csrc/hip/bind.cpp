@@ -275,11 +275,18 @@ static void nt_check(const at::Tensor& a, const at::Tensor& b) {
   TORCH_CHECK(gemm_nt_supported(a.size(0), b.size(0), a.size(1)), "gemm_nt: M, N % 256 and K % 64 required");
 }
 
-// c = a·bᵀ (+ bias)
-at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias) {
+// c = a·bᵀ (+ bias); into `out` ([M, N] contiguous bf16) when given
+at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> out) {
   nt_check(a, b);
   const int M = a.size(0), N = b.size(0), K = a.size(1);
-  auto c = at::empty({M, N}, a.options());
+  at::Tensor c;
+  if (out.has_value()) {
+    CHECK_IN((*out)); CHECK_BF16((*out));
+    TORCH_CHECK(out->dim() == 2 && out->size(0) == M && out->size(1) == N, "gemm_nt: out must be [M, N]");
+    c = *out;
+  } else {
+    c = at::empty({M, N}, a.options());
+  }
   const bf16* bptr = nullptr;
   if (bias.has_value()) {
     CHECK_IN((*bias)); CHECK_BF16((*bias)); TORCH_CHECK(bias->numel() == N);
@@ -684,7 +691,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
     if (impl >= 0) pdo::gemm_nt_set_impl(impl);
     return prev;
   }, py::arg("impl") = -1, "select gemm_nt's mainloop (0 = 8-wave ring, 1 = 4-wave); returns the previous");
-  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("out") = py::none());
   m.def("gemm_nt_gelu", &gemm_nt_gelu);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),
         py::arg("db_out") = py::none());

@@ -166,7 +166,6 @@ class GPT2(nn.Module):
                 x, h = ops.add_layer_norm(x, m, nb.ln1_w, nb.ln1_b, cfg.ln_eps, rbias=mb)
             else:
                 x, h = ops.add_layer_norm(x, m, self.lnf_w, self.lnf_b, cfg.ln_eps, rbias=mb)
-        logits = ops.linear(h, self.wte)
         if targets is None:
-            return logits[..., :cfg.vocab_size]
-        return ops.cross_entropy(logits, targets, cfg.vocab_size)
+            return ops.linear(h, self.wte)[..., :cfg.vocab_size]
+        return ops.lm_head_xent(h, self.wte, targets, cfg.vocab_size)

@@ -286,6 +286,37 @@ def test_cross_entropy(cuda):
     assert lh.grad[5].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("N,C,V,chunk", [(1024, 256, 1000, 256), (2048, 512, 50257, 512)])
+def test_lm_head_xent_chunked(cuda, N, C, V, chunk):
+    """Chunked LM head + cross-entropy (ops._LMHeadXentFn) vs fp32 autograd:
+    loss, dh and dW (incl. an ignored target, padded vocabulary rows, and the
+    50304-row half-width last tile at V = 50257)."""
+    ops = _ops()
+    Vp = (V + 127) // 128 * 128
+    g = torch.Generator(device=cuda).manual_seed(9)
+    h = torch.randn(N, C, device=cuda, generator=g).bfloat16()
+    w = (0.05 * torch.randn(Vp, C, device=cuda, generator=g)).bfloat16()
+    w[V:] = 0
+    tgt = torch.randint(0, V, (N,), device=cuda, generator=g)
+    tgt[3] = -100
+    prev = ops._LM_CHUNK[0]
+    ops._LM_CHUNK[0] = chunk
+    try:
+        hh = h.clone().requires_grad_()
+        ww = w.clone().requires_grad_()
+        loss = ops.lm_head_xent(hh, ww, tgt, V)
+        loss.backward(torch.tensor(1.5, device=cuda))
+    finally:
+        ops._LM_CHUNK[0] = prev
+    hf = h.float().requires_grad_()
+    wf = w.float().requires_grad_()
+    lossf = torch.nn.functional.cross_entropy((hf @ wf.t())[:, :V], tgt, ignore_index=-100)
+    (1.5 * lossf).backward()
+    assert abs(loss.item() - lossf.item()) < 2e-3 * max(1.0, lossf.item())
+    assert rel_err(hh.grad, hf.grad) < 3e-2
+    assert rel_err(ww.grad[:V], wf.grad[:V]) < 3e-2
+
+
 def test_embedding(cuda):
     ops = _ops()
     B, S, C, Vp, P = 4, 128, 256, 1024, 256
