@@ -136,27 +136,36 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   const int wm = w >> 1, wn = w & 1;
   const int tiles_n = (N + BN - 1) / BN;  // SCHED & 4: N % 256 = 128 allowed (half-width last tile column)
   const int nwg = (M / BM) * tiles_n;
-  int id = blockIdx.x;
-  {  // bijective XCD remap: each XCD walks a contiguous range of tiles (shared A panels in its L2)
-    const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
-    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  // grouped tile order: consecutive ids walk group_m tile rows, then the next
-  // tile column, so the 32 tiles an XCD runs at once form a group_m × (32 /
-  // group_m) block and share fewer A/B panels in that XCD's 4 MiB L2 (row-major,
-  // group_m = 1: 2 rows × 16 columns on the [65536, 4096] shapes = 18 panels)
-  int tn, tm;
-  {
+  // SCHED & 32: persistent workgroups (grid = one per CU), virtual tile ids
+  // blockIdx.x + k·gridDim.x.  The next tile's first two k-tiles are issued
+  // before this tile's register epilogue, so their HBM latency hides behind the
+  // epilogue's conversions and stores, and the stores drain under the next mainloop.
+  constexpr bool PERS = (SCHED & 32) != 0;
+  static_assert(!PERS || (SCHED & 5) == 5, "persistent tiles: SCHED 1 mainloop with the register row epilogue");
+  auto coords = [&](int v, int& tm_, int& tn_) {
+    int id = v;
+    {  // bijective XCD remap: each XCD walks a contiguous range of tiles (shared A panels in its L2)
+      const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
+      id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+    }
+    // grouped tile order: consecutive ids walk group_m tile rows, then the next
+    // tile column, so the 32 tiles an XCD runs at once form a group_m × (32 /
+    // group_m) block and share fewer A/B panels in that XCD's 4 MiB L2 (row-major,
+    // group_m = 1: 2 rows × 16 columns on the [65536, 4096] shapes = 18 panels)
     const int tiles_m = M / BM, per_group = group_m * tiles_n;
     const int g = id / per_group, first_m = g * group_m;
     const int gsz = min(tiles_m - first_m, group_m), r = id - g * per_group;
-    tm = first_m + r % gsz;
-    tn = r / gsz;
-  }
-  const int m0 = tm * BM, n0 = tn * BN;
+    tm_ = first_m + r % gsz;
+    tn_ = r / gsz;
+  };
+  int vcur = blockIdx.x;
+  int tn, tm;
+  coords(vcur, tm, tn);
+  int m0 = tm * BM, n0 = tn * BN;
   // half-width tile (only N - n0 = 128 columns exist): the B pieces of the upper
   // half re-read the lower half's rows (in bounds), the wn = 1 waves store nothing
-  const bool halfn = (SCHED & 4) && n0 + BN > N;
+  bool halfn = (SCHED & 4) && n0 + BN > N;
+  bool dhalfn = halfn;  // of the tile whose pieces are being issued
 
   // ---- LDS-DMA sources.  Wave w fills 8-row blocks b = w + 4i (i = 0..7) of
   // both operands; lane l → row 8b + (l >> 3), LDS chunk l & 7, global chunk
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       if (p < 8) glds(voffA, reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
       else {
         const int pp = p - 8;
-        const unsigned mul = (SCHED & 4) ? (unsigned)((pp & 3) + (halfn ? 0 : 64) * (pp >> 2)) : (unsigned)pp;
+        const unsigned mul = (SCHED & 4) ? (unsigned)((pp & 3) + (dhalfn ? 0 : 64) * (pp >> 2)) : (unsigned)pp;
         glds(voffB, reinterpret_cast<const bf16*>(sr.b + mul * sr.sb), base + OPB + (unsigned)(4096 * pp));
       }
     }
@@ -268,6 +277,96 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   f32x4 acc[8][8];  // first written by mma0 in tile 0's block 0
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
+  // ---- epilogue ----
+  // The accumulators leave the accumulator file through explicit
+  // v_accvgpr_read ("a" operands): with plain VALU uses here, hipcc's register
+  // classes put part of the 256 accumulators in arch VGPRs for the whole
+  // kernel and shuttled them through v_accvgpr_read/write around every MFMA
+  // (≈3 VALU per MFMA).  hipcc does not pad the asm against the last MFMAs:
+  // 16 wait states first (≥ the 8-pass XDL D → read requirement).
+  auto rd_acc = [](const f32x4& a) {
+    f32x4 v;
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\tv_accvgpr_read_b32 %3, %7"
+                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3])
+                 : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
+    return v;
+  };
+  auto st16 = [](bf16* p, bf16x8 v) {
+    if constexpr (SCHED & 8) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+    else *reinterpret_cast<bf16x8*>(p) = v;
+  };
+  // the row epilogue as a callable: the persistent loop runs it per tile
+  auto row_epilogue = [&]() {
+    if constexpr (SCHED & 4) {
+      // hipcc does not pad the asm against the last MFMAs: 16 wait states first
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+      // ---- row epilogue: acc[i][j][e] = C[m][n], m = wm·128 + 16i + 4(l >> 4) + e,
+      // n = wn·128 + 8(l & 15) + j.  Per (i, e) a lane stores 8 consecutive
+      // columns; the 64 lanes cover 4 rows × 128 columns.  Same per-element math
+      // and roundings as the LDS-staged path below.
+      if (halfn && wn == 1) return;
+      const int g4 = lane >> 4;
+      const int nb = n0 + wn * 128 + 8 * (lane & 15);
+      const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
+      bf16x8 pre[EPI == 3 ? 32 : 1];
+      if constexpr (EPI == 3) {
+#pragma unroll
+        for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
+      }
+      f32x8 bv8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI >= 1) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
+      f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      f32x2 m1 = {-1.f, -1.f};
+      asm volatile("" : "+v"(m1));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        f32x4 a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = rd_acc(acc[i][j]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x8 v = {a[0][e], a[1][e], a[2][e], a[3][e], a[4][e], a[5][e], a[6][e], a[7][e]};
+          const size_t m = mr + 16 * i + e;
+          bf16* crow = C + m * ldc + nb;
+          if constexpr (EPI <= 1) {
+            st16(crow, to_bf16(v + bv8));
+          } else if constexpr (EPI == 2) {
+            const bf16x8 o = to_bf16(v);
+            st16(crow, o);
+            const f32x8 x = to_f32(o) + bv8;
+            f32x8 y;
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+              const f32x2 gg = gelu_sig2(f32x2{x[q], x[q + 1]});
+              y[q] = gg[0];
+              y[q + 1] = gg[1];
+            }
+            st16(Y + m * ldy + nb, to_bf16(y));
+          } else {
+            const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
+            const f32x8 dy = to_f32(to_bf16(v));
+            f32x8 d;
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+              const f32x2 gg = f32x2{dy[q], dy[q + 1]} * gelu_sig_grad2(f32x2{x[q], x[q + 1]}, m1);
+              d[q] = gg[0];
+              d[q + 1] = gg[1];
+            }
+            colp += d;
+            st16(crow, to_bf16(d));
+          }
+        }
+      }
+      if constexpr (EPI == 3) {
+        // partial row 4·wm + (l >> 4) of this M-tile's 8: the rows 16i + 4(l >> 4) + e
+        float* prow = dbias_part + (size_t)(8 * tm + 4 * wm + g4) * N + nb;
+        *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
+        *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
+      }
+    }
+  };
+
+
   if constexpr (SCHED & 1) {
     constexpr bool MIR = (SCHED & 16) != 0;
     static_assert(!MIR || (SCHED & 4), "the mirrored schedule feeds A as SrcA");
@@ -294,21 +393,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         else fb0[q - 8] = rdB(buf_tag, 0, q - 8);
       }
     };
-    // ---- prologue: tiles 0 and 1 in flight, wait for tile 0, its F0 fragments
-    {
+    // ---- prologue: tiles 0 and 1 in flight (then: wait for tile 0, its F0 fragments)
+    auto issue01 = [&]() {
       const Src s0 = srcs(0);
 #pragma unroll
       for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
       const Src s1 = srcs(1);
 #pragma unroll
       for (int p = 0; p < 16; ++p) dma(s1, B1{}, p);
-    }
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) rdF0(B0{}, q);
+    };
 
     // slot s = MFMA index in the tile (128); run r = s >> 3 keeps B fragment
     // (r & 7) stationary over A fragments 0-7, k half s >> 6.
@@ -378,15 +471,48 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    // nk is even and ≥ 4 (host contract)
-    tile3(0, B0{}, T_{}, T_{}, T_{});
-    tile3(1, B1{}, F_{}, T_{}, T_{});
-    for (int t = 2; t < nk - 2; t += 2) {
-      tile3(t, B0{}, F_{}, T_{}, T_{});
-      tile3(t + 1, B1{}, F_{}, T_{}, T_{});
+    issue01();
+    for (;;) {
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (tile 1 may fly)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rdF0(B0{}, q);
+      // nk is even and ≥ 4 (host contract)
+      tile3(0, B0{}, T_{}, T_{}, T_{});
+      tile3(1, B1{}, F_{}, T_{}, T_{});
+      for (int t = 2; t < nk - 2; t += 2) {
+        tile3(t, B0{}, F_{}, T_{}, T_{});
+        tile3(t + 1, B1{}, F_{}, T_{}, T_{});
+      }
+      tile3(nk - 2, B0{}, F_{}, T_{}, F_{});
+      tile3(nk - 1, B1{}, F_{}, F_{}, F_{});
+      if constexpr (PERS) {
+        const int vn = vcur + (int)gridDim.x;
+        if (vn >= nwg) break;
+        int ntm, ntn;
+        coords(vn, ntm, ntn);
+        // every wave's last LDS reads of this tile precede any wave's refill
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        baseA = A + ((size_t)ntm * BM + 8 * w) * lda;
+        baseB = B + ((size_t)ntn * BN + 64 * (w & 1) + (w >> 1)) * ldb;
+        dhalfn = ntn * BN + BN > N;
+        issue01();
+        row_epilogue();  // of this tile (m0, n0, tm, halfn)
+        vcur = vn;
+        tm = ntm;
+        tn = ntn;
+        m0 = tm * BM;
+        n0 = tn * BN;
+        halfn = dhalfn;
+      } else {
+        break;
+      }
     }
-    tile3(nk - 2, B0{}, F_{}, T_{}, F_{});
-    tile3(nk - 1, B1{}, F_{}, F_{}, F_{});
   } else {
   // ---- prologue: tile 0 → buffer 0, F0 of tile 0
   {
@@ -495,90 +621,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   }  // SCHED
 
   // ---- epilogue ----
-  // The accumulators leave the accumulator file through explicit
-  // v_accvgpr_read ("a" operands): with plain VALU uses here, hipcc's register
-  // classes put part of the 256 accumulators in arch VGPRs for the whole
-  // kernel and shuttled them through v_accvgpr_read/write around every MFMA
-  // (≈3 VALU per MFMA).  hipcc does not pad the asm against the last MFMAs:
-  // 16 wait states first (≥ the 8-pass XDL D → read requirement).
-  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-  auto rd_acc = [](const f32x4& a) {
-    f32x4 v;
-    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\tv_accvgpr_read_b32 %3, %7"
-                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3])
-                 : "a"(a[0]), "a"(a[1]), "a"(a[2]), "a"(a[3]));
-    return v;
-  };
-  auto st16 = [](bf16* p, bf16x8 v) {
-    if constexpr (SCHED & 8) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
-    else *reinterpret_cast<bf16x8*>(p) = v;
-  };
   if constexpr (SCHED & 4) {
-    // ---- row epilogue: acc[i][j][e] = C[m][n], m = wm·128 + 16i + 4(l >> 4) + e,
-    // n = wn·128 + 8(l & 15) + j.  Per (i, e) a lane stores 8 consecutive
-    // columns; the 64 lanes cover 4 rows × 128 columns.  Same per-element math
-    // and roundings as the LDS-staged path below.
-    if (halfn && wn == 1) return;
-    const int g4 = lane >> 4;
-    const int nb = n0 + wn * 128 + 8 * (lane & 15);
-    const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
-    bf16x8 pre[EPI == 3 ? 32 : 1];
-    if constexpr (EPI == 3) {
-#pragma unroll
-      for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
-    }
-    f32x8 bv8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI >= 1) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
-    f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    f32x2 m1 = {-1.f, -1.f};
-    asm volatile("" : "+v"(m1));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      f32x4 a[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = rd_acc(acc[i][j]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const f32x8 v = {a[0][e], a[1][e], a[2][e], a[3][e], a[4][e], a[5][e], a[6][e], a[7][e]};
-        const size_t m = mr + 16 * i + e;
-        bf16* crow = C + m * ldc + nb;
-        if constexpr (EPI <= 1) {
-          st16(crow, to_bf16(v + bv8));
-        } else if constexpr (EPI == 2) {
-          const bf16x8 o = to_bf16(v);
-          st16(crow, o);
-          const f32x8 x = to_f32(o) + bv8;
-          f32x8 y;
-#pragma unroll
-          for (int q = 0; q < 8; q += 2) {
-            const f32x2 gg = gelu_sig2(f32x2{x[q], x[q + 1]});
-            y[q] = gg[0];
-            y[q + 1] = gg[1];
-          }
-          st16(Y + m * ldy + nb, to_bf16(y));
-        } else {
-          const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
-          const f32x8 dy = to_f32(to_bf16(v));
-          f32x8 d;
-#pragma unroll
-          for (int q = 0; q < 8; q += 2) {
-            const f32x2 gg = f32x2{dy[q], dy[q + 1]} * gelu_sig_grad2(f32x2{x[q], x[q + 1]}, m1);
-            d[q] = gg[0];
-            d[q + 1] = gg[1];
-          }
-          colp += d;
-          st16(crow, to_bf16(d));
-        }
-      }
-    }
-    if constexpr (EPI == 3) {
-      // partial row 4·wm + (l >> 4) of this M-tile's 8: the rows 16i + 4(l >> 4) + e
-      float* prow = dbias_part + (size_t)(8 * tm + 4 * wm + g4) * N + nb;
-      *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
-      *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
-    }
+    row_epilogue();
     return;
   }
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
   if constexpr (SCHED & 2) {
     // ---- register epilogue: no LDS round trip, no barrier.  Per 16-row block
     // i and 4-block column group h, the 4 lanes {r, r+16, r+32, r+48} hold a
@@ -769,7 +816,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 }  // namespace
 
 // the variants with row-major accumulators (SCHED & 4) take N % 256 = 128
-int gemm_nt4_half_n(int variant) { return variant == 8 || variant == 9 || variant == 11; }
+int gemm_nt4_half_n(int variant) { return variant == 8 || variant == 9 || variant == 11 || variant == 12 || variant == 13; }
+
+// persistent variants: one workgroup per CU (a multiple of 8: the XCD mapping)
+static int persistent_grid(long long tiles) {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n >= 8 ? n / 8 * 8 : 8;
+  }();
+  return (int)(tiles < ncu ? tiles : ncu);
+}
 
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
              const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant) {
@@ -788,11 +846,12 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   auto launch = [&](auto gpg, auto bar, auto bufld, auto sched) {
     constexpr int G = decltype(gpg)::value, R = decltype(bar)::value, L = decltype(bufld)::value;
     constexpr int S = decltype(sched)::value;
+    const int g = (S & 32) ? persistent_grid(grid) : (int)grid;
     switch (epi) {
-      case 0: gemm_nt4_kernel<0, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
-      case 1: gemm_nt4_kernel<1, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
-      case 2: gemm_nt4_kernel<2, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
-      case 3: gemm_nt4_kernel<3, G, R, L, S><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 0: gemm_nt4_kernel<0, G, R, L, S><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 1: gemm_nt4_kernel<1, G, R, L, S><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 2: gemm_nt4_kernel<2, G, R, L, S><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 3: gemm_nt4_kernel<3, G, R, L, S><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       default: return -4;
     }
     return 0;
@@ -825,6 +884,8 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
     case 9: return launch(I1{}, I11{}, I2{}, I13{});  // the same with non-temporal stores
     case 10: return launch(I1{}, I11{}, I2{}, I9{});  // LDS-staged epilogue, non-temporal stores
     case 11: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 29>{});  // impl 10 + mirrored schedule
+    case 12: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 61>{});  // variant 11, persistent
+    case 13: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 45>{});  // variant 9, persistent
     default: return launch(I1{}, I11{}, I2{}, I1{});
   }
   return 0;

@@ -727,8 +727,8 @@ class _LMHeadXentFn(torch.autograd.Function):
             hc, tc = h2[c0:c0 + chunk], t[c0:c0 + chunk]
             lg = logits[:hc.shape[0]]
             m.gemm_nt(hc, w, None, lg)
-            row_loss, lse, _ = m.xent_fwd(lg, tc, vocab)
-            loss_sum += row_loss.sum()
+            _, lse, st = m.xent_fwd(lg, tc, vocab)  # st = (chunk mean loss, chunk valid count)
+            loss_sum += st[0] * st[1]
             dl = m.xent_bwd(lg, tc, lse, ones, stats, vocab, True)  # (softmax − onehot) / count, in place
             m.gemm_nt(dl, wt, None, dh[c0:c0 + chunk])
             if not m.gemm_dw(dl, hc, dw, c0 > 0):
