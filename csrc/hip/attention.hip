@@ -756,10 +756,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
 template <int PRIO>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                         const float* __restrict__ lse, const float* __restrict__ delta,
-                                                         bf16* __restrict__ dqkv, int B, int S, int H, float c2,
-                                                         float scale, float* __restrict__ dbias_part, int order) {
+__device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                          bf16* __restrict__ dqkv, int B, int S, int H, float c2,
+                                          float scale, float* __restrict__ dbias_part, int order) {
   // ring of 3 slots × {Q [64][64] bf16, dO [64][64] bf16, lse·log2e [64] f32, delta [64] f32}
   constexpr int SLOT = 2 * TROWS * HD + 2 * TROWS * 2;  // bf16 units (16896 B)
   __shared__ __attribute__((aligned(16))) bf16 smem[3 * SLOT];
@@ -904,6 +904,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(const bf16* __restrict_
     colsum_finish<2>(red, out, tid);
   }
 }
+
+#define PDO_DKDV_ARGS                                                                                             \
+  const bf16 *__restrict__ qkv, const bf16 *__restrict__ dout, const float *__restrict__ lse,                        \
+      const float *__restrict__ delta, bf16 *__restrict__ dqkv, int B, int S, int H, float c2, float scale,          \
+      float *__restrict__ dbias_part, int order
+template <int PRIO>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(PDO_DKDV_ARGS) {
+  dkdv_body<PRIO>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+}
+// the same body capped at 168 VGPRs: 3 waves per SIMD instead of 2 (the LDS
+// ring, 49.5 KiB per workgroup, allows 3 workgroups per CU)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dkdv3_d64(PDO_DKDV_ARGS) {
+  dkdv_body<0>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+}
+#undef PDO_DKDV_ARGS
 
 // ============================================================================
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
@@ -1082,7 +1097,11 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   else
     attn_bwd_dq_d64<0><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                              dbias_part, attn_order());
-  if (attn_prio() & 4)
+  static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 0);
+  if (dkdv3)
+    attn_bwd_dkdv3_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
+                                             attn_order());
+  else if (attn_prio() & 4)
     attn_bwd_dkdv_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                                dbias_part, attn_order());
   else

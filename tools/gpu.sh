@@ -25,6 +25,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$NAME; mkdir -p "$O"
 export TMPDIR=/tmp
 cd "$R" || exit 1
 PMC_PASS=0
+PROF_PASS=0
 say() { echo "[gpu.sh $(date +%H:%M:%S)] $*"; }
 
 run_step() {
@@ -53,15 +54,17 @@ run_step() {
         || { tail -40 "$O/probe_${s%.py}.log"; return 1; }
       cat "$O/probe_${s%.py}.log" ;;
     prof|step)
+      PROF_PASS=$((PROF_PASS + 1))
       local s=${A[0]:-train_probe.py} rest=("${A[@]:1}")
       [[ $kind == step ]] && { s=train_probe.py; rest=(--dist --steps 7 --warmup 2); }
-      local d=$O/prof_${s%.py}
+      local tag=prof${PROF_PASS}_${s%.py}   # numbered: several passes in one call keep their tables
+      local d=$O/$tag
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 "$R/tools/$s" "${rest[@]}" ) \
-        > "$O/prof_${s%.py}.log" 2>&1 || { tail -30 "$O/prof_${s%.py}.log"; return 1; }
+        > "$O/$tag.log" 2>&1 || { tail -30 "$O/$tag.log"; return 1; }
       local db; db=$(find "$d" -name '*.db' | head -1)
       local steps=1; [[ $kind == step ]] && steps=9  # 2 warmup + 7 timed steps are all traced
-      python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/prof_${s%.py}.md" && rm -rf "$d"
-      tail -5 "$O/prof_${s%.py}.log"; head -45 "$O/prof_${s%.py}.md" ;;
+      python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/$tag.md" && rm -rf "$d"
+      tail -5 "$O/$tag.log"; head -45 "$O/$tag.md" ;;
     pmc)
       PMC_PASS=$((PMC_PASS + 1))
       local ctr=${A[0]//+/ } s=${A[1]} p=$O/pmc${PMC_PASS}_${A[1]%.py}
