@@ -316,7 +316,10 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int PRIO>
+// SPLIT: the 64-key tile's softmax runs per 32-key half, each with its own
+// defer-max check, so the exp / sum / pack of half 0 and its P·V depend only on
+// half 0's score MFMAs and can run while half 1's are still in the matrix pipe
+template <int PRIO, int SPLIT = 0>
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int B, int S, int H, float c2,
                                                      int order) {
@@ -367,72 +370,135 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
     if (key0 <= wave_qmax) {
       f32x16 s0 = nm16, s1 = nm16;
       prio_hi<PRIO>();
+      if constexpr (SPLIT) {  // half 0's chain first: its softmax can start under half 1's
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
-        s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
-      }
-      prio_lo<PRIO>();
-      if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
-        // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
-        const int d = q - key0 - 4 * hh;
+        for (int ks = 0; ks < 4; ++ks) s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int c = (r & 3) + 8 * (r >> 2);
-          s0[r] = c > d ? -INFINITY : s0[r];
-          s1[r] = c + 32 > d ? -INFINITY : s1[r];
+        for (int ks = 0; ks < 4; ++ks) s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
+          s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
         }
       }
-      // tile max of s' (relative to m): only a growth past 2^8 rescales
-      // (defer-max, cdna_hip_programming.md T13); the first tile sets m
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-      tmax = xhalf_max(tmax);
-      if (t == 0) {  // every query has key 0 unmasked here: tmax is finite
-        m = tmax;
-        s0 -= tmax;
-        s1 -= tmax;
-        nm16 = bcast16(-m);
-      } else if (__any(tmax > 8.f)) {
-        const float d = tmax > 8.f ? tmax : 0.f;
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-        m += d;
-        l *= alpha;
-        o0 *= alpha;
-        o1 *= alpha;
-        s0 -= d;
-        s1 -= d;
-        nm16 = bcast16(-m);
-      }
-      f32x2 ls2 = {0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
-        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
-        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
-      }
-      l += ls2[0] + ls2[1];
-      const bf16* V0 = Vt + vb0;
-      const bf16* V1 = Vt + vb1;
-      prio_hi<PRIO>();
-      {
-        const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
-        o0 = mfma(tr_frag_v<0>(V0), p0, o0);
-        o1 = mfma(tr_frag_v<0>(V1), p0, o1);
-        o0 = mfma(tr_frag_v<32>(V0), p1, o0);
-        o1 = mfma(tr_frag_v<32>(V1), p1, o1);
-      }
-      {
-        const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
-        o0 = mfma(tr_frag_v<16>(V0), p0, o0);
-        o1 = mfma(tr_frag_v<16>(V1), p0, o1);
-        o0 = mfma(tr_frag_v<48>(V0), p1, o0);
-        o1 = mfma(tr_frag_v<48>(V1), p1, o1);
-      }
       prio_lo<PRIO>();
+      if constexpr (SPLIT) {
+        const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;  // wave-uniform
+        const int dq = q - key0 - 4 * hh;
+        const bf16* V0 = Vt + vb0;
+        const bf16* V1 = Vt + vb1;
+        // one 32-key half h: mask, defer-max check (rescales o, l and the other
+        // half's pending scores), exp, row sum, P·V on its two 16-key slices
+        auto half = [&](f32x16& sh, f32x16& so, auto hc) {
+          constexpr int H = decltype(hc)::value;
+          if (diag) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int c = (r & 3) + 8 * (r >> 2) + 32 * H;
+              sh[r] = c > dq ? -INFINITY : sh[r];
+            }
+          }
+          float tmax = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 16; r += 4) tmax = fmaxf(fmaxf(tmax, fmaxf(sh[r], sh[r + 1])), fmaxf(sh[r + 2], sh[r + 3]));
+          tmax = xhalf_max(tmax);
+          if (H == 0 && t == 0) {  // every query has key 0 unmasked here: tmax is finite
+            m = tmax;
+            sh -= tmax;
+            so -= tmax;
+            nm16 = bcast16(-m);
+          } else if (__any(tmax > 8.f)) {
+            const float d = tmax > 8.f ? tmax : 0.f;
+            const float alpha = __builtin_amdgcn_exp2f(-d);
+            m += d;
+            l *= alpha;
+            o0 *= alpha;
+            o1 *= alpha;
+            sh -= d;
+            if constexpr (H == 0) so -= d;
+            nm16 = bcast16(-m);
+          }
+          f32x2 ls2 = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            sh[r] = __builtin_amdgcn_exp2f(sh[r]);
+            sh[r + 1] = __builtin_amdgcn_exp2f(sh[r + 1]);
+            ls2 += f32x2{sh[r], sh[r + 1]};
+          }
+          l += ls2[0] + ls2[1];
+          prio_hi<PRIO>();
+          const bf16x8 pa = pack8(sh, 0), pb = pack8(sh, 1);
+          o0 = mfma(tr_frag_v<32 * H>(V0), pa, o0);
+          o1 = mfma(tr_frag_v<32 * H>(V1), pa, o1);
+          o0 = mfma(tr_frag_v<32 * H + 16>(V0), pb, o0);
+          o1 = mfma(tr_frag_v<32 * H + 16>(V1), pb, o1);
+          prio_lo<PRIO>();
+        };
+        half(s0, s1, std::integral_constant<int, 0>{});
+        half(s1, s0, std::integral_constant<int, 1>{});
+      } else {
+        if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
+          // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
+          const int d = q - key0 - 4 * hh;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = (r & 3) + 8 * (r >> 2);
+            s0[r] = c > d ? -INFINITY : s0[r];
+            s1[r] = c + 32 > d ? -INFINITY : s1[r];
+          }
+        }
+        // tile max of s' (relative to m): only a growth past 2^8 rescales
+        // (defer-max, cdna_hip_programming.md T13); the first tile sets m
+        float tmax = -INFINITY;
+  #pragma unroll
+        for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+        tmax = xhalf_max(tmax);
+        if (t == 0) {  // every query has key 0 unmasked here: tmax is finite
+          m = tmax;
+          s0 -= tmax;
+          s1 -= tmax;
+          nm16 = bcast16(-m);
+        } else if (__any(tmax > 8.f)) {
+          const float d = tmax > 8.f ? tmax : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          m += d;
+          l *= alpha;
+          o0 *= alpha;
+          o1 *= alpha;
+          s0 -= d;
+          s1 -= d;
+          nm16 = bcast16(-m);
+        }
+        f32x2 ls2 = {0.f, 0.f};
+  #pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+          s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+          s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+          ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+        }
+        l += ls2[0] + ls2[1];
+        const bf16* V0 = Vt + vb0;
+        const bf16* V1 = Vt + vb1;
+        prio_hi<PRIO>();
+        {
+          const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
+          o0 = mfma(tr_frag_v<0>(V0), p0, o0);
+          o1 = mfma(tr_frag_v<0>(V1), p0, o1);
+          o0 = mfma(tr_frag_v<32>(V0), p1, o0);
+          o1 = mfma(tr_frag_v<32>(V1), p1, o1);
+        }
+        {
+          const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
+          o0 = mfma(tr_frag_v<16>(V0), p0, o0);
+          o1 = mfma(tr_frag_v<16>(V1), p0, o1);
+          o0 = mfma(tr_frag_v<48>(V0), p1, o0);
+          o1 = mfma(tr_frag_v<48>(V1), p1, o1);
+        }
+        prio_lo<PRIO>();
+      }
     }
     if (more) {
       bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
@@ -1079,7 +1145,9 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
     return 0;
   }
   const int grid = B * H * (S / 128);
-  if (attn_prio() & 1)
+  if (variant == 4)
+    attn_fwd_d64<0, 1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  else if (attn_prio() & 1)
     attn_fwd_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   else
     attn_fwd_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
@@ -1097,7 +1165,8 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   else
     attn_bwd_dq_d64<0><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                              dbias_part, attn_order());
-  static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 0);
+  // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step
+  static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 1);
   if (dkdv3)
     attn_bwd_dkdv3_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
                                              attn_order());

@@ -398,12 +398,16 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                 flush_pending(sl.dev)
 
     def status_table():
+        # a slot still warming reports its GPU's last READY record (footprint,
+        # warm time), so a status read right after a handoff is not empty
         return {"pid": os.getpid(), "served": served,
-                "slots": {d: {"pid": sl.pid, "ready": sl.ready, "t_spawn": sl.t_spawn, **sl.info}
+                "slots": {d: {"pid": sl.pid, "ready": sl.ready, "t_spawn": sl.t_spawn,
+                              **(sl.info or last_info.get(d, {}))}
                           for d, sl in slots.items()},
                 "respawn": SLOT_RESPAWN, "park_s": SLOT_PARK_S,
                 "devices": list(warm_devices or []), "failed": slot_fails}
 
+    last_info = {}
     for dev in warm_devices or []:
         spawn_slot(dev)
     while not stop:
@@ -451,6 +455,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                     except ValueError:
                         sl.info = {}
                     sl.info["warm_s"] = round(time.time() - sl.t_spawn, 3)
+                    last_info[sl.dev] = dict(sl.info)
                     slot_fails.pop(sl.dev, None)
                     log(f"slot gpu {sl.dev} warm in {sl.info['warm_s']}s ({sl.info})")
                     flush_pending(sl.dev)
