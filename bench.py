@@ -314,7 +314,7 @@ def orchestrate(a):
             if L.zygote and gpus:
                 # the warm slots' resident footprint (HIP context + RCCL code), per GPU
                 st = L.cl.zygote_status()
-                out["warm_slots"] = {node: {d: {k: sl.get(k) for k in ("mem_mb", "mem_mb_before_rccl", "warm_s")}
+                out["warm_slots"] = {node: {d: {k: sl.get(k) for k in ("mem_mb", "mem_mb_before_rccl", "warm_s", "n", "n_ready")}
                                             for d, sl in (z or {}).get("slots", {}).items()}
                                      for node, z in st.items()}
             if a.b2b_trials and not a.ready_only:

@@ -186,7 +186,8 @@ class LocalCluster:
         deadline = time.time() + timeout
         while time.time() < deadline:
             st = self.zygote_status()
-            if st and all(z is not None and all(s["ready"] for s in z["slots"].values())
+            if st and all(z is not None and all(s["ready"] and s.get("n_ready", 1) >= s.get("n", 1)
+                                                for s in z["slots"].values())
                           and (len(z["slots"]) + len(z.get("failed") or {})) >= len(z["devices"])
                           for z in st.values()):
                 return True

@@ -89,6 +89,12 @@ SLOT_WARM_MAX_S = float(os.environ.get("PDO_SLOT_WARM_MAX_S", "60"))
 # "mem_mb" in the status table), "exit" = once that job's rank exits (no
 # second context on the GPU while the job runs)
 SLOT_RESPAWN = os.environ.get("PDO_SLOT_RESPAWN", "handoff")
+# warm slots kept per GPU (PDO_SLOTS_PER_GPU).  With one, a job that starts
+# right after another on the same GPU finds its slot still re-warming (HIP +
+# RCCL init, ≈ 1 s: bench.py 'ready_b2b'); a second slot serves it warm.  Each
+# slot holds a HIP context and a 1-rank communicator on the GPU ('mem_mb' in
+# the status table, well under 1 GB of the 288 GB).
+SLOTS_PER_GPU = max(1, int(os.environ.get("PDO_SLOTS_PER_GPU", "2")))
 
 
 def runtime_key(env: Dict[str, str]) -> tuple:
@@ -291,7 +297,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
     signal.signal(signal.SIGTERM, lambda *a: stop.append(1))
     last_activity = time.time()
     key = runtime_key(dict(os.environ))
-    slots: Dict[str, _Slot] = {}       # device -> its (single) warm slot
+    slots: Dict[str, List[_Slot]] = {}  # device -> its warm slots (≤ SLOTS_PER_GPU)
     slot_pids: Dict[int, _Slot] = {}
     slot_fails: Dict[str, int] = {}
     pending: Dict[str, list] = {}      # device -> [(conn, req, fds, t_park)] waiting for a warming slot
@@ -301,8 +307,11 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
     def log(msg):
         print(f"[pdo-zygote] {msg}", flush=True)
 
+    def ready_slot(dev):
+        return next((s for s in slots.get(dev, ()) if s.ready), None)
+
     def spawn_slot(dev):
-        if stop or slot_fails.get(dev, 0) >= SLOT_RETRIES or dev in slots:
+        if stop or slot_fails.get(dev, 0) >= SLOT_RETRIES or len(slots.get(dev, ())) >= SLOTS_PER_GPU:
             return
         a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
         pid = os.fork()
@@ -311,12 +320,16 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
             _slot_main(dev, b, ls)
         b.close()
         sl = _Slot(dev, pid, a)
-        slots[dev] = sl
+        slots.setdefault(dev, []).append(sl)
         slot_pids[pid] = sl
         sel.register(a, selectors.EVENT_READ, ("slot", sl))
 
     def drop_slot(sl):
-        slots.pop(sl.dev, None)
+        lst = slots.get(sl.dev)
+        if lst and sl in lst:
+            lst.remove(sl)
+            if not lst:
+                slots.pop(sl.dev)
         try:
             sel.unregister(sl.sock)
         except (KeyError, ValueError):
@@ -362,8 +375,8 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
 
     def flush_pending(dev):
         for conn, req, fds, _ in pending.pop(dev, []):
-            sl = slots.get(dev)
-            if sl is not None and sl.ready:
+            sl = ready_slot(dev)
+            if sl is not None:
                 handoff(sl, conn, req, fds)
             else:
                 cold(conn, req, fds)
@@ -385,7 +398,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                 pending[dev] = keep
             else:
                 pending.pop(dev)
-        for sl in list(slots.values()):
+        for sl in [x for lst in slots.values() for x in lst]:
             if not sl.ready and now - sl.t_spawn > SLOT_WARM_MAX_S:
                 served["warm_timeouts"] += 1
                 log(f"slot gpu {sl.dev} pid {sl.pid} still warming after {now - sl.t_spawn:.0f}s; killed")
@@ -400,16 +413,20 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
     def status_table():
         # a slot still warming reports its GPU's last READY record (footprint,
         # warm time), so a status read right after a handoff is not empty
+        def one(d, lst):  # a ready slot first; n / n_ready count the pool
+            sl = next((x for x in lst if x.ready), lst[0])
+            return {"pid": sl.pid, "ready": sl.ready, "t_spawn": max(x.t_spawn for x in lst), "n": len(lst),
+                    "n_ready": sum(x.ready for x in lst), **(sl.info or last_info.get(d, {}))}
         return {"pid": os.getpid(), "served": served,
-                "slots": {d: {"pid": sl.pid, "ready": sl.ready, "t_spawn": sl.t_spawn,
-                              **(sl.info or last_info.get(d, {}))}
-                          for d, sl in slots.items()},
+                "slots": {d: one(d, lst) for d, lst in slots.items() if lst},
+                "slots_per_gpu": SLOTS_PER_GPU,
                 "respawn": SLOT_RESPAWN, "park_s": SLOT_PARK_S,
                 "devices": list(warm_devices or []), "failed": slot_fails}
 
     last_info = {}
     for dev in warm_devices or []:
-        spawn_slot(dev)
+        for _ in range(SLOTS_PER_GPU):
+            spawn_slot(dev)
     while not stop:
         for skey, _ in sel.select(timeout=0.01):
             if skey.data == "listen":
@@ -433,10 +450,10 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                     continue
                 last_activity = time.time()
                 dev = warm_device_of(req, key) if warm_devices else None
-                sl = slots.get(dev) if dev is not None else None
-                if sl is not None and sl.ready:
+                sl = ready_slot(dev) if dev is not None else None
+                if sl is not None:
                     handoff(sl, conn, req, fds)
-                elif sl is not None:  # warming: wait for it, but at most SLOT_PARK_S (expire)
+                elif dev is not None and slots.get(dev):  # warming: wait for one, at most SLOT_PARK_S (expire)
                     pending.setdefault(dev, []).append((conn, req, fds, time.time()))
                 else:
                     cold(conn, req, fds)
@@ -489,7 +506,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                 break
             sl = slot_pids.pop(pid, None)
             if sl is not None:  # an unused slot exited
-                if slots.get(sl.dev) is sl:
+                if sl in slots.get(sl.dev, ()):
                     slot_fails[sl.dev] = slot_fails.get(sl.dev, 0) + 1
                     drop_slot(sl)
                     flush_pending(sl.dev)
@@ -519,7 +536,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
             os.killpg(pid, signal.SIGTERM)
         except ProcessLookupError:
             pass
-    for sl in list(slots.values()):  # idle slots exit on EOF
+    for sl in [x for lst in slots.values() for x in lst]:  # idle slots exit on EOF
         drop_slot(sl)
     for pid in list(slot_pids):
         try:

@@ -109,7 +109,7 @@ def test_slot_stuck_warming_is_killed_and_counted(tmp_path):
 
 @pytest.mark.parametrize("policy", ["handoff", "exit"])
 def test_slot_respawn_policy(tmp_path, policy):
-    p, path, env = _start(tmp_path, PDO_SLOT_TEST="cpu", PDO_SLOT_RESPAWN=policy)
+    p, path, env = _start(tmp_path, PDO_SLOT_TEST="cpu", PDO_SLOT_RESPAWN=policy, PDO_SLOTS_PER_GPU="1")
     try:
         t_end = time.time() + 30
         while time.time() < t_end and not (zygote.query_status(path)["slots"].get("0") or {}).get("ready"):
@@ -134,5 +134,33 @@ def test_slot_respawn_policy(tmp_path, policy):
         assert "0" in st["slots"]  # respawned either way once the rank exited
         if policy == "exit":
             assert st["slots"]["0"]["t_spawn"] > t_exit - 1.0
+    finally:
+        _stop(p)
+
+
+def test_two_slots_serve_back_to_back_jobs_warm(tmp_path):
+    """PDO_SLOTS_PER_GPU=2: a job arriving while the first job's replacement
+    slot is still warming takes the second warm slot instead of parking."""
+    p, path, env = _start(tmp_path, PDO_SLOT_TEST="cpu", PDO_SLOTS_PER_GPU="2")
+    try:
+        t_end = time.time() + 30
+        while time.time() < t_end:
+            sl = zygote.query_status(path)["slots"].get("0") or {}
+            if sl.get("n_ready") == 2:
+                break
+            time.sleep(0.05)
+        st = zygote.query_status(path)
+        assert st["slots_per_gpu"] == 2 and st["slots"]["0"]["n_ready"] == 2, st
+        socks = []
+        for _ in range(2):  # back to back: no wait for the replacement
+            s = _request(path, env, ["--workload", "noop", "--exit-after-ready"], PDO_RANK_HOLD_S="1.0")
+            assert _readline(s).startswith("PID ")
+            socks.append(s)
+        st = zygote.query_status(path)
+        assert st["served"]["warm"] == 2 and st["served"]["cold"] == 0, st
+        assert st["served"]["park_timeouts"] == 0
+        for s in socks:
+            assert _readline(s).startswith("EXIT ")
+            s.close()
     finally:
         _stop(p)
