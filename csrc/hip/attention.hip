@@ -989,13 +989,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // ============================================================================
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
 // ============================================================================
-template <int PRIO>
+// RING: K / V tiles by LDS-DMA two tiles ahead through 3 slots (the dK/dV
+// kernel's ring) instead of register staging one tile ahead
+template <int PRIO, int RING = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
                                                        int H, float c2, float scale, float* __restrict__ dbias_part,
                                                        int order) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
+  __shared__ __attribute__((aligned(16))) bf16 smem[(RING ? 3 : 2) * 2 * TROWS * HD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   int bh, r_;
@@ -1048,16 +1050,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
   Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
-  stage_store(sk, smem, tid);
-  stage_store(sv, smem + TROWS * HD, tid);
-  __syncthreads();
+  constexpr int SLOT = 2 * TROWS * HD;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned vk0 = dma_voff(lane, rs, 0), vk1 = dma_voff(lane, rs, 1);
+  auto issue = [&](int t, int slot) {  // this wave's 4 pieces (2 K, 2 V) of tile t
+    const unsigned base = lds0 + (unsigned)(slot * SLOT * 2);
+    dma_tile(kbase, rs, t * TROWS, wu, vk0, vk1, base);
+    dma_tile(vbase, rs, t * TROWS, wu, vk0, vk1, base + TROWS * HD * 2);
+  };
+  if constexpr (RING) {
+    issue(0, 0);
+    if (ntiles > 1) issue(1, 1);
+  } else {
+    stage_load(sk, kbase, rs, 0, tid);
+    stage_load(sv, vbase, rs, 0, tid);
+    stage_store(sk, smem, tid);
+    stage_store(sv, smem + TROWS * HD, tid);
+    __syncthreads();
+  }
+  int sl = 0;
   for (int t = 0; t < ntiles; ++t) {
-    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
-    const bf16* Vt = Kt + TROWS * HD;
     const bool more = t + 1 < ntiles;
-    if (more) {
+    if constexpr (RING) {
+      if (more)
+        vm_wait<4>();  // this wave's pieces of tile t have landed (t + 1's 4 may still fly)
+      else
+        vm_wait<0>();
+      __syncthreads();  // ... and every other wave's; slot (sl + 2) % 3 is free again
+      if (t + 2 < ntiles) issue(t + 2, sl == 0 ? 2 : sl - 1);
+    }
+    const bf16* Kt = RING ? smem + sl * SLOT : smem + (t & 1) * 2 * TROWS * HD;
+    const bf16* Vt = Kt + TROWS * HD;
+    if (!RING && more) {
       stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
       stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
     }
@@ -1099,13 +1124,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         prio_lo<PRIO>();
       }
     }
-    if (more) {
-      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-      stage_store(sk, Kn, tid);
-      stage_store(sv, Kn + TROWS * HD, tid);
+    if constexpr (RING) {
+      sl = sl == 2 ? 0 : sl + 1;
+    } else {
+      if (more) {
+        bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+        stage_store(sk, Kn, tid);
+        stage_store(sv, Kn + TROWS * HD, tid);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
+  if constexpr (RING) __syncthreads();  // the epilogue's column sums reuse the ring
   bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
   store_acc_rows(qrow, a0, 0, hh, scale);
   store_acc_rows(qrow, a1, 32, hh, scale);
@@ -1159,7 +1189,11 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  if (attn_prio() & 2)
+  static const int dq3 = env_int("PDO_ATTN_DQ3", 0);
+  if (dq3)
+    attn_bwd_dq_d64<0, 1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                                dbias_part, attn_order());
+  else if (attn_prio() & 2)
     attn_bwd_dq_d64<1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                              dbias_part, attn_order());
   else
