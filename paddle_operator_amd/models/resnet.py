@@ -33,12 +33,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         # BN + ReLU (+ residual add) fused into one HIP pass each (ops.bn_act)
+        # 1×1 stride-1 convolutions as token-major GEMMs (ops.conv1x1: gemm_nt4 /
+        # gemm_dw4 / MIOpen per product, whichever measured faster at the shape)
         idt = x
-        out = ops.bn_act(self.bn1, self.conv1(x))
+        out = ops.bn_act(self.bn1, ops.conv1x1(self.conv1, x))
         out = ops.bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
-            idt = ops.bn_act(self.downsample[1], self.downsample[0](x), relu=False)
-        return ops.bn_act(self.bn3, self.conv3(out), relu=True, residual=idt)
+            idt = ops.bn_act(self.downsample[1], ops.conv1x1(self.downsample[0], x), relu=False)
+        return ops.bn_act(self.bn3, ops.conv1x1(self.conv3, out), relu=True, residual=idt)
 
 
 class ResNet(nn.Module):

@@ -861,6 +861,81 @@ def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
     return F.relu(y) if relu else y
 
 
+class _Conv1x1Fn(torch.autograd.Function):
+    """1×1 stride-1 convolution on a channels_last bf16 activation as token-major
+    GEMMs over its [N·H·W, C] view — per product, the kernel that measured
+    faster at ResNet-50's shapes (tools/conv1x1_probe.py, profiles/r3_resnet_conv1x1.md):
+
+    * forward y = x·Wᵀ and input gradient dX = dY·W on gemm_nt4 where its
+      contract holds (output width % 128, reduction ≥ 256), else MIOpen;
+    * weight gradient dW = dYᵀ·X on gemm_dw4 where it has ≥ 8 output tiles,
+      else hipBLASLt over 64 token slices + an fp32 fold (no MIOpen zero-fill /
+      cast passes), else (64 × 64) MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        m = _native.require_hip()
+        N, C, H, W_ = x.shape
+        Co = w.shape[0]
+        wb = w.detach().to(torch.bfloat16).view(Co, C) if w.dtype != torch.bfloat16 else w.view(Co, C)
+        T = N * H * W_
+        x2 = x.permute(0, 2, 3, 1).reshape(T, C)
+        if m.gemm_nt_supported(T, Co, C):
+            y = m.gemm_nt(x2, wb).view(N, H, W_, Co).permute(0, 3, 1, 2)
+        else:
+            y = F.conv2d(x, wb.view(Co, C, 1, 1))
+        ctx.save_for_backward(x, wb)
+        ctx.wdtype = w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x, wb = ctx.saved_tensors
+        N, C, H, W_ = x.shape
+        Co = wb.shape[0]
+        T = N * H * W_
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dy2 = dy.permute(0, 2, 3, 1).reshape(T, Co)
+        x2 = x.permute(0, 2, 3, 1).reshape(T, C)
+        cb = torch.ops.aten.convolution_backward
+        w4 = wb.view(Co, C, 1, 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if m.gemm_nt_supported(T, C, Co):
+                dx = m.gemm_nt(dy2, transpose(wb)).view(N, H, W_, C).permute(0, 3, 1, 2)
+            else:
+                dx = cb(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            tiles = ((Co + 255) // 256) * (C // 256)
+            g = torch.empty(Co, C, device=x.device, dtype=torch.bfloat16)
+            if tiles >= 8 and m.gemm_dw(dy2, x2, g, False):
+                pass
+            elif Co * C >= 64 * 256 and T % 64 == 0:
+                s = 64
+                part = torch.bmm(dy2.view(s, T // s, Co).transpose(1, 2), x2.view(s, T // s, C))
+                g = part.sum(0, dtype=torch.float32)
+            else:
+                g = cb(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+            dw = g.view(Co, C, 1, 1).to(ctx.wdtype)
+        return dx, dw
+
+
+_CONV1X1 = [os.environ.get("PDO_CONV1X1", "1") != "0"]
+
+
+def conv1x1(conv: torch.nn.Conv2d, x):
+    """``conv(x)`` for a 1×1, stride-1, bias-free convolution; the GEMM path
+    (_Conv1x1Fn) for channels_last bf16 activations on the HIP path."""
+    if (_CONV1X1[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.kernel_size == (1, 1)
+            and conv.stride == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None
+            and x.shape[1] % 64 == 0 and conv.out_channels % 64 == 0
+            and (x.shape[0] * x.shape[2] * x.shape[3]) % 256 == 0):
+        return _Conv1x1Fn.apply(x, conv.weight)
+    return conv(x)
+
+
 class _MaxPool3s2Fn(torch.autograd.Function):
     """3×3 / stride 2 / pad 1 max-pool, NHWC bf16 (csrc/hip/pool.hip)."""
 

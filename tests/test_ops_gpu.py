@@ -599,6 +599,35 @@ def test_bn_act_nhwc(cuda, N, C, H, relu, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,Cin,Cout,H", [(16, 256, 64, 16), (16, 64, 256, 16), (8, 512, 256, 16),
+                                          (16, 1024, 256, 8), (4, 64, 64, 16), (8, 256, 128, 32)])
+def test_conv1x1_gemm_path_vs_fp32(cuda, N, Cin, Cout, H):
+    """ops.conv1x1 (GEMM products, MIOpen where it measured faster) against an
+    fp32 convolution: output, input gradient and weight gradient, under
+    autocast with an fp32 master weight as in the ResNet trainer."""
+    ops = _ops()
+    g = torch.Generator(device=cuda).manual_seed(Cin + Cout)
+    conv = torch.nn.Conv2d(Cin, Cout, 1, bias=False).to(cuda)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, device=cuda, generator=g))
+    x = torch.randn(N, Cin, H, H, device=cuda, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, Cout, H, H, device=cuda, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    xh = x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.conv1x1(conv, xh)
+    y.backward(dy)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xf = x.float().requires_grad_()
+    wf = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    yf = torch.nn.functional.conv2d(xf, wf)
+    yf.backward(dy.float())
+    assert rel_err(y, yf) < 1e-2
+    assert rel_err(xh.grad, xf.grad) < 1e-2
+    assert conv.weight.grad.dtype == torch.float32
+    assert rel_err(conv.weight.grad, wf.grad) < 2e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("N,C,H,W", [(4, 64, 112, 112), (2, 16, 9, 7), (3, 8, 2, 5)])
 def test_maxpool3s2_nhwc(cuda, N, C, H, W):
     """HIP 3×3/2 max-pool (fwd value + gather backward) vs fp32 PyTorch."""
