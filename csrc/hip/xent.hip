@@ -23,8 +23,8 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16* __restrict__ 
   const bf16x8* lv = reinterpret_cast<const bf16x8*>(logits + (size_t)row * Vp);
   const int nv = Vp >> 3;
   float m = -INFINITY, s = 0.f;
-  for (int i = threadIdx.x; i < nv; i += 256) {
-    f32x8 v = to_f32(lv[i]);
+  auto acc = [&](bf16x8 raw, int i) {
+    f32x8 v = to_f32(raw);
     const int c0 = i * 8;
     float vm = -INFINITY;
 #pragma unroll
@@ -38,7 +38,16 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16* __restrict__ 
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += __expf(v[j] - m);
+  };
+  int i = threadIdx.x;
+  for (; i + 3 * 256 < nv; i += 4 * 256) {  // four loads in flight per thread
+    const bf16x8 a0 = lv[i], a1 = lv[i + 256], a2 = lv[i + 512], a3 = lv[i + 768];
+    acc(a0, i);
+    acc(a1, i + 256);
+    acc(a2, i + 512);
+    acc(a3, i + 768);
   }
+  for (; i < nv; i += 256) acc(lv[i], i);
   // wave combine of (m, s)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -95,8 +104,8 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16* __restrict__ 
   const bf16x8* lv = reinterpret_cast<const bf16x8*>(logits + (size_t)row * Vp);
   bf16x8* dv = reinterpret_cast<bf16x8*>(dlogits + (size_t)row * Vp);
   const int nv = Vp >> 3;
-  for (int i = threadIdx.x; i < nv; i += 256) {
-    f32x8 v = to_f32(lv[i]);
+  auto grad = [&](bf16x8 raw, int i) {
+    const f32x8 v = to_f32(raw);
     const int c0 = i * 8;
     f32x8 o;
 #pragma unroll
@@ -107,7 +116,18 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16* __restrict__ 
       o[j] = p * scale;
     }
     dv[i] = to_bf16(o);
+  };
+  // four 16-B loads in flight per thread before the first use: one per thread
+  // left the row pass latency-bound (≈ 5.2 TB/s for the read + write stream)
+  int i = threadIdx.x;
+  for (; i + 3 * 256 < nv; i += 4 * 256) {
+    const bf16x8 a0 = lv[i], a1 = lv[i + 256], a2 = lv[i + 512], a3 = lv[i + 768];
+    grad(a0, i);
+    grad(a1, i + 256);
+    grad(a2, i + 512);
+    grad(a3, i + 768);
   }
+  for (; i < nv; i += 256) grad(lv[i], i);
 }
 
 int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,
