@@ -158,3 +158,31 @@ def test_nt4_half_width_last_tile(hip, impl):
     torch.nn.functional.gelu(xp, approximate="tanh").backward(ref.to(torch.bfloat16).float())
     torch.testing.assert_close(dx.float(), xp.grad, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=3e-2, atol=0.5)
+
+
+@pytest.mark.parametrize("impl", [13, 16])
+def test_nt4_fused_epilogues_many_tiles_vs_fp32(hip, impl):
+    """The GELU and GELU'+bias-grad epilogues on a grid with several tiles per
+    persistent workgroup (16384 x 4096 x 1024: 1024 tiles over 256 workgroups),
+    against fp32: pre-activation, activation, input gradient, bias gradient."""
+    M, N, K = 16384, 4096, 1024
+    g = torch.Generator(device="cuda").manual_seed(21)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
+    bias = torch.empty(N, device="cuda", dtype=torch.bfloat16).uniform_(-0.1, 0.1, generator=g)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16).uniform_(-2, 2, generator=g)
+    prev = hip.gemm_nt_impl(impl)
+    try:
+        p, y = hip.gemm_nt_gelu(a, b, bias)
+        dx, db = hip.gemm_nt_dgelu(a, b, pre, bias)
+    finally:
+        hip.gemm_nt_impl(prev)
+    ref = a.float() @ b.float().t()
+    tol = 1e-2 + 8e-3 * ref.abs()
+    assert bool(((p.float() - ref).abs() <= tol).all())
+    gl = torch.nn.functional.gelu(p.float() + bias.float(), approximate="tanh")
+    assert bool(((y.float() - gl).abs() <= 1e-2 + 8e-3 * gl.abs()).all())
+    xp = (pre.float() + bias.float()).requires_grad_(True)
+    torch.nn.functional.gelu(xp, approximate="tanh").backward(ref.to(torch.bfloat16).float())
+    assert bool(((dx.float() - xp.grad).abs() <= 2e-2 + 1e-2 * xp.grad.abs()).all())
+    torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=2e-2, atol=0.5)
