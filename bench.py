@@ -297,6 +297,9 @@ def orchestrate(a):
     if gpus:
         # read by the in-process agent (csrc/core/agent.cpp) and its warm launcher
         os.environ["PDO_GPU_VISIBILITY"] = "isolate" if a.rehearse_shared_gpu else a.gpu_visibility
+        # warm slots per GPU: two (back-to-back jobs start warm) up to 2 GPUs; one
+        # above, so ranks + slots stay at ≤ 2 processes per GPU on a full node
+        os.environ.setdefault("PDO_SLOTS_PER_GPU", "2" if N <= 2 else "1")
     sandbox = tempfile.mkdtemp(prefix="pdo-bench-")
     if a.no_warm_slots:
         os.environ["PDO_WARM_SLOTS"] = "0"  # read by the agent when it starts the zygote
