@@ -21,7 +21,7 @@
 //     first and also writes delta = rowsum(dO ∘ O) (its dO fragments are
 //     already in registers) and lse·log2e, which dK/dV then DMAs: no
 //     separate delta pass.
-// Staging choice per kernel measured in the training step (tools/gpu_so_prof.sh:
+// Staging choice per kernel measured in the training step (profiled with tools/gpu.sh step / soab:
 // rocprofv3 per-kernel times of extension variants in one session): LDS-DMA
 // wins for dK/dV (427.7 vs 448.0 µs) but not for the forward (DMA 2-slot ring at
 // 4 waves/SIMD 278.5 µs, 3-slot 275.6, register staging 267.4 — although the

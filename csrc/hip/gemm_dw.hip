@@ -26,7 +26,7 @@
 // plain LDS-DMA 2-barrier versions of this tiling ran 0.92-0.95 PF, and a
 // 16x16x32 version over a 5-deep ring of 32-token stages (gemm_nt.hip's
 // schedule, which gained 5 % there) ran 8-20 % slower here: qkv 445, proj
-// 165, fc1 546, fc2 523 µs (tools/gpu_dw.sh).
+// 165, fc1 546, fc2 523 µs (tools/dw_probe.py).
 #include "common.h"
 #include "kernels.h"
 

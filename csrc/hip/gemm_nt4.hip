@@ -838,7 +838,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
   static const int group_m = [] {
     const char* e = getenv("PDO_NT_GROUP_M");
-    // 8: tools/gpu_group_m.sh on the GPT-2 NT shapes (row-major = 1: wide K = 1024 GEMM
+    // 8: group_m sweep (tools/nt4_probe.py; in the step: tools/gpu.sh stepab, 8 ahead of 4 and 16) on the GPT-2 NT shapes (row-major = 1: wide K = 1024 GEMM
     // 501 -> 451 us, fc2 dX ⊙ GELU' 642 -> 607, qkv 433 -> 419; 16 is slower; bit-identical)
     const int g = e ? atoi(e) : 8;
     return g >= 1 ? g : 1;
