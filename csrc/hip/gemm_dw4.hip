@@ -340,6 +340,225 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
     }
 }
 
+// ============================================================================
+// The half-buffer-refill schedule on v_mfma_f32_16x16x32_bf16 (variant 3).
+// Same tile (256 × 256 per workgroup, 128 × 128 per wave), same DMA and
+// barriers; each wave's outputs are 8 × 8 accumulators of 16 × 16 (still 256
+// AGPRs), a 32-token block is ONE k-step (8 A + 8 B fragments, 64 MFMAs of
+// half the 32x32x16 cycles).  Why: on random bf16 data the chip holds a higher
+// clock on the 16x16x32 shape — MI355X_MICROARCH.md 'DVFS give-back' item 7
+// (1.12-1.15x FLOP/s at equal cycles per FLOP in LDS-fed loops).
+//
+// Fragment: lane group g = l >> 4 reads 4 token rows 4g .. 4g+3 (lo) and
+// 16 + 4g .. (hi) of the 16 columns cb .. cb+15 with ds_read_b64_tr_b16, so lane
+// l holds column cb + (l & 15) at tokens {4g..4g+3, 16+4g..16+4g+3} — a k
+// permutation shared by both operands.  The 16 rows a wave reads per
+// instruction pair up as lane groups {0,1} / {2,3} (or {0,2} / {1,3}); with the
+// 32x32 swizzle rows r and r + 4 would hit the same banks, so this tile's
+// swizzle XORs the 32-B column pair index with (r & 3) | bit2 = b2(r) ^ b3(r):
+// 8 distinct bank octets for either pairing.  The DMA's source-side swizzle
+// then depends on the piece's parity (row bit 3): two per-lane offsets per operand.
+__device__ __forceinline__ int swz16(int r) { return ((r & 3) | ((((r >> 2) ^ (r >> 3)) & 1) << 2)) << 1; }
+__device__ __forceinline__ int loff16(int r, int ch) { return r * LROW + ((ch ^ swz16(r)) << 3); }
+__device__ __forceinline__ int frag_base16(int cb, int lane) {
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  const int col = cb + 4 * p;
+  return loff16(4 * g + q, col >> 3) + (col & 7);
+}
+template <int K0>
+__device__ __forceinline__ bf16x8 frag16(const bf16* T) {
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(T + K0 * LROW));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(T + (K0 + 16) * LROW));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ __launch_bounds__(NTHR, 1) void gemm_dw4m16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                              int lda, int ldb, int M, int N, int ksteps_total,
+                                                              int splits, bf16* __restrict__ C, int ldc,
+                                                              long long split_stride, int accumulate) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];  // [buf][A|B][BK][256]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n * splits;
+  int id = blockIdx.x;
+  {  // bijective XCD remap
+    const int xcd = id & 7, slot = id >> 3, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tn = id % tiles_n;
+  const int tm = (id / tiles_n) % tiles_m;
+  const int split = id / (tiles_n * tiles_m);
+  const int pq = (ksteps_total >> 1) / splits, pr = (ksteps_total >> 1) % splits;
+  const int k0 = 2 * (split * pq + min(split, pr));
+  const int nk = 2 * (pq + (split < pr ? 1 : 0));
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // LDS-DMA: piece i of an operand = rows 8i + 2w + rl (rl = l >> 5), LDS chunk
+  // l & 31 ← global chunk (l & 31) ^ swz16(row); swz16 of that row is fixed per
+  // lane up to the piece parity (row bit 3 = i & 1)
+  const int rl = lane >> 5, rw = 2 * w + rl;
+  unsigned voffA[2], voffB[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int cs = (lane & 31) ^ swz16(8 * par + rw);
+    const int csa = (m0 + BM > M && cs >= 16) ? cs - 16 : cs;  // half-height edge tile (as gemm_dw4_kernel)
+    voffA[par] = (unsigned)((rl * lda + csa * 8) * 2);
+    voffB[par] = (unsigned)((rl * ldb + cs * 8) * 2);
+  }
+  const bf16* baseA = A + ((size_t)k0 * BK + 2 * w) * lda + m0;
+  const bf16* baseB = B + ((size_t)k0 * BK + 2 * w) * ldb + n0;
+  const unsigned stepAb = (unsigned)(16 * lda), stepBb = (unsigned)(16 * ldb);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem + (unsigned)(w * 1024);
+  auto glds = [](unsigned voff, const bf16* sbase, unsigned lds_byte) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
+                 : "v"(voff), "s"(sbase), "s"(lds_byte)
+                 : "memory");
+  };
+  struct Src {
+    const char* a;
+    const char* b;
+    unsigned sa, sb;
+  };
+  auto srcs = [&](int kt) {
+    Src r{reinterpret_cast<const char*>(baseA + (size_t)kt * BK * lda),
+          reinterpret_cast<const char*>(baseB + (size_t)kt * BK * ldb), stepAb, stepBb};
+    asm volatile("" : "+s"(r.a), "+s"(r.b), "+s"(r.sa), "+s"(r.sb));
+    return r;
+  };
+  auto dma = [&](const Src& sr, auto buf_tag, int p) {  // p < 8: A piece p, else B piece p - 8
+    constexpr int BUF = decltype(buf_tag)::value;
+    const unsigned base = lds0 + (unsigned)(BUF * 2 * OPB);
+    if (p < 8) glds(voffA[p & 1], reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
+    else glds(voffB[p & 1], reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+  };
+
+  // fragment slot q (0..15) of block h (tokens 32h .. 32h+31): q < 8 → A rows
+  // wm·128 + 16q, else B columns wn·128 + 16(q - 8)
+  const bf16* smA[2] = {smem, smem + 2 * TILE};
+  int fo[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fo[i] = frag_base16(wm * 128 + 16 * i, lane);
+    fo[8 + i] = TILE + frag_base16(wn * 128 + 16 * i, lane);
+  }
+  auto rd = [&](auto buf_tag, int h, int q) -> bf16x8 {
+    constexpr int BUF = decltype(buf_tag)::value;
+    const bf16* T = smA[BUF] + fo[q];
+    return h ? frag16<32>(T) : frag16<0>(T);
+  };
+  auto mma = [](f32x4& c, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  };
+  auto mma0 = [](f32x4& c, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+
+  f32x4 acc[8][8];  // first written by mma0 in tile 0's block 0
+  bf16x8 f0[16], f1[16];
+
+  {
+    const Src s0 = srcs(0), s1 = srcs(1);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) dma(s1, B1{}, p);
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (tile 1 may fly)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) f0[q] = rd(B0{}, 0, q);
+  // group g of a block: A fragment g >> 1 against B fragments 4(g & 1) .. +3
+  auto tileH = [&](int t, auto buf_tag, auto more_tag, auto first_tag, auto eout_tag) {
+    constexpr int BUF = decltype(buf_tag)::value;
+    constexpr bool MORE = decltype(more_tag)::value;
+    constexpr bool FIRST = decltype(first_tag)::value;
+    constexpr bool EOUT = decltype(eout_tag)::value;
+    using NB = std::integral_constant<int, BUF ^ 1>;
+    using SB = std::integral_constant<int, BUF>;
+    Src sn2{};
+    if constexpr (EOUT) sn2 = srcs(t + 2);
+    // B0: every wave's F0(t) reads (tokens 0-31 of BUF) are done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int mb = g >> 1, nb0 = 4 * (g & 1);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (FIRST) mma0(acc[mb][nb0 + u], f0[mb], f0[8 + nb0 + u]);
+        else mma(acc[mb][nb0 + u], f0[mb], f0[8 + nb0 + u]);
+      }
+      f1[g] = rd(buf_tag, 1, g);
+      if constexpr (EOUT) {
+        if (g & 1) dma(sn2, SB{}, (g >> 1) < 4 ? (g >> 1) : (g >> 1) + 4);  // first-half pieces
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // B1: every wave's F1(t) reads are done and tile t+1 has landed
+    if constexpr (MORE || EOUT) {
+      if constexpr (EOUT)
+        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int mb = g >> 1, nb0 = 4 * (g & 1);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) mma(acc[mb][nb0 + u], f1[mb], f1[8 + nb0 + u]);
+      if constexpr (MORE) f0[g] = rd(NB{}, 0, g);
+      if constexpr (EOUT) {
+        if (g & 1) dma(sn2, SB{}, (g >> 1) < 4 ? (g >> 1) + 4 : (g >> 1) + 8);  // second-half pieces
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  tileH(0, B0{}, T_{}, T_{}, T_{});
+  tileH(1, B1{}, T_{}, F_{}, T_{});
+  for (int t = 2; t < nk - 2; t += 2) {
+    tileH(t, B0{}, T_{}, F_{}, T_{});
+    tileH(t + 1, B1{}, T_{}, F_{}, T_{});
+  }
+  tileH(nk - 2, B0{}, T_{}, F_{}, F_{});
+  tileH(nk - 1, B1{}, F_{}, F_{}, F_{});
+
+  // ---- epilogue: acc[mb][nb][r] = C[m0 + wm·128 + 16mb + 4(l >> 4) + r][n0 + wn·128 + 16nb + (l & 15)]
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  bf16* Cb = C + (size_t)split * split_stride;
+  const int g4 = lane >> 4, li = lane & 15;
+  if (m0 + wm * 128 >= M) return;  // edge tile: wm = 1 holds rows m0 + 128 .. (wave-uniform)
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[r]) : "a"(acc[mb][nb][r]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 128 + 16 * mb + 4 * g4 + r;
+        bf16* p = Cb + (size_t)m * ldc + n0 + wn * 128 + 16 * nb + li;
+        float x = v[r];
+        if (accumulate) x += (float)*p;
+        *p = (bf16)x;
+      }
+    }
+}
+
 }  // namespace
 
 // every slice gets ≥ 2 pairs of k-tiles (uneven splits allowed: pairs are dealt
@@ -368,6 +587,8 @@ int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, i
     gemm_dw4_kernel<7><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   else if (variant == 2)  // half-buffer refill schedule (two barriers per tile, ≈1.5 tiles of DMA lead)
     gemm_dw4_kernel<-1><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+  else if (variant == 3)  // variant 2's schedule on 16x16x32 MFMAs
+    gemm_dw4m16_kernel<<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   else
     gemm_dw4_kernel<11><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   if (splits > 1) return splitk_add(ws, splits, (long long)M * N, C, accumulate, st);

@@ -661,7 +661,7 @@ def test_gemm_dw4_half_height_edge(cuda, T, M, N, acc, splits):
     ref = base.float() + dy.float().t() @ x.float()
     prev = m.gemm_dw_impl(-1)
     try:
-        for impl in (1, 2, 3):
+        for impl in (1, 2, 3, 4):
             m.gemm_dw_impl(impl)
             out = base.clone()
             assert m.gemm_dw(dy, x, out, True, splits)
@@ -675,7 +675,7 @@ def test_gemm_dw4_half_height_edge(cuda, T, M, N, acc, splits):
 @pytest.mark.parametrize("T,M,N,acc", [(8192, 4096, 4096, True), (65536, 1024, 3072, False), (16384, 512, 768, True),
                                        (16384, 3072, 1024, True)])  # last: 48 tiles → 5 uneven slices
 def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
-    """The 4-wave dW mainloop (gemm_dw4.hip, all three schedule variants; split-K or
+    """The 4-wave dW mainloop (gemm_dw4.hip, all four variants incl. the 16x16x32 one; split-K or
     in-kernel accumulate at one split) and the 8-wave one against fp32."""
     from paddle_operator_amd import _native
     m = _native.require_hip()
@@ -687,7 +687,7 @@ def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
     ref = base.float() + dy.float().t() @ x.float()
     prev = m.gemm_dw_impl(0)
     try:
-        for impl in (0, 1, 2, 3):
+        for impl in (0, 1, 2, 3, 4):
             m.gemm_dw_impl(impl)
             out = base.clone()
             assert m.gemm_dw(dy, x, out, True)

@@ -36,7 +36,7 @@ def bench(fn, iters, warm=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=65536)
-    ap.add_argument("--variants", type=int, default=2)
+    ap.add_argument("--variants", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -73,7 +73,7 @@ def main():
             rec[k + "_PF"] = round(fl / med / 1e9, 3)
         print(json.dumps(rec), flush=True)
         del dy, x, out
-    m.gemm_dw_impl(3)
+    m.gemm_dw_impl(4)
 
 
 if __name__ == "__main__":

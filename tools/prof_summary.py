@@ -63,6 +63,27 @@ def main():
         if a.steps:
             line += f" {d/1e6/a.steps:.3f} |"
         print(line)
+    # device idle inside the steady-state steps: steps end at the optimizer kernel
+    # (one adamw dispatch per step); between the 2nd and the last one, busy = the
+    # union of kernel intervals, idle = span - busy (launch gaps, host stalls)
+    ends = sorted(r[3] for r in rows if "adamw" in r[0])
+    if len(ends) >= 4:
+        lo, hi = ends[1], ends[-1]
+        iv = sorted((max(s, lo), min(e, hi)) for _, _, s, e in rows if e > lo and s < hi)
+        busy, cur_s, cur_e = 0, None, None
+        for s, e in iv:
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        busy += cur_e - cur_s
+        n = len(ends) - 2
+        nk = sum(1 for _, _, s, e in rows if s >= lo and e <= hi)
+        print(f"\nsteady state ({n} steps between optimizer kernels): {(hi - lo) / 1e6 / n:.3f} ms/step span, "
+              f"{busy / 1e6 / n:.3f} busy, {(hi - lo - busy) / 1e6 / n:.3f} idle "
+              f"({nk // n} dispatches/step, {(hi - lo - busy) / 1e3 / max(nk, 1):.2f} us idle per dispatch)")
     try:
         regs = c.execute("select name, start, end, extdata from regions").fetchall()
     except sqlite3.Error:
