@@ -241,6 +241,7 @@ static int g_impl = [] {
 static int nt4_variant(int epi, int K) {
   if (g_impl == 13) return epi == 2 ? 9 : 11;
   if (g_impl == 16) return K <= 1024 ? 13 : 12;
+  if (g_impl == 17) return K <= 1024 ? 15 : 14;  // impl 16 with the deferred store drain
   return g_impl - 1;
 }
 

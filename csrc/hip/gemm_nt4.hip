@@ -142,6 +142,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   // epilogue's conversions and stores, and the stores drain under the next mainloop.
   constexpr bool PERS = (SCHED & 32) != 0;
   static_assert(!PERS || (SCHED & 5) == 5, "persistent tiles: SCHED 1 mainloop with the register row epilogue");
+  // SCHED & 64 (with PERS): the row epilogue's stores drain under the next
+  // tile's first two k-tiles.  vmcnt retires loads, stores and LDS-DMA in issue
+  // order, so "wait for the next tile's pieces" was written vmcnt(16), which
+  // also waited for every store of the epilogue issued after them — the
+  // epilogue's 128-256 KiB per workgroup then drained with the matrix pipe
+  // idle.  Tiles 0 and 1 of the next tile were issued BEFORE the stores, so
+  // their waits may leave the NST stores in flight: vmcnt(16 + NST) (capped at
+  // the counter's 63).  Tile 2's pieces come after the stores; its wait drains them.
+  constexpr bool DEFER = (SCHED & 64) != 0;
+  static_assert(!DEFER || PERS, "deferred store drain: persistent tiles only");
+  constexpr int NST = EPI == 2 ? 64 : EPI == 3 ? 34 : 32;  // vm stores one wave's row epilogue issues
+  constexpr int WDEF = 16 + NST > 63 ? 63 : 16 + NST;
+  int pend = 0;  // this wave has epilogue stores in flight (wave-uniform)
   auto coords = [&](int v, int& tm_, int& tn_) {
     int id = v;
     {  // bijective XCD remap: each XCD walks a contiguous range of tiles (shared A panels in its L2)
@@ -459,9 +472,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         }
         if constexpr (LOAD && s >= 52 && s < 92 && (s - 52) % 5 == 0) dma(sn2, SB{}, (MIR ? 0 : 8) + (s - 52) / 5);
         if constexpr (MORE && s == 93) {
-          // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in flight)
-          if constexpr (LOAD) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in flight;
+          // DEFER: in the first tile after an epilogue, its stores too)
+          if constexpr (LOAD && DEFER && FIRST) {
+            if (pend) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WDEF) : "memory");
+            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          } else if constexpr (LOAD) {
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           __builtin_amdgcn_sched_barrier(0);
           __builtin_amdgcn_s_barrier();
         }
@@ -473,7 +493,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     using F_ = std::false_type;
     issue01();
     for (;;) {
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (tile 1 may fly)
+      // tile 0 landed (tile 1 may fly; DEFER: and the previous epilogue's stores)
+      if (DEFER && pend) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WDEF) : "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -503,6 +525,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         dhalfn = ntn * BN + BN > N;
         issue01();
         row_epilogue();  // of this tile (m0, n0, tm, halfn)
+        pend = __builtin_amdgcn_readfirstlane((halfn && wn == 1) ? 0 : 1);
         vcur = vn;
         tm = ntm;
         tn = ntn;
@@ -816,7 +839,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 }  // namespace
 
 // the variants with row-major accumulators (SCHED & 4) take N % 256 = 128
-int gemm_nt4_half_n(int variant) { return variant == 8 || variant == 9 || variant == 11 || variant == 12 || variant == 13; }
+int gemm_nt4_half_n(int variant) { return variant == 8 || variant == 9 || (variant >= 11 && variant <= 15); }
 
 // persistent variants: one workgroup per CU (a multiple of 8: the XCD mapping)
 static int persistent_grid(long long tiles) {
@@ -886,6 +909,8 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
     case 11: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 29>{});  // impl 10 + mirrored schedule
     case 12: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 61>{});  // variant 11, persistent
     case 13: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 45>{});  // variant 9, persistent
+    case 14: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 125>{});  // variant 12, deferred store drain
+    case 15: return launch(I1{}, I11{}, I2{}, std::integral_constant<int, 109>{});  // variant 13, deferred store drain
     default: return launch(I1{}, I11{}, I2{}, I1{});
   }
   return 0;
