@@ -157,11 +157,17 @@ struct Stage {
   bf16x8 v[2];
 };
 
+// The tile origin is wave-uniform (a scalar pointer) and the lane's part a
+// loop-invariant 32-bit byte offset, so each load is one saddr-form
+// global_load_dwordx4 — not the 64-bit multiply-add address chain per load
+// per tile that (base + (row0 + r) · stride) compiled to (17 VALU per tile).
 __device__ __forceinline__ void stage_load(Stage& st, const bf16* base, size_t row_stride, int row0, int tid) {
+  const char* sp = reinterpret_cast<const char*>(base + (size_t)row0 * row_stride);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    st.v[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(row0 + r) * row_stride + ch * 8);
+    const unsigned off = (unsigned)((r * (int)row_stride + ch * 8) * 2);
+    st.v[i] = *reinterpret_cast<const bf16x8*>(sp + off);
   }
 }
 
