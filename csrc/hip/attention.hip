@@ -325,13 +325,8 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
 // SPLIT: the 64-key tile's softmax runs per 32-key half, each with its own
 // defer-max check, so the exp / sum / pack of half 0 and its P·V depend only on
 // half 0's score MFMAs and can run while half 1's are still in the matrix pipe
-// HOIST: the tile's LDS operand reads are issued as a batch ahead of their
-// MFMAs instead of one read pair per MFMA (hipcc otherwise emits read → wait
-// lgkmcnt → MFMA for each, exposing the LDS latency 16 times per tile): 1 = all
-// 8 K fragments before the score MFMAs and the first 4 V fragments before the
-// softmax VALU (+16 VGPRs at the peak), 2 = all 8 V fragments (+32)
-template <int PRIO, int SPLIT = 0, int HOIST = 0, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+template <int PRIO, int SPLIT = 0>
+__global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int B, int S, int H, float c2,
                                                      int order) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
@@ -386,19 +381,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int ks = 0; ks < 4; ++ks) s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
-      } else if constexpr (HOIST) {
-        bf16x8 k0[4], k1[4];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          k0[ks] = row_frag(Kt, 0, ks, lane);
-          k1[ks] = row_frag(Kt, 32, ks, lane);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          s0 = mfma(k0[ks], qf[ks], s0);
-          s1 = mfma(k1[ks], qf[ks], s1);
-        }
       } else {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -462,23 +444,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         half(s0, s1, std::integral_constant<int, 0>{});
         half(s1, s0, std::integral_constant<int, 1>{});
       } else {
-        const bf16* V0 = Vt + vb0;
-        const bf16* V1 = Vt + vb1;
-        // HOIST: V fragments in flight under the mask / max / exp work
-        bf16x8 vh[HOIST ? 8 : 1];
-        if constexpr (HOIST) {
-          vh[0] = tr_frag_v<0>(V0);
-          vh[1] = tr_frag_v<0>(V1);
-          vh[2] = tr_frag_v<32>(V0);
-          vh[3] = tr_frag_v<32>(V1);
-          if constexpr (HOIST >= 2) {
-            vh[4] = tr_frag_v<16>(V0);
-            vh[5] = tr_frag_v<16>(V1);
-            vh[6] = tr_frag_v<48>(V0);
-            vh[7] = tr_frag_v<48>(V1);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
         if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
           // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
           const int d = q - key0 - 4 * hh;
@@ -521,45 +486,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
         }
         l += ls2[0] + ls2[1];
+        const bf16* V0 = Vt + vb0;
+        const bf16* V1 = Vt + vb1;
         prio_hi<PRIO>();
-        if constexpr (HOIST) {
-          bf16x8 vb[4];
-          if constexpr (HOIST < 2) {  // the second half's reads go out now, under the first half's MFMAs
-            vb[0] = tr_frag_v<16>(V0);
-            vb[1] = tr_frag_v<16>(V1);
-            vb[2] = tr_frag_v<48>(V0);
-            vb[3] = tr_frag_v<48>(V1);
-          } else {
-            vb[0] = vh[4];
-            vb[1] = vh[5];
-            vb[2] = vh[6];
-            vb[3] = vh[7];
-          }
+        {
           const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
-          o0 = mfma(vh[0], p0, o0);
-          o1 = mfma(vh[1], p0, o1);
-          o0 = mfma(vh[2], p1, o0);
-          o1 = mfma(vh[3], p1, o1);
-          const bf16x8 q0 = pack8(s0, 1), q1 = pack8(s1, 1);
-          o0 = mfma(vb[0], q0, o0);
-          o1 = mfma(vb[1], q0, o1);
-          o0 = mfma(vb[2], q1, o0);
-          o1 = mfma(vb[3], q1, o1);
-        } else {
-          {
-            const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
-            o0 = mfma(tr_frag_v<0>(V0), p0, o0);
-            o1 = mfma(tr_frag_v<0>(V1), p0, o1);
-            o0 = mfma(tr_frag_v<32>(V0), p1, o0);
-            o1 = mfma(tr_frag_v<32>(V1), p1, o1);
-          }
-          {
-            const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
-            o0 = mfma(tr_frag_v<16>(V0), p0, o0);
-            o1 = mfma(tr_frag_v<16>(V1), p0, o1);
-            o0 = mfma(tr_frag_v<48>(V0), p1, o0);
-            o1 = mfma(tr_frag_v<48>(V1), p1, o1);
-          }
+          o0 = mfma(tr_frag_v<0>(V0), p0, o0);
+          o1 = mfma(tr_frag_v<0>(V1), p0, o1);
+          o0 = mfma(tr_frag_v<32>(V0), p1, o0);
+          o1 = mfma(tr_frag_v<32>(V1), p1, o1);
+        }
+        {
+          const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
+          o0 = mfma(tr_frag_v<16>(V0), p0, o0);
+          o1 = mfma(tr_frag_v<16>(V1), p0, o1);
+          o0 = mfma(tr_frag_v<48>(V0), p1, o0);
+          o1 = mfma(tr_frag_v<48>(V1), p1, o1);
         }
         prio_lo<PRIO>();
       }
@@ -570,6 +512,171 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       stage_store_v(sv, Kn + TROWS * HD, tid);
     }
     __syncthreads();
+  }
+  const float lt = xhalf_sum(l);
+  const float inv = 1.f / lt;
+  bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
+  store_acc_rows(orow, o0, 0, hh, inv);
+  store_acc_rows(orow, o1, 32, hh, inv);
+  if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
+}
+
+// ============================================================================
+// forward, software-pipelined across key tiles (PDO_ATTN_FWD=8): the score
+// MFMAs of tile t+1 are issued BEFORE the softmax VALU of tile t, so the matrix
+// pipe works through S(t+1) (then P·V(t)) while the same wave's VALU runs the
+// max / exp / sum / pack of tile t — the overlap no longer rests on the other
+// waves of the SIMD alone.  K therefore runs one tile ahead of V in LDS: in
+// iteration t the K slot (t+1)&1 holds K(t+1) and the V slot t&1 holds V(t);
+// the end of iteration t writes K(t+2) over K(t) (read in iteration t-1) and
+// V(t+1) over V(t-1), behind the iteration's barrier.  A rescale of the
+// running max (defer-max) also shifts the already-computed S(t+1).
+// ============================================================================
+__global__ __launch_bounds__(256) void attn_fwd_pipe_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                         float* __restrict__ lse, int B, int S, int H, float c2,
+                                                         int order) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [slot][K|V][64][64]
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, li = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = S / 128;
+  int bh, r_;
+  attn_block(order, nqb, B * H, bh, r_);
+  const int qb = nqb - 1 - r_;  // heaviest query blocks first
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+
+  const int q = qb * 128 + w * 32 + li;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
+  retire(qf);
+  prescale(qf, c2);
+
+  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = 0.f, l = 0.f;
+  f32x16 nm16 = zero16();
+  const int ntiles = (qb * 128 + 128) / TROWS;  // ≥ 2
+  const int wave_qmax = qb * 128 + w * 32 + 31;
+  const int wave_qmin = qb * 128 + w * 32;
+  auto kslot = [&](int t) -> bf16* { return smem + (t & 1) * 2 * TROWS * HD; };
+  auto vslot = [&](int t) -> bf16* { return smem + (t & 1) * 2 * TROWS * HD + TROWS * HD; };
+
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, kslot(0), tid);
+  stage_store_v(sv, vslot(0), tid);
+  stage_load(sk, kbase, rs, TROWS, tid);
+  stage_store(sk, kslot(1), tid);
+  __syncthreads();
+
+  // S^T of one K tile: the 8 K fragments in flight as one batch, then the MFMAs
+  auto scores = [&](const bf16* Kt, f32x16& a0, f32x16& a1) {
+    bf16x8 k0[4], k1[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      k0[ks] = row_frag(Kt, 0, ks, lane);
+      k1[ks] = row_frag(Kt, 32, ks, lane);
+    }
+    a0 = nm16;
+    a1 = nm16;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      a0 = mfma(k0[ks], qf[ks], a0);
+      a1 = mfma(k1[ks], qf[ks], a1);
+    }
+  };
+  f32x16 s0, s1, n0 = nm16, n1 = nm16;
+  scores(kslot(0), s0, s1);  // key tile 0 reaches every query
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int key0 = t * TROWS;
+    const bool act = key0 <= wave_qmax;  // wave-uniform (w is an SGPR)
+    const bool act1 = t + 1 < ntiles && key0 + TROWS <= wave_qmax;
+    const bool ldv = t + 1 < ntiles, ldk = t + 2 < ntiles;
+    if (ldk) stage_load(sk, kbase, rs, (t + 2) * TROWS, tid);
+    if (ldv) stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    if (act1) scores(kslot(t + 1), n0, n1);
+    if (act) {
+      const bf16* V0 = vslot(t) + vb0;
+      const bf16* V1 = vslot(t) + vb1;
+      bf16x8 vh[4];
+      vh[0] = tr_frag_v<0>(V0);
+      vh[1] = tr_frag_v<0>(V1);
+      vh[2] = tr_frag_v<32>(V0);
+      vh[3] = tr_frag_v<32>(V1);
+      if (key0 + TROWS - 1 > wave_qmin) {  // diagonal tile (wave-uniform)
+        const int d = q - key0 - 4 * hh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = (r & 3) + 8 * (r >> 2);
+          s0[r] = c > d ? -INFINITY : s0[r];
+          s1[r] = c + 32 > d ? -INFINITY : s1[r];
+        }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+      tmax = xhalf_max(tmax);
+      if (t == 0) {
+        m = tmax;
+        s0 -= tmax;
+        s1 -= tmax;
+        if (act1) {
+          n0 -= tmax;
+          n1 -= tmax;
+        }
+        nm16 = bcast16(-m);
+      } else if (__any(tmax > 8.f)) {
+        const float dd = tmax > 8.f ? tmax : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-dd);
+        m += dd;
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+        s0 -= dd;
+        s1 -= dd;
+        if (act1) {
+          n0 -= dd;
+          n1 -= dd;
+        }
+        nm16 = bcast16(-m);
+      }
+      f32x2 ls2 = {0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+      }
+      l += ls2[0] + ls2[1];
+      bf16x8 vb[4];
+      vb[0] = tr_frag_v<16>(V0);
+      vb[1] = tr_frag_v<16>(V1);
+      vb[2] = tr_frag_v<48>(V0);
+      vb[3] = tr_frag_v<48>(V1);
+      const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
+      o0 = mfma(vh[0], p0, o0);
+      o1 = mfma(vh[1], p0, o1);
+      o0 = mfma(vh[2], p1, o0);
+      o1 = mfma(vh[3], p1, o1);
+      const bf16x8 r0 = pack8(s0, 1), r1 = pack8(s1, 1);
+      o0 = mfma(vb[0], r0, o0);
+      o1 = mfma(vb[1], r0, o1);
+      o0 = mfma(vb[2], r1, o0);
+      o1 = mfma(vb[3], r1, o1);
+    }
+    if (ldk) stage_store(sk, kslot(t + 2), tid);
+    if (ldv) stage_store_v(sv, vslot(t + 1), tid);
+    __syncthreads();
+    s0 = n0;
+    s1 = n1;
   }
   const float lt = xhalf_sum(l);
   const float inv = 1.f / lt;
@@ -885,7 +992,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__
 // ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
-template <int PRIO, int HOIST = 0>
+template <int PRIO>
 __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                           bf16* __restrict__ dqkv, int B, int S, int H, float c2,
@@ -974,36 +1081,12 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
           }
         }
         prio_hi<PRIO>();
-        if constexpr (HOIST) {
-          bf16x8 qr[4], dr[4];
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            qr[ks] = row_frag(Qt, 32 * qs, ks, lane);
-            dr[ks] = row_frag(Dt, 32 * qs, ks, lane);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            sacc = mfma(qr[ks], kf[ks], sacc);
-            dpacc = mfma(dr[ks], vf[ks], dpacc);
-          }
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
-            dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
-          }
+        for (int ks = 0; ks < 4; ++ks) {
+          sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
+          dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
         }
         prio_lo<PRIO>();
-        // HOIST: the first half's 4 transposed fragments in flight under the softmax gradient
-        bf16x8 th[HOIST ? 4 : 1];
-        if constexpr (HOIST) {
-          th[0] = tr_frag(Dt, 32 * qs, 0, lane);
-          th[1] = tr_frag(Dt, 32 * qs, 32, lane);
-          th[2] = tr_frag(Qt, 32 * qs, 0, lane);
-          th[3] = tr_frag(Qt, 32 * qs, 32, lane);
-          __builtin_amdgcn_sched_barrier(0);
-        }
         // The causal mask only touches the diagonal sub-tile (wave-uniform): a
         // separate body keeps its compares and selects out of every other tile
         auto softmax_grad = [&](auto masked) {
@@ -1029,17 +1112,10 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 pb = pack8(sacc, sst);
           const bf16x8 db = pack8(dpacc, sst);
-          if (HOIST && sst == 0) {
-            dv0 = mfma(th[0], pb, dv0);
-            dv1 = mfma(th[1], pb, dv1);
-            dk0 = mfma(th[2], db, dk0);
-            dk1 = mfma(th[3], db, dk1);
-          } else {
-            dv0 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 0, lane), pb, dv0);
-            dv1 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 32, lane), pb, dv1);
-            dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
-            dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
-          }
+          dv0 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 0, lane), pb, dv0);
+          dv1 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 32, lane), pb, dv1);
+          dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
+          dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
         }
         prio_lo<PRIO>();
       }
@@ -1079,10 +1155,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(PDO_DKDV_ARGS) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dkdv3_d64(PDO_DKDV_ARGS) {
   dkdv_body<0>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
-// the same with the HOIST batches (PDO_ATTN_DKDV_HOIST=1)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dkdv3h_d64(PDO_DKDV_ARGS) {
-  dkdv_body<0, 1>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
-}
 #undef PDO_DKDV_ARGS
 
 // ============================================================================
@@ -1090,10 +1162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // ============================================================================
 // RING: K / V tiles by LDS-DMA two tiles ahead through 3 slots (the dK/dV
 // kernel's ring) instead of register staging one tile ahead
-// HOIST (as the forward's): the 8 K / V row fragments of a 32-key sub-tile are
-// read as one batch before the score MFMAs, its 4 transposed K fragments before
-// the softmax-gradient VALU
-template <int PRIO, int RING = 0, int HOIST = 0>
+template <int PRIO, int RING = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
@@ -1195,35 +1264,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       for (int ksub = 0; ksub < 2; ++ksub) {
         f32x16 s = zero16(), dp = zero16();
         prio_hi<PRIO>();
-        if constexpr (HOIST) {
-          bf16x8 kr[4], vr[4];
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            kr[ks] = row_frag(Kt, 32 * ksub, ks, lane);
-            vr[ks] = row_frag(Vt, 32 * ksub, ks, lane);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            s = mfma(kr[ks], qf[ks], s);
-            dp = mfma(vr[ks], df[ks], dp);
-          }
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
-            dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
-          }
+        for (int ks = 0; ks < 4; ++ks) {
+          s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
+          dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
         }
         prio_lo<PRIO>();
-        bf16x8 kt[HOIST ? 4 : 1];
-        if constexpr (HOIST) {
-          kt[0] = tr_frag(Kt, 32 * ksub, 0, lane);
-          kt[1] = tr_frag(Kt, 32 * ksub, 32, lane);
-          kt[2] = tr_frag(Kt, 32 * ksub + 16, 0, lane);
-          kt[3] = tr_frag(Kt, 32 * ksub + 16, 32, lane);
-          __builtin_amdgcn_sched_barrier(0);
-        }
         auto softmax_grad = [&](auto masked) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -1243,13 +1289,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 dsb = pack8(s, sst);
-          if constexpr (HOIST) {
-            a0 = mfma(kt[2 * sst], dsb, a0);
-            a1 = mfma(kt[2 * sst + 1], dsb, a1);
-          } else {
-            a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
-            a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
-          }
+          a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
+          a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
         }
         prio_lo<PRIO>();
       }
@@ -1307,12 +1348,8 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
   const int grid = B * H * (S / 128);
   if (variant == 4)
     attn_fwd_d64<0, 1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else if (variant == 5)
-    attn_fwd_d64<0, 0, 1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else if (variant == 6)
-    attn_fwd_d64<0, 0, 2><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else if (variant == 7)  // variant 5 held at 3 waves per SIMD (≤ 168 VGPRs)
-    attn_fwd_d64<0, 0, 1, 3><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  else if (variant == 8)
+    attn_fwd_pipe_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   else if (attn_prio() & 1)
     attn_fwd_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   else
@@ -1326,11 +1363,7 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
   static const int dq3 = env_int("PDO_ATTN_DQ3", 0);
-  static const int dqh = env_int("PDO_ATTN_DQ_HOIST", 0);
-  if (dqh)
-    attn_bwd_dq_d64<0, 0, 1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                                   dbias_part, attn_order());
-  else if (dq3)
+  if (dq3)
     attn_bwd_dq_d64<0, 1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                                 dbias_part, attn_order());
   else if (attn_prio() & 2)
@@ -1341,11 +1374,7 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
                                              dbias_part, attn_order());
   // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step
   static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 1);
-  static const int dkdvh = env_int("PDO_ATTN_DKDV_HOIST", 0);
-  if (dkdv3 && dkdvh)
-    attn_bwd_dkdv3h_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
-                                              attn_order());
-  else if (dkdv3)
+  if (dkdv3)
     attn_bwd_dkdv3_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
                                              attn_order());
   else if (attn_prio() & 4)

@@ -338,10 +338,17 @@ std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre
   return {dx, db};
 }
 
-at::Tensor transpose(at::Tensor x) {
+at::Tensor transpose(at::Tensor x, std::optional<at::Tensor> out) {
   CHECK_IN(x); CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R, C] with R, C % 64 == 0");
-  auto y = at::empty({x.size(1), x.size(0)}, x.options());
+  at::Tensor y;
+  if (out.has_value()) {
+    y = *out;
+    CHECK_IN(y); CHECK_BF16(y);
+    TORCH_CHECK(y.dim() == 2 && y.size(0) == x.size(1) && y.size(1) == x.size(0), "transpose: out must be [C, R]");
+  } else {
+    y = at::empty({x.size(1), x.size(0)}, x.options());
+  }
   CHECK_RC(pdo::transpose_bf16(bp(x), bp(y), (int)x.size(0), (int)x.size(1), cur_stream()), "transpose");
   return y;
 }
@@ -676,7 +683,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("sumsq", &sumsq);
   m.def("adamw_flat", &adamw_flat);
   m.def("splitk_add", &splitk_add);
-  m.def("transpose", &transpose);
+  m.def("transpose", &transpose, py::arg("x"), py::arg("out") = py::none());
   m.def("gemm_dw", &gemm_dw, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = true,
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
