@@ -157,17 +157,11 @@ struct Stage {
   bf16x8 v[2];
 };
 
-// The tile origin is wave-uniform (a scalar pointer) and the lane's part a
-// loop-invariant 32-bit byte offset, so each load is one saddr-form
-// global_load_dwordx4 — not the 64-bit multiply-add address chain per load
-// per tile that (base + (row0 + r) · stride) compiled to (17 VALU per tile).
 __device__ __forceinline__ void stage_load(Stage& st, const bf16* base, size_t row_stride, int row0, int tid) {
-  const char* sp = reinterpret_cast<const char*>(base + (size_t)row0 * row_stride);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
-    const unsigned off = (unsigned)((r * (int)row_stride + ch * 8) * 2);
-    st.v[i] = *reinterpret_cast<const bf16x8*>(sp + off);
+    st.v[i] = *reinterpret_cast<const bf16x8*>(base + (size_t)(row0 + r) * row_stride + ch * 8);
   }
 }
 
@@ -512,171 +506,6 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
       stage_store_v(sv, Kn + TROWS * HD, tid);
     }
     __syncthreads();
-  }
-  const float lt = xhalf_sum(l);
-  const float inv = 1.f / lt;
-  bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
-  store_acc_rows(orow, o0, 0, hh, inv);
-  store_acc_rows(orow, o1, 32, hh, inv);
-  if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
-}
-
-// ============================================================================
-// forward, software-pipelined across key tiles (PDO_ATTN_FWD=8): the score
-// MFMAs of tile t+1 are issued BEFORE the softmax VALU of tile t, so the matrix
-// pipe works through S(t+1) (then P·V(t)) while the same wave's VALU runs the
-// max / exp / sum / pack of tile t — the overlap no longer rests on the other
-// waves of the SIMD alone.  K therefore runs one tile ahead of V in LDS: in
-// iteration t the K slot (t+1)&1 holds K(t+1) and the V slot t&1 holds V(t);
-// the end of iteration t writes K(t+2) over K(t) (read in iteration t-1) and
-// V(t+1) over V(t-1), behind the iteration's barrier.  A rescale of the
-// running max (defer-max) also shifts the already-computed S(t+1).
-// ============================================================================
-__global__ __launch_bounds__(256) void attn_fwd_pipe_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                         float* __restrict__ lse, int B, int S, int H, float c2,
-                                                         int order) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [slot][K|V][64][64]
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, li = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nqb = S / 128;
-  int bh, r_;
-  attn_block(order, nqb, B * H, bh, r_);
-  const int qb = nqb - 1 - r_;  // heaviest query blocks first
-  const int b = bh / H, h = bh % H;
-  const size_t rs = (size_t)3 * H * HD;
-  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
-  const bf16* kbase = qbase + (size_t)H * HD;
-  const bf16* vbase = qbase + (size_t)2 * H * HD;
-
-  const int q = qb * 128 + w * 32 + li;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
-  retire(qf);
-  prescale(qf, c2);
-
-  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
-  f32x16 o0 = zero16(), o1 = zero16();
-  float m = 0.f, l = 0.f;
-  f32x16 nm16 = zero16();
-  const int ntiles = (qb * 128 + 128) / TROWS;  // ≥ 2
-  const int wave_qmax = qb * 128 + w * 32 + 31;
-  const int wave_qmin = qb * 128 + w * 32;
-  auto kslot = [&](int t) -> bf16* { return smem + (t & 1) * 2 * TROWS * HD; };
-  auto vslot = [&](int t) -> bf16* { return smem + (t & 1) * 2 * TROWS * HD + TROWS * HD; };
-
-  Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
-  stage_store(sk, kslot(0), tid);
-  stage_store_v(sv, vslot(0), tid);
-  stage_load(sk, kbase, rs, TROWS, tid);
-  stage_store(sk, kslot(1), tid);
-  __syncthreads();
-
-  // S^T of one K tile: the 8 K fragments in flight as one batch, then the MFMAs
-  auto scores = [&](const bf16* Kt, f32x16& a0, f32x16& a1) {
-    bf16x8 k0[4], k1[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      k0[ks] = row_frag(Kt, 0, ks, lane);
-      k1[ks] = row_frag(Kt, 32, ks, lane);
-    }
-    a0 = nm16;
-    a1 = nm16;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      a0 = mfma(k0[ks], qf[ks], a0);
-      a1 = mfma(k1[ks], qf[ks], a1);
-    }
-  };
-  f32x16 s0, s1, n0 = nm16, n1 = nm16;
-  scores(kslot(0), s0, s1);  // key tile 0 reaches every query
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int key0 = t * TROWS;
-    const bool act = key0 <= wave_qmax;  // wave-uniform (w is an SGPR)
-    const bool act1 = t + 1 < ntiles && key0 + TROWS <= wave_qmax;
-    const bool ldv = t + 1 < ntiles, ldk = t + 2 < ntiles;
-    if (ldk) stage_load(sk, kbase, rs, (t + 2) * TROWS, tid);
-    if (ldv) stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
-    if (act1) scores(kslot(t + 1), n0, n1);
-    if (act) {
-      const bf16* V0 = vslot(t) + vb0;
-      const bf16* V1 = vslot(t) + vb1;
-      bf16x8 vh[4];
-      vh[0] = tr_frag_v<0>(V0);
-      vh[1] = tr_frag_v<0>(V1);
-      vh[2] = tr_frag_v<32>(V0);
-      vh[3] = tr_frag_v<32>(V1);
-      if (key0 + TROWS - 1 > wave_qmin) {  // diagonal tile (wave-uniform)
-        const int d = q - key0 - 4 * hh;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int c = (r & 3) + 8 * (r >> 2);
-          s0[r] = c > d ? -INFINITY : s0[r];
-          s1[r] = c + 32 > d ? -INFINITY : s1[r];
-        }
-      }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-      tmax = xhalf_max(tmax);
-      if (t == 0) {
-        m = tmax;
-        s0 -= tmax;
-        s1 -= tmax;
-        if (act1) {
-          n0 -= tmax;
-          n1 -= tmax;
-        }
-        nm16 = bcast16(-m);
-      } else if (__any(tmax > 8.f)) {
-        const float dd = tmax > 8.f ? tmax : 0.f;
-        const float alpha = __builtin_amdgcn_exp2f(-dd);
-        m += dd;
-        l *= alpha;
-        o0 *= alpha;
-        o1 *= alpha;
-        s0 -= dd;
-        s1 -= dd;
-        if (act1) {
-          n0 -= dd;
-          n1 -= dd;
-        }
-        nm16 = bcast16(-m);
-      }
-      f32x2 ls2 = {0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
-        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
-        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
-      }
-      l += ls2[0] + ls2[1];
-      bf16x8 vb[4];
-      vb[0] = tr_frag_v<16>(V0);
-      vb[1] = tr_frag_v<16>(V1);
-      vb[2] = tr_frag_v<48>(V0);
-      vb[3] = tr_frag_v<48>(V1);
-      const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
-      o0 = mfma(vh[0], p0, o0);
-      o1 = mfma(vh[1], p0, o1);
-      o0 = mfma(vh[2], p1, o0);
-      o1 = mfma(vh[3], p1, o1);
-      const bf16x8 r0 = pack8(s0, 1), r1 = pack8(s1, 1);
-      o0 = mfma(vb[0], r0, o0);
-      o1 = mfma(vb[1], r0, o1);
-      o0 = mfma(vb[2], r1, o0);
-      o1 = mfma(vb[3], r1, o1);
-    }
-    if (ldk) stage_store(sk, kslot(t + 2), tid);
-    if (ldv) stage_store_v(sv, vslot(t + 1), tid);
-    __syncthreads();
-    s0 = n0;
-    s1 = n1;
   }
   const float lt = xhalf_sum(l);
   const float inv = 1.f / lt;
@@ -1348,8 +1177,6 @@ int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, f
   const int grid = B * H * (S / 128);
   if (variant == 4)
     attn_fwd_d64<0, 1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else if (variant == 8)
-    attn_fwd_pipe_d64<<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   else if (attn_prio() & 1)
     attn_fwd_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   else

@@ -266,62 +266,15 @@ def _transposable(w) -> bool:
             and w.shape[1] % 64 == 0 and w.is_contiguous())
 
 
-# Wᵀ of the step's weights, computed ahead on a side stream (prefetch_transposes):
-# id(w) → [w, persistent Wᵀ buffer, event, waited]
-_WT: dict = {}
-_WT_STREAM: dict = {}
+def transpose(w, out=None):
+    """Contiguous Wᵀ of a 2-D tensor (HIP kernel for bf16 with 64-multiple dims).
 
-
-def prefetch_transposes(weights):
-    """Compute every weight's Wᵀ for this step's input-gradient GEMMs on a side
-    HIP stream, so the 97 memory-bound transposes of a GPT-2-medium step run
-    under the forward pass's GEMMs (one workgroup per CU at 131 KiB of LDS and
-    ≈ 410 registers per lane leaves room for the 9 KiB / few-register transpose
-    workgroups on every CU) instead of between the backward's kernels.
-
-    Call after the weights' last update and before the forward (the trainer
-    does, every step); ``release_transposes`` after the optimizer step drops
-    the entries, so a Wᵀ never outlives the weights it was made from."""
-    ws = [w for w in weights if _transposable(w)]
-    if not ws:
-        return
-    m = _native.require_hip()
-    dev = ws[0].device
-    side = _WT_STREAM.get(dev)
-    if side is None:
-        side = _WT_STREAM[dev] = torch.cuda.Stream(device=dev)
-    main = torch.cuda.current_stream(dev)
-    side.wait_stream(main)  # the optimizer's update of the weights
-    with torch.cuda.stream(side):
-        for w in ws:
-            e = _WT.get(id(w))
-            buf = e[1] if e is not None and e[0] is w else torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=dev)
-            m.transpose(w, buf)
-            _WT[id(w)] = [w, buf, None, False]
-        ev = torch.cuda.Event()
-        ev.record(side)
-    for w in ws:
-        _WT[id(w)][2] = ev
-
-
-def release_transposes():
-    """Invalidate the prefetched Wᵀ (their weights are about to change); the
-    buffers stay allocated for the next step's prefetch."""
-    for e in _WT.values():
-        e[2] = None
-        e[3] = False
-
-
-def transpose(w):
-    """Contiguous Wᵀ of a 2-D tensor (HIP kernel for bf16 with 64-multiple dims);
-    the side-stream prefetched copy when this step has one."""
-    e = _WT.get(id(w))
-    if e is not None and e[0] is w and e[2] is not None:
-        if not e[3]:
-            torch.cuda.current_stream(w.device).wait_event(e[2])
-            e[3] = True
-        return e[1]
+    (Measured, round 3: the step's 97 transposes prefetched on a side stream
+    under the forward GEMMs made the step 1 ms slower — 148.2 vs 147.2 ms,
+    profiles/r3_attention_variants_a5.md — so they stay in-stream.)"""
     if _transposable(w):
+        if out is not None:
+            return _native.require_hip().transpose(w, out)
         return _native.require_hip().transpose(w)
     return w.t().contiguous()
 

@@ -14,7 +14,6 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-from . import ops
 from .models.gpt2 import GPT2, GPT2Config
 from .ops.optim import FlatAdamW
 from .parallel.ddp import BucketedDDP
@@ -99,9 +98,6 @@ class GPT2Trainer:
         self.flat = FlatParams(model, dtype=dtype, device=self.device, bucket_bytes=bucket_bytes, late=("wte",))
         self.ddp = BucketedDDP(self.flat)
         self.opt = FlatAdamW(self.flat, lr=lr)
-        # 2-D weights whose Wᵀ the backward needs (PDO_WT_PREFETCH=0: transpose in-stream)
-        self._wt = ([p for p in model.parameters() if p.dim() == 2 and p is not model.wpe]
-                    if self.device.type == "cuda" and os.environ.get("PDO_WT_PREFETCH", "1") != "0" else [])
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + (dist.get_rank() if dist.is_initialized() else 0))
 
@@ -119,16 +115,12 @@ class GPT2Trainer:
             idx, tgt = self.batch()
         self.flat.zero_grad()
         self.ddp.prepare()
-        if self._wt:
-            ops.prefetch_transposes(self._wt)  # Wᵀ for the backward's dX GEMMs, under the forward
         with trace.range("forward"):
             loss = self.model(idx, tgt)
         with trace.range("backward"):
             loss.backward()
         with trace.range("allreduce_drain"):
             self.ddp.finish()
-        if self._wt:
-            ops.release_transposes()
         with trace.range("optimizer"):
             self.opt.step(grad_scale=self.ddp.grad_scale)
         return loss

@@ -68,28 +68,3 @@ def test_resnet_arena_grads_match_autograd(cuda):
         err = (pa.grad.float() - pb.grad.float()).norm() / (pb.grad.float().norm() + 1e-12)
         assert err < 1e-5, f"{n}: {err}"
 
-
-@pytest.mark.gpu
-def test_gpt2_trainer_transpose_prefetch_bitwise(cuda, monkeypatch):
-    """Wᵀ prefetched on a side stream under the forward (ops.prefetch_transposes,
-    the trainer's default) gives the same loss, gradients and updated weights,
-    bit for bit, as the in-stream transposes (PDO_WT_PREFETCH=0), over 3 steps."""
-    from paddle_operator_amd import ops
-    from paddle_operator_amd.models.gpt2 import GPT2Config
-    from paddle_operator_amd.train import GPT2Trainer
-
-    cfg = GPT2Config.named("gpt2-smoke")
-    runs = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("PDO_WT_PREFETCH", flag)
-        t = GPT2Trainer(cfg, micro_batch=4, seq_len=512, device="cuda:0", seed=3)
-        assert bool(t._wt) == (flag == "1")
-        losses = [t.step().item() for _ in range(3)]
-        torch.cuda.synchronize()
-        runs[flag] = (losses, t.flat.grads.clone(), t.flat.params.clone())
-        del t
-    assert runs["1"][0] == runs["0"][0]
-    assert torch.equal(runs["1"][1], runs["0"][1])
-    assert torch.equal(runs["1"][2], runs["0"][2])
-    # after the optimizer step no prefetched Wᵀ is live: a stray transpose recomputes
-    assert all(e[2] is None for e in ops._WT.values())
