@@ -3,8 +3,6 @@
 // One pass: bf16 grad → ×(grad_scale · clip_coef) → fp32 moments/master →
 // bf16 compute copy.  The clip coefficient is read from device memory
 // (written by `sumsq`), so clipping costs no host synchronisation.
-#include <stdlib.h>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -32,10 +30,6 @@ __global__ __launch_bounds__(1024) void sumsq_final_kernel(const float* __restri
   if (threadIdx.x == 0) out[0] = s * scale2;
 }
 
-// FAST: the update's division as a reciprocal (v_rcp_f32, ≤ 1 ulp) instead of the
-// IEEE division sequence, and the fp32 state (master / moments, touched once per
-// step) written with non-temporal stores
-template <bool FAST>
 __global__ __launch_bounds__(256) void adamw_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
                                                     float* __restrict__ master, float* __restrict__ m1,
                                                     float* __restrict__ m2, const float* __restrict__ decay_chunks,
@@ -62,26 +56,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16* __restrict__ p, const 
     const float shrink = 1.f - lr * wd * dec;
     f32x8 upd;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if constexpr (FAST) upd[j] = (a[j] * inv_bc1) * __builtin_amdgcn_rcpf(sqrtf(v[j]) * inv_sqrt_bc2 + eps);
-      else upd[j] = (a[j] * inv_bc1) / (sqrtf(v[j]) * inv_sqrt_bc2 + eps);
-    }
+    for (int j = 0; j < 8; ++j) upd[j] = (a[j] * inv_bc1) / (sqrtf(v[j]) * inv_sqrt_bc2 + eps);
     w = w * shrink - lr * upd;
-    if constexpr (FAST) {
-      __builtin_nontemporal_store(f32x4{w[0], w[1], w[2], w[3]}, mp);
-      __builtin_nontemporal_store(f32x4{w[4], w[5], w[6], w[7]}, mp + 1);
-      __builtin_nontemporal_store(f32x4{a[0], a[1], a[2], a[3]}, ap);
-      __builtin_nontemporal_store(f32x4{a[4], a[5], a[6], a[7]}, ap + 1);
-      __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, vp);
-      __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, vp + 1);
-    } else {
-      mp[0] = f32x4{w[0], w[1], w[2], w[3]};
-      mp[1] = f32x4{w[4], w[5], w[6], w[7]};
-      ap[0] = f32x4{a[0], a[1], a[2], a[3]};
-      ap[1] = f32x4{a[4], a[5], a[6], a[7]};
-      vp[0] = f32x4{v[0], v[1], v[2], v[3]};
-      vp[1] = f32x4{v[4], v[5], v[6], v[7]};
-    }
+    mp[0] = f32x4{w[0], w[1], w[2], w[3]};
+    mp[1] = f32x4{w[4], w[5], w[6], w[7]};
+    ap[0] = f32x4{a[0], a[1], a[2], a[3]};
+    ap[1] = f32x4{a[4], a[5], a[6], a[7]};
+    vp[0] = f32x4{v[0], v[1], v[2], v[3]};
+    vp[1] = f32x4{v[4], v[5], v[6], v[7]};
     reinterpret_cast<bf16x8*>(p)[i] = to_bf16(w);
   }
 }
@@ -100,16 +82,8 @@ int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, cons
                float bc2, float grad_scale, float clip, hipStream_t st) {
   if (n % 1024) return -2;
   const long long nvec = n / 8;
-  static const bool fast = [] {
-    const char* e = getenv("PDO_ADAMW_FAST");
-    return e && *e == '1';
-  }();
-  if (fast)
-    adamw_kernel<true><<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr,
-                                                               b1, b2, eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
-  else
-    adamw_kernel<false><<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr,
-                                                                b1, b2, eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
+  adamw_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr, b1, b2,
+                                                        eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
   return 0;
 }
 

@@ -10,8 +10,6 @@
 // registers, dlogits written in the forward — 4.6 ms vs these two passes'
 // 3.6 ms at [65536, 50304]: with ≤ 1 resident 50k-column row per CU the load,
 // reduce and store phases serialise.)
-#include <stdlib.h>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -94,7 +92,6 @@ __global__ __launch_bounds__(1024) void xent_mean_kernel(const float* __restrict
   }
 }
 
-template <bool NT>
 __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                        const float* __restrict__ lse, const float* __restrict__ dloss,
                                                        const float* __restrict__ stats, bf16* __restrict__ dlogits,
@@ -118,10 +115,7 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16* __restrict__ 
       if (c == t) p -= 1.f;
       o[j] = p * scale;
     }
-    // NT: non-temporal stores — the 6.6 GB dlogits stream cannot stay in L2 / MALL
-    // anyway and would evict the LM-head GEMMs' operand panels
-    if constexpr (NT) __builtin_nontemporal_store(to_bf16(o), dv + i);
-    else dv[i] = to_bf16(o);
+    dv[i] = to_bf16(o);
   };
   // four 16-B loads in flight per thread before the first use: one per thread
   // left the row pass latency-bound (≈ 5.2 TB/s for the read + write stream)
@@ -147,12 +141,7 @@ int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse
 int xent_bwd(const bf16* logits, const int64_t* tgt, const float* lse, const float* dloss, const float* stats,
              bf16* dlogits, int N, int Vp, int V, hipStream_t st) {
   if (Vp % 8) return -2;
-  static const bool nt = [] {
-    const char* e = getenv("PDO_XENT_NT");
-    return e && *e == '1';
-  }();
-  if (nt) xent_bwd_kernel<true><<<N, 256, 0, st>>>(logits, tgt, lse, dloss, stats, dlogits, Vp, V);
-  else xent_bwd_kernel<false><<<N, 256, 0, st>>>(logits, tgt, lse, dloss, stats, dlogits, Vp, V);
+  xent_bwd_kernel<<<N, 256, 0, st>>>(logits, tgt, lse, dloss, stats, dlogits, Vp, V);
   return 0;
 }
 
