@@ -129,74 +129,6 @@ __device__ __forceinline__ f32x2 gelu_sig_grad2(f32x2 x, f32x2 m1) {
   return pk_fma(sg, q, sg);
 }
 
-// GELU / GELU′ without transcendentals, for the GEMM epilogues (PDO_GELU_POLY):
-// h(x) = GELU(x) − x/2 is even, GELU′(x) − 1/2 odd, so on |x| ≤ 4 both are a
-// degree-9 polynomial in u = x² (Chebyshev fit of the tanh form, float32
-// Horner: |error| ≤ 4.3e-5 for GELU, ≤ 2.5e-4 for GELU′, far below a bf16 ulp
-// of the outputs); past ±4 GELU is x / 0 and GELU′ 1 / 0 to within 7e-5 / 3e-4.
-// 12 packed fp32 ops + 4 per-value min/max/med3 per pair, against 4
-// quarter-rate transcendentals + 5 packed ops (gelu_sig2) — the epilogue runs
-// with the matrix pipe idle, so its instruction count is the epilogue's time.
-// P's constant term carries −4: GELU = x/2 + P(u) + max(x, 4) for every x.
-constexpr float GPR = 4.f;
-__device__ __forceinline__ f32x2 med3_2(f32x2 x) {
-  return f32x2{__builtin_amdgcn_fmed3f(x[0], -GPR, GPR), __builtin_amdgcn_fmed3f(x[1], -GPR, GPR)};
-}
-__device__ __forceinline__ f32x2 gelu_poly2(f32x2 x) {
-  const f32x2 xc = med3_2(x);
-  const f32x2 u = xc * xc;
-  f32x2 p = f32x2(8.466256862e-11f);
-  p = pk_fma(p, u, f32x2(-7.414315828e-09f));
-  p = pk_fma(p, u, f32x2(2.889336201e-07f));
-  p = pk_fma(p, u, f32x2(-6.686887900e-06f));
-  p = pk_fma(p, u, f32x2(1.040399438e-04f));
-  p = pk_fma(p, u, f32x2(-1.172441640e-03f));
-  p = pk_fma(p, u, f32x2(1.002618670e-02f));
-  p = pk_fma(p, u, f32x2(-6.660894305e-02f));
-  p = pk_fma(p, u, f32x2(3.988460302e-01f));
-  p = pk_fma(p, u, f32x2(-3.999992847e+00f));
-  return pk_fma(xc, f32x2(0.5f), p) + f32x2{fmaxf(x[0], GPR), fmaxf(x[1], GPR)};
-}
-__device__ __forceinline__ f32x2 gelu_poly_grad2(f32x2 x) {
-  const f32x2 xc = med3_2(x);
-  const f32x2 u = xc * xc;
-  f32x2 q = f32x2(-8.573315669e-11f);
-  q = pk_fma(q, u, f32x2(7.589871842e-09f));
-  q = pk_fma(q, u, f32x2(-2.986855066e-07f));
-  q = pk_fma(q, u, f32x2(6.956192010e-06f));
-  q = pk_fma(q, u, f32x2(-1.080884613e-04f));
-  q = pk_fma(q, u, f32x2(1.200574683e-03f));
-  q = pk_fma(q, u, f32x2(-9.917682968e-03f));
-  q = pk_fma(q, u, f32x2(6.113014743e-02f));
-  q = pk_fma(q, u, f32x2(-2.672294974e-01f));
-  q = pk_fma(q, u, f32x2(7.978803515e-01f));
-  return pk_fma(xc, q, f32x2(0.5f));
-}
-// the same sequences on one value (bit-identical to a lane of the pair forms:
-// packed fp32 fma / mul round as the scalar ones) — the standalone bias-GELU kernels
-__device__ __forceinline__ float gelu_poly(float x) { return gelu_poly2(f32x2{x, x})[0]; }
-__device__ __forceinline__ float gelu_poly_grad(float x) { return gelu_poly_grad2(f32x2{x, x})[0]; }
-#ifndef PDO_GELU_POLY
-#define PDO_GELU_POLY 1
-#endif
-// the GEMM epilogues' GELU / GELU′ on a pair (m1: gelu_sig_grad2's (-1, -1))
-__device__ __forceinline__ f32x2 epi_gelu2(f32x2 x) {
-  if constexpr (PDO_GELU_POLY) return gelu_poly2(x);
-  else return gelu_sig2(x);
-}
-__device__ __forceinline__ f32x2 epi_gelu_grad2(f32x2 x, f32x2 m1) {
-  if constexpr (PDO_GELU_POLY) return gelu_poly_grad2(x);
-  else return gelu_sig_grad2(x, m1);
-}
-__device__ __forceinline__ float epi_gelu(float x) {
-  if constexpr (PDO_GELU_POLY) return gelu_poly(x);
-  else return gelu_sig(x);
-}
-__device__ __forceinline__ float epi_gelu_grad(float x) {
-  if constexpr (PDO_GELU_POLY) return gelu_poly_grad(x);
-  else return gelu_sig_grad(x);
-}
-
 // number of workgroups for a grid-stride memory-bound kernel (256 CUs × 8)
 inline int stream_grid(long long work_items, int per_block) {
   long long g = (work_items + per_block - 1) / per_block;

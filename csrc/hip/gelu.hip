@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16* __restri
         const f32x8 v = to_f32(in[u]) + bb;
         f32x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = epi_gelu(v[j]);
+        for (int j = 0; j < 8; ++j) o[j] = gelu_sig(v[j]);
         yv[i + u * stride] = to_bf16(o);
       }
     }
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16* __restri
           const f32x8 v = to_f32(xx[u]) + bb;
           f32x8 o;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = d[j] * epi_gelu_grad(v[j]);
+          for (int j = 0; j < 8; ++j) o[j] = d[j] * gelu_sig_grad(v[j]);
           dxv[(size_t)(r + u) * F8 + c8] = to_bf16(o);
           acc += o;
         }

@@ -201,14 +201,14 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
       const f32x8 x = to_f32(v) + bv8;
       f32x8 y;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = epi_gelu(x[e]);
+      for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
       *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
     } else {
       const f32x8 x = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n)) + bv8;
       const f32x8 dy = to_f32(v);
       f32x8 d;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] = dy[e] * epi_gelu_grad(x[e]);
+      for (int e = 0; e < 8; ++e) d[e] = dy[e] * gelu_sig_grad(x[e]);
       colp += d;
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(d);
     }

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
             f32x8 y;
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
-              const f32x2 gg = epi_gelu2(f32x2{x[q], x[q + 1]});
+              const f32x2 gg = gelu_sig2(f32x2{x[q], x[q + 1]});
               y[q] = gg[0];
               y[q + 1] = gg[1];
             }
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
             f32x8 d;
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
-              const f32x2 gg = f32x2{dy[q], dy[q + 1]} * epi_gelu_grad2(f32x2{x[q], x[q + 1]}, m1);
+              const f32x2 gg = f32x2{dy[q], dy[q + 1]} * gelu_sig_grad2(f32x2{x[q], x[q + 1]}, m1);
               d[q] = gg[0];
               d[q + 1] = gg[1];
             }
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
             f32x8 y;
 #pragma unroll
             for (int e = 0; e < 8; e += 2) {
-              const f32x2 g = epi_gelu2(f32x2{x[e], x[e + 1]});
+              const f32x2 g = gelu_sig2(f32x2{x[e], x[e + 1]});
               y[e] = g[0];
               y[e + 1] = g[1];
             }
@@ -722,7 +722,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
             f32x8 d;
 #pragma unroll
             for (int e = 0; e < 8; e += 2) {
-              const f32x2 g = f32x2{dy[e], dy[e + 1]} * epi_gelu_grad2(f32x2{x[e], x[e + 1]}, m1);
+              const f32x2 g = f32x2{dy[e], dy[e + 1]} * gelu_sig_grad2(f32x2{x[e], x[e + 1]}, m1);
               d[e] = g[0];
               d[e + 1] = g[1];
             }
@@ -809,7 +809,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       f32x8 y;
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {  // packed pairs (common.h)
-        const f32x2 g = epi_gelu2(f32x2{x[e], x[e + 1]});
+        const f32x2 g = gelu_sig2(f32x2{x[e], x[e + 1]});
         y[e] = g[0];
         y[e + 1] = g[1];
       }
@@ -820,7 +820,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       f32x8 d;
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
-        const f32x2 g = f32x2{dy[e], dy[e + 1]} * epi_gelu_grad2(f32x2{x[e], x[e + 1]}, m1);
+        const f32x2 g = f32x2{dy[e], dy[e + 1]} * gelu_sig_grad2(f32x2{x[e], x[e + 1]}, m1);
         d[e] = g[0];
         d[e + 1] = g[1];
       }
