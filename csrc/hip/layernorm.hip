@@ -6,8 +6,6 @@
 // computes dx per row and accumulates dgamma/dbeta per lane in registers over
 // a grid-stride row loop; the 4 waves of a block combine through LDS and the
 // per-block partials are summed by the two-level `colsum` (reduce.hip).
-#include <stdlib.h>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -79,11 +77,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* __restrict__ x,
 
 // NA = 2: partials (dgamma, dbeta); NA = 3: + colsum(dx) — the gradient of a
 // bias folded into the residual branch (h = x + r + rbias).
-// RECOMP: keep the row's raw bf16 operands instead of its fp32 x̂ / g / dres
-// vectors and recompute them in the output pass (-24 VGPRs: 182 → ≤ 168, three
-// waves per SIMD instead of two for the memory stream)
-template <int VPL, bool ADD, int NA, bool RECOMP = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RECOMP ? 3 : 1))) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+template <int VPL, bool ADD, int NA>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                      const bf16* __restrict__ w, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const bf16* __restrict__ dres,
                                                      bf16* __restrict__ dx, float* __restrict__ part, int N, int C) {
@@ -123,49 +118,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RECOMP ? 3 
   for (; row < N; row += nw) {
     const size_t base = (size_t)row * C;
     const float mu = mean[row], rs = rstd[row];
-    float s1 = 0.f, s2 = 0.f;
-    if constexpr (RECOMP) {
-      bf16x8 cd[VPL], cx[VPL], cr[VPL];
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        cd[i] = nd[i];
-        cx[i] = nx[i];
-        if (ADD) cr[i] = nr[i];
-      }
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        const int c8 = lane + i * 64;
-        if (c8 < C8) {
-          const f32x8 d = to_f32(cd[i]);
-          const f32x8 xh = (to_f32(cx[i]) - mu) * rs;
-          const f32x8 g = d * wv[i];
-          adw[i] += d * xh;
-          adb[i] += d;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            s1 += g[j];
-            s2 += g[j] * xh[j];
-          }
-        }
-      }
-      if (row + nw < N) fetch(row + nw);
-      s1 = wave_sum(s1) * inv_c;
-      s2 = wave_sum(s2) * inv_c;
-#pragma unroll
-      for (int i = 0; i < VPL; ++i) {
-        const int c8 = lane + i * 64;
-        if (c8 < C8) {
-          const f32x8 xh = (to_f32(cx[i]) - mu) * rs;
-          const f32x8 g = to_f32(cd[i]) * wv[i];
-          f32x8 o = (g - s1 - xh * s2) * rs;
-          if (ADD) o += to_f32(cr[i]);
-          if (NA == 3) adx[i] += o;
-          reinterpret_cast<bf16x8*>(dx + base)[c8] = to_bf16(o);
-        }
-      }
-      continue;
-    }
     f32x8 xh[VPL], g[VPL], rr[VPL];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c8 = lane + i * 64;
@@ -259,21 +213,11 @@ int layernorm_fwd(const bf16* x, const bf16* r, const bf16* rb, const bf16* w, c
   return 0;
 }
 
-static bool ln_bwd_recomp() {
-  static const bool r = [] {
-    const char* e = getenv("PDO_LN_BWD_RECOMP");
-    return e && *e == '1';
-  }();
-  return r;
-}
-
 int layernorm_bwd_grid(int N) {
   // one resident round: ≤ 2 waves/SIMD at this kernel's register count
-  // (4 waves per block, 256 CUs × 4 SIMDs × 2 / 4 = 512 blocks; 3 waves: 768
-  // for the RECOMP form), ≥ 4 rows per wave
+  // (4 waves per block, 256 CUs × 4 SIMDs × 2 / 4 = 512 blocks), ≥ 4 rows per wave
   int g = (N + 15) / 16;
-  const int cap = ln_bwd_recomp() ? 768 : 512;
-  if (g > cap) g = cap;
+  if (g > 512) g = 512;
   if (g < 1) g = 1;
   return g;
 }
@@ -290,9 +234,7 @@ int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mea
   const int vpl = vpl_for(C);
   if (vpl > 4) return -3;  // register/LDS budget of the in-block combine
   const int NA = rbias ? 3 : 2;
-  if (rbias && ln_bwd_recomp()) {
-    LN_DISPATCH(vpl, ln_bwd_kernel<V, true, 3, true><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
-  } else if (rbias) {
+  if (rbias) {
     LN_DISPATCH(vpl, ln_bwd_kernel<V, true, 3><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
   } else if (dres) {
     LN_DISPATCH(vpl, ln_bwd_kernel<V, true, 2><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
