@@ -194,6 +194,18 @@ at::Tensor xent_bwd(at::Tensor logits, at::Tensor tgt, at::Tensor lse, at::Tenso
   return out;
 }
 
+// logits → dlogits in place (for dloss = 1); returns the mean loss over valid targets
+at::Tensor xent_fused(at::Tensor logits, at::Tensor tgt, at::Tensor inv_cnt, int64_t V) {
+  CHECK_IN(logits); CHECK_IN(tgt); CHECK_IN(inv_cnt); CHECK_BF16(logits); CHECK_I64(tgt); CHECK_F32(inv_cnt);
+  TORCH_CHECK(logits.dim() == 2 && tgt.numel() == logits.size(0) && V <= logits.size(1) && inv_cnt.numel() == 1);
+  const int N = logits.size(0), Vp = logits.size(1);
+  auto row_loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  auto loss = at::empty({}, logits.options().dtype(at::kFloat));
+  CHECK_RC(pdo::xent_fused(bp(logits), tgt.data_ptr<int64_t>(), fp(inv_cnt), fp(row_loss), fp(loss), N, Vp, (int)V,
+                           cur_stream()), "xent_fused");
+  return loss;
+}
+
 // ---------------------------------------------------------------- embedding
 at::Tensor embed_fwd(at::Tensor idx, at::Tensor wte, at::Tensor wpe) {
   CHECK_IN(idx); CHECK_IN(wte); CHECK_IN(wpe); CHECK_I64(idx); CHECK_BF16(wte); CHECK_BF16(wpe);
@@ -678,6 +690,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out") = py::none());
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("xent_fused", &xent_fused);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("sumsq", &sumsq);

@@ -97,6 +97,9 @@ int bias_gelu_bwd(const bf16* dy, const bf16* x, const bf16* b, bf16* dx, float*
 // xent.hip
 int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,
              hipStream_t st);
+// xent.hip: stats + dlogits (dloss = 1, scaled by inv_cnt) in place, one kernel; loss = mean over valid targets
+int xent_fused(bf16* logits, const int64_t* tgt, const float* inv_cnt, float* row_loss, float* loss, int N, int Vp,
+               int V, hipStream_t st);
 int xent_bwd(const bf16* logits, const int64_t* tgt, const float* lse, const float* dloss, const float* stats,
              bf16* dlogits, int N, int Vp, int V, hipStream_t st);
 

@@ -130,6 +130,115 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16* __restrict__ 
   for (; i < nv; i += 256) grad(lv[i], i);
 }
 
+// Forward statistics AND dlogits in one kernel, for dloss = 1 (ops._LMHeadXentFn
+// scales the downstream dX / dW by the real dloss): per row, pass 1 streams the
+// logits once for (max, sum-exp) → lse and the row loss, pass 2 streams the same
+// row again — from the XCD's L2 / the MALL, the 100 KB row was read microseconds
+// before — and writes (softmax − onehot) / count in place.  HBM sees one read and
+// one write of [N, Vp] instead of the two kernels' two reads and one write.
+// inv_cnt: 1 / (number of valid targets), precomputed on device.
+__global__ __launch_bounds__(256) void xent_fused_kernel(bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                         const float* __restrict__ inv_cnt, float* __restrict__ row_loss,
+                                                         int Vp, int V) {
+  __shared__ float red_m[4], red_s[4], lse_sh;
+  const int row = blockIdx.x;
+  const bf16x8* lv = reinterpret_cast<const bf16x8*>(logits + (size_t)row * Vp);
+  const int nv = Vp >> 3;
+  float m = -INFINITY, s = 0.f;
+  auto acc = [&](bf16x8 raw, int i) {
+    f32x8 v = to_f32(raw);
+    const int c0 = i * 8;
+    float vm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c0 + j >= V) v[j] = -INFINITY;
+      vm = fmaxf(vm, v[j]);
+    }
+    if (vm > m) {
+      s *= __expf(m - vm);
+      m = vm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(v[j] - m);
+  };
+  int i = threadIdx.x;
+  for (; i + 3 * 256 < nv; i += 4 * 256) {
+    const bf16x8 a0 = lv[i], a1 = lv[i + 256], a2 = lv[i + 512], a3 = lv[i + 768];
+    acc(a0, i);
+    acc(a1, i + 256);
+    acc(a2, i + 512);
+    acc(a3, i + 768);
+  }
+  for (; i < nv; i += 256) acc(lv[i], i);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red_m[w] = m;
+    red_s[w] = s;
+  }
+  __syncthreads();
+  const int64_t t = tgt[row];
+  if (threadIdx.x == 0) {
+    float M = red_m[0];
+    for (int k = 1; k < 4; ++k) M = fmaxf(M, red_m[k]);
+    float S = 0.f;
+    for (int k = 0; k < 4; ++k) S += red_m[k] == -INFINITY ? 0.f : red_s[k] * __expf(red_m[k] - M);
+    const float lse = M + __logf(S);
+    lse_sh = lse;
+    row_loss[row] = (t >= 0 && t < V) ? lse - (float)logits[(size_t)row * Vp + t] : 0.f;
+  }
+  __syncthreads();  // also orders the target logit's read before pass 2 overwrites it
+  const float L = lse_sh;
+  const float scale = (t >= 0 && t < V) ? inv_cnt[0] : 0.f;
+  bf16x8* dv = reinterpret_cast<bf16x8*>(logits + (size_t)row * Vp);
+  auto grad = [&](bf16x8 raw, int k) {
+    const f32x8 v = to_f32(raw);
+    const int c0 = k * 8;
+    f32x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      float p = c < V ? __expf(v[j] - L) : 0.f;
+      if (c == t) p -= 1.f;
+      o[j] = p * scale;
+    }
+    dv[k] = to_bf16(o);
+  };
+  i = threadIdx.x;
+  for (; i + 3 * 256 < nv; i += 4 * 256) {
+    const bf16x8 a0 = lv[i], a1 = lv[i + 256], a2 = lv[i + 512], a3 = lv[i + 768];
+    grad(a0, i);
+    grad(a1, i + 256);
+    grad(a2, i + 512);
+    grad(a3, i + 768);
+  }
+  for (; i < nv; i += 256) grad(lv[i], i);
+}
+
+// loss = Σ row_loss · inv_cnt
+__global__ __launch_bounds__(1024) void xent_sum_kernel(const float* __restrict__ row_loss, int N,
+                                                        const float* __restrict__ inv_cnt, float* __restrict__ loss) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < N; i += 1024) s += row_loss[i];
+  s = block_sum<16>(s, red);
+  if (threadIdx.x == 0) loss[0] = s * inv_cnt[0];
+}
+
+int xent_fused(bf16* logits, const int64_t* tgt, const float* inv_cnt, float* row_loss, float* loss, int N, int Vp,
+               int V, hipStream_t st) {
+  if (Vp % 8) return -2;
+  xent_fused_kernel<<<N, 256, 0, st>>>(logits, tgt, inv_cnt, row_loss, Vp, V);
+  xent_sum_kernel<<<1, 1024, 0, st>>>(row_loss, N, inv_cnt, loss);
+  return 0;
+}
+
 int xent_fwd(const bf16* logits, const int64_t* tgt, float* row_loss, float* lse, float* stats, int N, int Vp, int V,
              hipStream_t st) {
   if (Vp % 8) return -2;

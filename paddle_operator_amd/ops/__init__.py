@@ -729,6 +729,8 @@ class _LMHeadXentFn(torch.autograd.Function):
         valid = ((t >= 0) & (t < vocab)).sum().float()
         stats = torch.stack([torch.zeros_like(valid), valid])  # xent_bwd reads the count from stats[1]
         ones = torch.ones(1, device=h.device, dtype=torch.float32)
+        fused = _XENT_FUSED[0]
+        inv_cnt = (1.0 / valid.clamp(min=1.0)).reshape(1)
         logits = torch.empty(chunk, Vp, device=h.device, dtype=h.dtype)
         dh = torch.empty_like(h2)
         dw = torch.empty(Vp, C, device=h.device, dtype=h.dtype)
@@ -737,9 +739,15 @@ class _LMHeadXentFn(torch.autograd.Function):
             hc, tc = h2[c0:c0 + chunk], t[c0:c0 + chunk]
             lg = logits[:hc.shape[0]]
             m.gemm_nt(hc, w, None, lg)
-            _, lse, st = m.xent_fwd(lg, tc, vocab)  # st = (chunk mean loss, chunk valid count)
-            loss_sum += st[0] * st[1]
-            dl = m.xent_bwd(lg, tc, lse, ones, stats, vocab, True)  # (softmax − onehot) / count, in place
+            if fused:
+                # one kernel: row statistics, then (softmax − onehot) / count in place
+                # (the chunk's loss already divided by the total count)
+                loss_sum += m.xent_fused(lg, tc, inv_cnt, vocab)
+                dl = lg
+            else:
+                _, lse, st = m.xent_fwd(lg, tc, vocab)  # st = (chunk mean loss, chunk valid count)
+                loss_sum += st[0] * st[1]
+                dl = m.xent_bwd(lg, tc, lse, ones, stats, vocab, True)  # (softmax − onehot) / count, in place
             m.gemm_nt(dl, wt, None, dh[c0:c0 + chunk])
             if not m.gemm_dw(dl, hc, dw, c0 > 0):
                 if c0 == 0:
@@ -748,7 +756,7 @@ class _LMHeadXentFn(torch.autograd.Function):
                     dw.addmm_(dl.t(), hc)
         ctx.save_for_backward(dh, dw)
         ctx.shape = h.shape
-        return loss_sum / valid
+        return loss_sum if fused else loss_sum / valid
 
     @staticmethod
     def backward(ctx, dloss):
@@ -757,15 +765,20 @@ class _LMHeadXentFn(torch.autograd.Function):
         return (dh * d).view(ctx.shape), dw * d, None, None, None
 
 
-# PDO_LM_CHUNK=tokens: the chunked LM head + cross-entropy (_LMHeadXentFn); 0 = the
-# full-logits path (ops.linear + ops.cross_entropy)
+# PDO_LM_CHUNK=tokens: the chunked LM head + cross-entropy (_LMHeadXentFn); -1 = one
+# chunk of every token; 0 = the full-logits path (ops.linear + ops.cross_entropy)
 _LM_CHUNK = [int(os.environ.get("PDO_LM_CHUNK", "0"))]
+# the chunk path's cross-entropy as one kernel per row (xent_fused: statistics +
+# dlogits, one HBM read of the logits) instead of xent_fwd + xent_bwd (two)
+_XENT_FUSED = [os.environ.get("PDO_XENT_FUSED", "1") != "0"]
 
 
 def lm_head_xent(h, w, target, vocab: int):
     """Mean cross-entropy of the tied LM head h·Wᵀ over the first ``vocab`` columns."""
     N = h.numel() // h.shape[-1]
     ch = _LM_CHUNK[0]
+    if ch < 0:
+        ch = N
     if (ch and use_hip(h) and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and N % ch == 0
             and h.is_contiguous() and w.is_contiguous()
             and _native.require_hip().gemm_nt_supported(ch, w.shape[0], w.shape[1])

@@ -286,12 +286,16 @@ def test_cross_entropy(cuda):
     assert lh.grad[5].abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("N,C,V,chunk", [(1024, 256, 1000, 256), (2048, 512, 50257, 512)])
-def test_lm_head_xent_chunked(cuda, N, C, V, chunk):
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("N,C,V,chunk", [(1024, 256, 1000, 256), (2048, 512, 50257, 512), (2048, 512, 50257, -1)])
+def test_lm_head_xent_chunked(cuda, N, C, V, chunk, fused):
     """Chunked LM head + cross-entropy (ops._LMHeadXentFn) vs fp32 autograd:
     loss, dh and dW (incl. an ignored target, padded vocabulary rows, and the
-    50304-row half-width last tile at V = 50257)."""
+    50304-row half-width last tile at V = 50257); chunk -1 = one chunk of every
+    token; fused = the one-kernel statistics + dlogits pass (xent_fused)."""
     ops = _ops()
+    prev_f = ops._XENT_FUSED[0]
+    ops._XENT_FUSED[0] = fused
     Vp = (V + 127) // 128 * 128
     g = torch.Generator(device=cuda).manual_seed(9)
     h = torch.randn(N, C, device=cuda, generator=g).bfloat16()
@@ -308,6 +312,7 @@ def test_lm_head_xent_chunked(cuda, N, C, V, chunk):
         loss.backward(torch.tensor(1.5, device=cuda))
     finally:
         ops._LM_CHUNK[0] = prev
+        ops._XENT_FUSED[0] = prev_f
     hf = h.float().requires_grad_()
     wf = w.float().requires_grad_()
     lossf = torch.nn.functional.cross_entropy((hf @ wf.t())[:, :V], tgt, ignore_index=-100)
