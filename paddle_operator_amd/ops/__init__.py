@@ -765,9 +765,13 @@ class _LMHeadXentFn(torch.autograd.Function):
         return (dh * d).view(ctx.shape), dw * d, None, None, None
 
 
-# PDO_LM_CHUNK=tokens: the chunked LM head + cross-entropy (_LMHeadXentFn); -1 = one
-# chunk of every token; 0 = the full-logits path (ops.linear + ops.cross_entropy)
-_LM_CHUNK = [int(os.environ.get("PDO_LM_CHUNK", "0"))]
+# PDO_LM_CHUNK=tokens: the chunked LM head + cross-entropy (_LMHeadXentFn); -1
+# (default) = one chunk of every token: the LM head, the one-kernel cross-entropy
+# (xent_fused) and the dX / dW GEMMs in the forward, dloss applied to dX / dW in the
+# backward — 143.55 vs 144.04 ms/step against the separate linear + cross_entropy
+# Functions (0), whose statistics and dlogits passes read the 6.6 GB logits twice
+# (profiles/r3_xent_fused.md); 16384 caps the logits buffer at 1.6 GB (memory option)
+_LM_CHUNK = [int(os.environ.get("PDO_LM_CHUNK", "-1"))]
 # the chunk path's cross-entropy as one kernel per row (xent_fused: statistics +
 # dlogits, one HBM read of the logits) instead of xent_fwd + xent_bwd (two)
 _XENT_FUSED = [os.environ.get("PDO_XENT_FUSED", "1") != "0"]
