@@ -7,8 +7,6 @@
 // partial row; level 2 folds the ≤ a few dozen partial rows and writes bf16.
 // Enough workgroups to keep HBM busy (the single-level version with one
 // block per 64 columns was latency-bound at ~20 µs per call).
-#include <stdlib.h>
-
 #include "common.h"
 #include "kernels.h"
 
@@ -75,74 +73,6 @@ __global__ __launch_bounds__(512) void colsum_bf16_pass(const bf16* __restrict__
   }
 }
 
-// One launch for both levels: every block of a column stripe writes its partial
-// row, then counts itself in the stripe's arrival counter; the block that
-// arrives last folds the stripe's gs partial rows (in row order: the same sums
-// and rounding as the second colsum_f32_pass launch) and re-arms the counter.
-// The fence before the count makes the partial rows visible device-wide before
-// any block can observe the stripe complete.
-__global__ __launch_bounds__(512) void colsum_f32_fused(const float* __restrict__ in, int G, int C, int ld, int rpb,
-                                                        float* __restrict__ part, unsigned* __restrict__ arrivals,
-                                                        ColOut co) {
-  __shared__ f32x4 red[8][64];
-  __shared__ int last;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col = (blockIdx.x * 64 + lane) * 4;
-  const int r0 = blockIdx.y * rpb;
-  const int r1 = min(G, r0 + rpb);
-  f32x4 s = {0, 0, 0, 0};
-  if (col < C) {
-#pragma unroll 4
-    for (int r = r0 + w; r < r1; r += 8) s += *reinterpret_cast<const f32x4*>(in + (size_t)r * ld + col);
-  }
-  red[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && col < C) {
-    f32x4 t = red[0][lane];
-#pragma unroll
-    for (int i = 1; i < 8; ++i) t += red[i][lane];
-    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.y * C + col) = t;
-  }
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(arrivals + blockIdx.x, 1u) == gridDim.y - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (w == 0 && col < C) {
-    f32x4 t = {0, 0, 0, 0};
-    for (int r = 0; r < (int)gridDim.y; ++r) t += *reinterpret_cast<const f32x4*>(part + (size_t)r * C + col);
-    const int k = col / co.seg, c = col - k * co.seg;
-    bf16* dst = co.p[k] + c;
-    if (co.acc) {
-      const bf16x4 old = *reinterpret_cast<const bf16x4*>(dst);
-      t += f32x4{(float)old[0], (float)old[1], (float)old[2], (float)old[3]};
-    }
-    bf16x4 o = {(bf16)t[0], (bf16)t[1], (bf16)t[2], (bf16)t[3]};
-    *reinterpret_cast<bf16x4*>(dst) = o;
-  }
-  if (threadIdx.x == 0) arrivals[blockIdx.x] = 0u;  // re-armed for the next launch on this stream
-}
-
-// per-device arrival counters of colsum_f32_fused (zeroed once; each launch leaves them zero)
-static unsigned* colsum_arrivals() {
-  static unsigned* a = [] {
-    unsigned* p = nullptr;
-    if (hipMalloc(&p, 4096 * sizeof(unsigned)) != hipSuccess) return (unsigned*)nullptr;
-    if (hipMemset(p, 0, 4096 * sizeof(unsigned)) != hipSuccess) return (unsigned*)nullptr;
-    return p;
-  }();
-  return a;
-}
-
-static bool colsum_fused_on() {
-  static const bool on = [] {
-    const char* e = getenv("PDO_COLSUM_FUSED");
-    return e && *e == '1';
-  }();
-  return on;
-}
-
 int colsum_scratch_floats(int G, int C) { return ((G + RPB - 1) / RPB) * C; }
 
 // part: [G][ld] f32 (first C columns used).  scratch: colsum_scratch_floats(G, C)
@@ -153,11 +83,6 @@ void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* s
     return;
   }
   const int gs = (G + RPB - 1) / RPB;
-  unsigned* arr = colsum_fused_on() && gx <= 4096 && out.p[0] ? colsum_arrivals() : nullptr;
-  if (arr) {
-    colsum_f32_fused<<<dim3(gx, gs), 512, 0, st>>>(part, G, C, ld, RPB, scratch, arr, out);
-    return;
-  }
   colsum_f32_pass<<<dim3(gx, gs), 512, 0, st>>>(part, G, C, ld, RPB, scratch, ColOut{});
   colsum_f32_pass<<<dim3(gx, 1), 512, 0, st>>>(scratch, gs, C, C, gs, nullptr, out);
 }
