@@ -1,5 +1,8 @@
 """Minimal driver for PMC passes: gemm_nt and hipBLASLt on one GPT-2 shape.
-    python tools/nt_only.py [N] [K] [iters]"""
+    python tools/nt_only.py [N] [K] [iters] [impl] [gelu]
+With a 5th argument "gelu", each iteration also runs the fused bias-GELU
+epilogue form (gemm_nt_gelu) and the fused GELU'-dX form (gemm_nt_dgelu) of the
+same shape, for per-epilogue counter comparisons."""
 import os
 import sys
 
@@ -20,7 +23,14 @@ if impl >= 0:
     m.gemm_nt_impl(impl)
 x = torch.randn(65536, K, device="cuda", dtype=torch.bfloat16)
 w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
+gelu = len(sys.argv) > 5 and sys.argv[5] == "gelu"
+b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+pre = torch.randn(65536, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(it):
     m.gemm_nt(x, w)
-    F.linear(x, w)
+    if gelu:
+        m.gemm_nt_gelu(x, w, b)
+        m.gemm_nt_dgelu(x, w, pre, b)
+    else:
+        F.linear(x, w)
 torch.cuda.synchronize()
