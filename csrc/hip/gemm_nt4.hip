@@ -344,9 +344,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           if constexpr (EPI <= 1) {
             st16(crow, to_bf16(v + bv8));
           } else if constexpr (EPI == 2) {
-            const bf16x8 o = to_bf16(v);
-            st16(crow, o);
-            const f32x8 x = to_f32(o) + bv8;
+            // GELU of the fp32 pre-activation (the bf16 copy is stored for the
+            // backward, as hipBLASLt's GELU_AUX epilogue does); no bf16 round trip:
+            // the fused epilogues' cost is their VALU count with the matrix pipe
+            // idle (profiles/r3_nt4_deferred_drain.md, PMC section)
+            st16(crow, to_bf16(v));
+            const f32x8 x = v + bv8;
             f32x8 y;
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
             st16(Y + m * ldy + nb, to_bf16(y));
           } else {
             const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
-            const f32x8 dy = to_f32(to_bf16(v));
+            const f32x8& dy = v;  // the fp32 product, not its bf16 rounding
             f32x8 d;
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {

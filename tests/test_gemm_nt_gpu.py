@@ -44,8 +44,9 @@ def test_gelu_epilogue(hip):
     torch.testing.assert_close(pre.float(), ref, atol=2e-2, rtol=1e-2)
     # the activation is computed from the bf16-rounded pre-activation (as the unfused path)
     torch.testing.assert_close(y.float(), F.gelu(pre.float() + b.float(), approximate="tanh"), atol=1e-2, rtol=1e-2)
-    # and bit-identical to the standalone HIP bias-GELU kernel on the same input
-    assert torch.equal(y, hip.bias_gelu_fwd(pre, b))
+    # and the standalone HIP bias-GELU kernel on the same (bf16) input to a bf16
+    # ulp: the row epilogue applies GELU to the fp32 pre-activation
+    torch.testing.assert_close(y.float(), hip.bias_gelu_fwd(pre, b).float(), atol=1e-2, rtol=1e-2)
 
 
 def test_dgelu_epilogue_and_bias_grad(hip):
@@ -73,10 +74,15 @@ def test_rejects_unsupported_shapes(hip):
         hip.gemm_nt(x, w)
 
 
+# impls whose gemm_nt4 variant has the row epilogue (SCHED & 4): variants 8, 9, 11-15
+ROW_EPILOGUE_IMPLS = {9, 10, 12, 13, 14, 15, 16, 17}
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 256, 256), (256, 768, 384), (1024, 512, 2048), (768, 256, 128)])
 def test_nt4_mainloop_matches_ring(hip, M, N, K):
     """The 4-wave mainloop (gemm_nt4.hip, every schedule variant) runs the k-tiles
-    in the same order as the 8-wave ring: outputs equal bit for bit; K = 128
+    in the same order as the 8-wave ring: outputs equal bit for bit (the row
+    epilogue's GELU / GELU' forms to a bf16 rounding step); K = 128
     falls back to the ring (the 4-wave loop needs ≥ 4 even k-tiles)."""
     g = torch.Generator(device="cuda").manual_seed(7)
     a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
@@ -94,11 +100,19 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
             # products and their k order are the same, so they still match bitwise
             assert torch.equal(hip.gemm_nt(a, b, bias), ref), impl
             p, y = hip.gemm_nt_gelu(a, b, bias)
-            assert torch.equal(p, ref_p) and torch.equal(y, ref_y), impl
             dx, db = hip.gemm_nt_dgelu(a, b, pre, bias)
-            assert torch.equal(dx, ref_dx), impl
+            assert torch.equal(p, ref_p), impl
+            if impl in ROW_EPILOGUE_IMPLS:
+                # the row epilogue takes GELU / GELU' on the fp32 product instead of
+                # its bf16 rounding: equal to a bf16 rounding step
+                torch.testing.assert_close(y.float(), ref_y.float(), atol=2e-2, rtol=1e-2)
+                torch.testing.assert_close(dx.float(), ref_dx.float(), atol=2e-2, rtol=1e-2)
+            else:
+                assert torch.equal(y, ref_y) and torch.equal(dx, ref_dx), impl
             # bias-gradient partials are summed in another order: fp32 rounding only
-            torch.testing.assert_close(db.float(), ref_db.float(), rtol=2e-2, atol=2e-2)
+            # (row epilogue: sums of the unrounded dX, so up to a bf16 step per row)
+            torch.testing.assert_close(db.float(), ref_db.float(), rtol=2e-2,
+                                       atol=0.5 if impl in ROW_EPILOGUE_IMPLS else 2e-2)
         exact = a.float() @ b.float().t() + bias.float()
         torch.testing.assert_close(ref.float(), exact, rtol=2e-2, atol=6e-2)
     finally:
