@@ -111,8 +111,8 @@ def test_nt4_mainloop_matches_ring(hip, M, N, K):
                 assert torch.equal(y, ref_y) and torch.equal(dx, ref_dx), impl
             # bias-gradient partials are summed in another order: fp32 rounding only
             # (row epilogue: sums of the unrounded dX, so up to a bf16 step per row)
-            torch.testing.assert_close(db.float(), ref_db.float(), rtol=2e-2,
-                                       atol=0.5 if impl in ROW_EPILOGUE_IMPLS else 2e-2)
+            atol = 2e-2 * ref_db.float().abs().max().item() if impl in ROW_EPILOGUE_IMPLS else 2e-2
+            torch.testing.assert_close(db.float(), ref_db.float(), rtol=2e-2, atol=atol)
         exact = a.float() @ b.float().t() + bias.float()
         torch.testing.assert_close(ref.float(), exact, rtol=2e-2, atol=6e-2)
     finally:
