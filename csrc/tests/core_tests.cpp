@@ -555,14 +555,21 @@ static void test_k8s_exec_v5_fixture() {
     RawServer::send_all(fd, frame(0x82, std::string(1, '\x01')));          // stream init (channel byte only)
     RawServer::send_all(fd, frame(0x02, std::string("\x01") + "hel"));      // binary, FIN = 0
     RawServer::send_all(fd, frame(0x89, "hb"));                             // ping between fragments
+    // the client answers the ping as soon as it reads it: take its pong (masked,
+    // opcode 0xA) here, while the stream is still open (reading it only after the
+    // close let the client's close race the read)
+    char buf[512];
+    size_t have = 0;
+    for (int tries = 0; have < 2 && tries < 200; ++tries) {
+      const ssize_t n = ::recv(fd, buf + have, sizeof buf - have, 0);
+      if (n <= 0) break;
+      have += (size_t)n;
+    }
+    if (have >= 2 && ((unsigned char)buf[0] & 0x0f) == 0x0a) got_pong = true;
     RawServer::send_all(fd, frame(0x80, "lo\n"));                           // continuation, FIN = 1
     RawServer::send_all(fd, frame(0x82, std::string("\x02") + std::string(300, 'e')));
     RawServer::send_all(fd, frame(0x82, std::string("\x03") + status));
     RawServer::send_all(fd, frame(0x88, std::string("\x03\xe8", 2)));      // close 1000
-    // the client's pong (masked, opcode 0xA) arrives before its close
-    char buf[512];
-    ssize_t n = ::recv(fd, buf, sizeof buf, 0);
-    if (n >= 2 && ((unsigned char)buf[0] & 0x0f) == 0x0a) got_pong = true;
     usleep(20000);
   });
   pdo::http::ClientOptions o;
