@@ -297,18 +297,6 @@ __device__ __forceinline__ int tr_base_v(int cbase, int lane) {
   return toff_v(r0, col >> 3) + (col & 7);
 }
 
-// PRIO: wave priority 1 while issuing a run of MFMAs, 0 for the softmax VALU
-// work, so the SIMD's arbiter keeps the matrix pipe fed from whichever of its
-// waves is in an MFMA phase while the others' exp / max / pack fill the gaps
-template <int PRIO>
-__device__ __forceinline__ void prio_hi() {
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-}
-template <int PRIO>
-__device__ __forceinline__ void prio_lo() {
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-}
-
 template <int K0>
 __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Tlane + K0 * HD));
@@ -316,10 +304,6 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// SPLIT: the 64-key tile's softmax runs per 32-key half, each with its own
-// defer-max check, so the exp / sum / pack of half 0 and its P·V depend only on
-// half 0's score MFMAs and can run while half 1's are still in the matrix pipe
-template <int PRIO, int SPLIT = 0>
 __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                      float* __restrict__ lse, int B, int S, int H, float c2,
                                                      int order) {
@@ -369,222 +353,13 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       f32x16 s0 = nm16, s1 = nm16;
-      prio_hi<PRIO>();
-      if constexpr (SPLIT) {  // half 0's chain first: its softmax can start under half 1's
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
-          s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
-        }
-      }
-      prio_lo<PRIO>();
-      if constexpr (SPLIT) {
-        const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;  // wave-uniform
-        const int dq = q - key0 - 4 * hh;
-        const bf16* V0 = Vt + vb0;
-        const bf16* V1 = Vt + vb1;
-        // one 32-key half h: mask, defer-max check (rescales o, l and the other
-        // half's pending scores), exp, row sum, P·V on its two 16-key slices
-        auto half = [&](f32x16& sh, f32x16& so, auto hc) {
-          constexpr int H = decltype(hc)::value;
-          if (diag) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int c = (r & 3) + 8 * (r >> 2) + 32 * H;
-              sh[r] = c > dq ? -INFINITY : sh[r];
-            }
-          }
-          float tmax = -INFINITY;
-#pragma unroll
-          for (int r = 0; r < 16; r += 4) tmax = fmaxf(fmaxf(tmax, fmaxf(sh[r], sh[r + 1])), fmaxf(sh[r + 2], sh[r + 3]));
-          tmax = xhalf_max(tmax);
-          if (H == 0 && t == 0) {  // every query has key 0 unmasked here: tmax is finite
-            m = tmax;
-            sh -= tmax;
-            so -= tmax;
-            nm16 = bcast16(-m);
-          } else if (__any(tmax > 8.f)) {
-            const float d = tmax > 8.f ? tmax : 0.f;
-            const float alpha = __builtin_amdgcn_exp2f(-d);
-            m += d;
-            l *= alpha;
-            o0 *= alpha;
-            o1 *= alpha;
-            sh -= d;
-            if constexpr (H == 0) so -= d;
-            nm16 = bcast16(-m);
-          }
-          f32x2 ls2 = {0.f, 0.f};
-#pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            sh[r] = __builtin_amdgcn_exp2f(sh[r]);
-            sh[r + 1] = __builtin_amdgcn_exp2f(sh[r + 1]);
-            ls2 += f32x2{sh[r], sh[r + 1]};
-          }
-          l += ls2[0] + ls2[1];
-          prio_hi<PRIO>();
-          const bf16x8 pa = pack8(sh, 0), pb = pack8(sh, 1);
-          o0 = mfma(tr_frag_v<32 * H>(V0), pa, o0);
-          o1 = mfma(tr_frag_v<32 * H>(V1), pa, o1);
-          o0 = mfma(tr_frag_v<32 * H + 16>(V0), pb, o0);
-          o1 = mfma(tr_frag_v<32 * H + 16>(V1), pb, o1);
-          prio_lo<PRIO>();
-        };
-        half(s0, s1, std::integral_constant<int, 0>{});
-        half(s1, s0, std::integral_constant<int, 1>{});
-      } else {
-        if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
-          // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
-          const int d = q - key0 - 4 * hh;
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int c = (r & 3) + 8 * (r >> 2);
-            s0[r] = c > d ? -INFINITY : s0[r];
-            s1[r] = c + 32 > d ? -INFINITY : s1[r];
-          }
-        }
-        // tile max of s' (relative to m): only a growth past 2^8 rescales
-        // (defer-max, cdna_hip_programming.md T13); the first tile sets m
-        float tmax = -INFINITY;
-  #pragma unroll
-        for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-        tmax = xhalf_max(tmax);
-        if (t == 0) {  // every query has key 0 unmasked here: tmax is finite
-          m = tmax;
-          s0 -= tmax;
-          s1 -= tmax;
-          nm16 = bcast16(-m);
-        } else if (__any(tmax > 8.f)) {
-          const float d = tmax > 8.f ? tmax : 0.f;
-          const float alpha = __builtin_amdgcn_exp2f(-d);
-          m += d;
-          l *= alpha;
-          o0 *= alpha;
-          o1 *= alpha;
-          s0 -= d;
-          s1 -= d;
-          nm16 = bcast16(-m);
-        }
-        f32x2 ls2 = {0.f, 0.f};
-  #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-          s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
-          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-          s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
-          ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
-        }
-        l += ls2[0] + ls2[1];
-        const bf16* V0 = Vt + vb0;
-        const bf16* V1 = Vt + vb1;
-        prio_hi<PRIO>();
-        {
-          const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
-          o0 = mfma(tr_frag_v<0>(V0), p0, o0);
-          o1 = mfma(tr_frag_v<0>(V1), p0, o1);
-          o0 = mfma(tr_frag_v<32>(V0), p1, o0);
-          o1 = mfma(tr_frag_v<32>(V1), p1, o1);
-        }
-        {
-          const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
-          o0 = mfma(tr_frag_v<16>(V0), p0, o0);
-          o1 = mfma(tr_frag_v<16>(V1), p0, o1);
-          o0 = mfma(tr_frag_v<48>(V0), p1, o0);
-          o1 = mfma(tr_frag_v<48>(V1), p1, o1);
-        }
-        prio_lo<PRIO>();
-      }
-    }
-    if (more) {
-      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-      stage_store(sk, Kn, tid);
-      stage_store_v(sv, Kn + TROWS * HD, tid);
-    }
-    __syncthreads();
-  }
-  const float lt = xhalf_sum(l);
-  const float inv = 1.f / lt;
-  bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
-  store_acc_rows(orow, o0, 0, hh, inv);
-  store_acc_rows(orow, o1, 32, hh, inv);
-  if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
-}
-
-// ============================================================================
-// forward with an LDS-DMA ring (PDO_ATTN_FWD=3): the forward's structure, with
-// K / V tiles arriving by LDS-DMA two tiles ahead through 3 slots (the dK/dV
-// kernel's ring) instead of register staging one tile ahead — no staging
-// registers, no ds_write pass, and each tile's loads have ≈ 2 tiles of lead
-// ============================================================================
-__device__ __forceinline__ unsigned dma_voff_v(int lane, size_t row_stride) {
-  const int rr = lane >> 3;  // toff_v's swizzle sees row bit 1 only: one offset for every piece
-  return (unsigned)(((size_t)rr * row_stride + (size_t)(((lane & 7) ^ (((rr >> 1) & 1) << 2)) << 3)) * 2);
-}
-
-__global__ __launch_bounds__(256) void attn_fwd3_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                      float* __restrict__ lse, int B, int S, int H, float c2,
-                                                      int order) {
-  constexpr int SLOT = 2 * TROWS * HD;                                   // bf16 units: K then V (16 KiB)
-  __shared__ __attribute__((aligned(16))) bf16 smem[3 * SLOT];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
-  const int nqb = S / 128;
-  int bh, r_;
-  attn_block(order, nqb, B * H, bh, r_);
-  const int qb = nqb - 1 - r_;  // heaviest query blocks first
-  const int b = bh / H, h = bh % H;
-  const size_t rs = (size_t)3 * H * HD;
-  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
-  const bf16* kbase = qbase + (size_t)H * HD;
-  const bf16* vbase = qbase + (size_t)2 * H * HD;
-
-  const int q = qb * 128 + w * 32 + li;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * ks + 8 * hh);
-  retire(qf);
-  prescale(qf, c2);
-
-  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
-  f32x16 o0 = zero16(), o1 = zero16();
-  float m = 0.f, l = 0.f;
-  f32x16 nm16 = zero16();
-  const int ntiles = (qb * 128 + 128) / TROWS;
-  const int wave_qmax = qb * 128 + w * 32 + 31;
-
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const unsigned lds0 = lds_addr(smem);
-  const unsigned vk0 = dma_voff(lane, rs, 0), vk1 = dma_voff(lane, rs, 1), vv = dma_voff_v(lane, rs);
-  auto issue = [&](int t, int slot) {  // this wave's 4 pieces (2 K, 2 V) of tile t
-    const unsigned base = lds0 + (unsigned)(slot * SLOT * 2);
-    dma_tile(kbase, rs, t * TROWS, wu, vk0, vk1, base);
-    dma_tile(vbase, rs, t * TROWS, wu, vv, vv, base + TROWS * HD * 2);
-  };
-  issue(0, 0);
-  if (ntiles > 1) issue(1, 1);
-  int sl = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles)
-      vm_wait<4>();  // this wave's pieces of tile t have landed (t + 1's 4 may still fly)
-    else
-      vm_wait<0>();
-    __syncthreads();  // ... and every other wave's; slot (sl + 2) % 3 (tile t - 1) is free again
-    if (t + 2 < ntiles) issue(t + 2, sl == 0 ? 2 : sl - 1);
-    const bf16* Kt = smem + sl * SLOT;
-    const bf16* Vt = Kt + TROWS * HD;
-    const int key0 = t * TROWS;
-    if (key0 <= wave_qmax) {
-      f32x16 s0 = nm16, s1 = nm16;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         s0 = mfma(row_frag(Kt, 0, ks, lane), qf[ks], s0);
         s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
       }
       if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
+        // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
         const int d = q - key0 - 4 * hh;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -593,11 +368,13 @@ __global__ __launch_bounds__(256) void attn_fwd3_d64(const bf16* __restrict__ qk
           s1[r] = c + 32 > d ? -INFINITY : s1[r];
         }
       }
+      // tile max of s' (relative to m): only a growth past 2^8 rescales
+      // (defer-max, cdna_hip_programming.md T13); the first tile sets m
       float tmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
       tmax = xhalf_max(tmax);
-      if (t == 0) {
+      if (t == 0) {  // every query has key 0 unmasked here: tmax is finite
         m = tmax;
         s0 -= tmax;
         s1 -= tmax;
@@ -640,7 +417,12 @@ __global__ __launch_bounds__(256) void attn_fwd3_d64(const bf16* __restrict__ qk
         o1 = mfma(tr_frag_v<48>(V1), p1, o1);
       }
     }
-    sl = sl == 2 ? 0 : sl + 1;
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store_v(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
   }
   const float lt = xhalf_sum(l);
   const float inv = 1.f / lt;
@@ -651,177 +433,8 @@ __global__ __launch_bounds__(256) void attn_fwd3_d64(const bf16* __restrict__ qk
 }
 
 // ============================================================================
-// forward, two 32-query blocks per wave (PDO_ATTN_FWD=2): workgroup = 4 waves =
-// 256 queries.  Every K fragment (ds_read_b128) and V fragment (transposed
-// reads) feeds two MFMAs instead of one, and each wave carries two independent
-// softmax chains per tile for the scheduler to interleave with the other
-// block's MFMAs.  2 waves per SIMD (≤ 256 VGPRs) instead of 3.
-// ============================================================================
-struct FwdBlock {
-  f32x16 o0, o1;  // output accumulators
-  float m, l;     // running max (log2 units; −m broadcast is the score MFMAs' initial C) and sum
-};
-
-__global__ __launch_bounds__(256, 2) void attn_fwd2_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                         float* __restrict__ lse, int B, int S, int H, float c2,
-                                                         int order) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
-  const int nqb = S / 256;
-  int bh, r_;
-  attn_block(order, nqb, B * H, bh, r_);
-  const int qb = nqb - 1 - r_;  // heaviest query blocks first
-  const int b = bh / H, h = bh % H;
-  const size_t rs = (size_t)3 * H * HD;
-  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
-  const bf16* kbase = qbase + (size_t)H * HD;
-  const bf16* vbase = qbase + (size_t)2 * H * HD;
-
-  const int qw0 = qb * 256 + w * 64;  // first query of this wave (block 0; block 1 = +32)
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[u][ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)(qw0 + 32 * u + li) * rs + 16 * ks + 8 * hh);
-  retire(qf[0]);
-  retire(qf[1]);
-  prescale(qf[0], c2);
-  prescale(qf[1], c2);
-
-  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
-  FwdBlock blk[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    blk[u].o0 = zero16();
-    blk[u].o1 = zero16();
-    blk[u].m = 0.f;
-    blk[u].l = 0.f;
-  }
-  const int ntiles = (qb * 256 + 256) / TROWS;
-
-  Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
-  stage_store(sk, smem, tid);
-  stage_store_v(sv, smem + TROWS * HD, tid);
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
-    const bf16* Vt = Kt + TROWS * HD;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
-      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
-    }
-    const int key0 = t * TROWS;
-    if (key0 <= qw0 + 63) {
-      const bool do0 = key0 <= qw0 + 31;  // block 0 has a key of this tile at or before its queries
-      f32x16 s[2][2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) s[u][0] = s[u][1] = bcast16(-blk[u].m);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 k0 = row_frag(Kt, 0, ks, lane), k1 = row_frag(Kt, 32, ks, lane);
-        if (do0) {
-          s[0][0] = mfma(k0, qf[0][ks], s[0][0]);
-          s[0][1] = mfma(k1, qf[0][ks], s[0][1]);
-        }
-        s[1][0] = mfma(k0, qf[1][ks], s[1][0]);
-        s[1][1] = mfma(k1, qf[1][ks], s[1][1]);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (u == 0 && !do0) continue;
-        FwdBlock& k = blk[u];
-        f32x16& s0 = s[u][0];
-        f32x16& s1 = s[u][1];
-        const int qfirst = qw0 + 32 * u;
-        if (key0 + TROWS - 1 > qfirst) {  // diagonal tile (wave-uniform)
-          const int d = qfirst + li - key0 - 4 * hh;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int c = (r & 3) + 8 * (r >> 2);
-            s0[r] = c > d ? -INFINITY : s0[r];
-            s1[r] = c + 32 > d ? -INFINITY : s1[r];
-          }
-        }
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-        tmax = xhalf_max(tmax);
-        if (t == 0) {
-          k.m = tmax;
-          s0 -= tmax;
-          s1 -= tmax;
-        } else if (__any(tmax > 8.f)) {
-          const float dm = tmax > 8.f ? tmax : 0.f;
-          const float alpha = __builtin_amdgcn_exp2f(-dm);
-          k.m += dm;
-          k.l *= alpha;
-          k.o0 *= alpha;
-          k.o1 *= alpha;
-          s0 -= dm;
-          s1 -= dm;
-        }
-        f32x2 ls2 = {0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-          s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
-          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-          s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
-          ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
-        }
-        k.l += ls2[0] + ls2[1];
-      }
-      const bf16* V0 = Vt + vb0;
-      const bf16* V1 = Vt + vb1;
-#define PV_STEP(KA, KB, PR)                                           \
-  {                                                                   \
-    const bf16x8 va0 = tr_frag_v<KA>(V0), va1 = tr_frag_v<KA>(V1);    \
-    const bf16x8 vb0_ = tr_frag_v<KB>(V0), vb1_ = tr_frag_v<KB>(V1);  \
-    if (do0) {                                                        \
-      const bf16x8 pa = pack8(s[0][0], PR), pb = pack8(s[0][1], PR);  \
-      blk[0].o0 = mfma(va0, pa, blk[0].o0);                           \
-      blk[0].o1 = mfma(va1, pa, blk[0].o1);                           \
-      blk[0].o0 = mfma(vb0_, pb, blk[0].o0);                          \
-      blk[0].o1 = mfma(vb1_, pb, blk[0].o1);                          \
-    }                                                                 \
-    const bf16x8 pa = pack8(s[1][0], PR), pb = pack8(s[1][1], PR);    \
-    blk[1].o0 = mfma(va0, pa, blk[1].o0);                             \
-    blk[1].o1 = mfma(va1, pa, blk[1].o1);                             \
-    blk[1].o0 = mfma(vb0_, pb, blk[1].o0);                            \
-    blk[1].o1 = mfma(vb1_, pb, blk[1].o1);                            \
-  }
-      PV_STEP(0, 32, 0)
-      PV_STEP(16, 48, 1)
-#undef PV_STEP
-    }
-    if (more) {
-      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-      stage_store(sk, Kn, tid);
-      stage_store_v(sv, Kn + TROWS * HD, tid);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int q = qw0 + 32 * u + li;
-    const float lt = xhalf_sum(blk[u].l);
-    const float inv = 1.f / lt;
-    bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
-    store_acc_rows(orow, blk[u].o0, 0, hh, inv);
-    store_acc_rows(orow, blk[u].o1, 32, hh, inv);
-    if (hh == 0) lse[(size_t)bh * S + q] = (blk[u].m + log2f(lt)) * LN2;
-  }
-}
-
-// ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
-template <int PRIO>
 __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                           bf16* __restrict__ dqkv, int B, int S, int H, float c2,
@@ -909,13 +522,11 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
             dpacc[4 * g + e] = d4[e];
           }
         }
-        prio_hi<PRIO>();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
           dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
         }
-        prio_lo<PRIO>();
         // The causal mask only touches the diagonal sub-tile (wave-uniform): a
         // separate body keeps its compares and selects out of every other tile
         auto softmax_grad = [&](auto masked) {
@@ -936,7 +547,6 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
           softmax_grad(std::true_type{});
         else
           softmax_grad(std::false_type{});
-        prio_hi<PRIO>();
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 pb = pack8(sacc, sst);
@@ -946,7 +556,6 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
           dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
           dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
         }
-        prio_lo<PRIO>();
       }
     }
     sl = sl == 2 ? 0 : sl + 1;
@@ -975,29 +584,25 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
   const bf16 *__restrict__ qkv, const bf16 *__restrict__ dout, const float *__restrict__ lse,                        \
       const float *__restrict__ delta, bf16 *__restrict__ dqkv, int B, int S, int H, float c2, float scale,          \
       float *__restrict__ dbias_part, int order
-template <int PRIO>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(PDO_DKDV_ARGS) {
-  dkdv_body<PRIO>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+  dkdv_body(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 // the same body capped at 168 VGPRs: 3 waves per SIMD instead of 2 (the LDS
 // ring, 49.5 KiB per workgroup, allows 3 workgroups per CU)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dkdv3_d64(PDO_DKDV_ARGS) {
-  dkdv_body<0>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+  dkdv_body(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 #undef PDO_DKDV_ARGS
 
 // ============================================================================
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
 // ============================================================================
-// RING: K / V tiles by LDS-DMA two tiles ahead through 3 slots (the dK/dV
-// kernel's ring) instead of register staging one tile ahead
-template <int PRIO, int RING = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                        const bf16* __restrict__ o, const float* __restrict__ lse,
                                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
                                                        int H, float c2, float scale, float* __restrict__ dbias_part,
                                                        int order) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[(RING ? 3 : 2) * 2 * TROWS * HD];
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
   int bh, r_;
@@ -1050,39 +655,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
   Stage sk, sv;
-  constexpr int SLOT = 2 * TROWS * HD;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const unsigned lds0 = lds_addr(smem);
-  const unsigned vk0 = dma_voff(lane, rs, 0), vk1 = dma_voff(lane, rs, 1);
-  auto issue = [&](int t, int slot) {  // this wave's 4 pieces (2 K, 2 V) of tile t
-    const unsigned base = lds0 + (unsigned)(slot * SLOT * 2);
-    dma_tile(kbase, rs, t * TROWS, wu, vk0, vk1, base);
-    dma_tile(vbase, rs, t * TROWS, wu, vk0, vk1, base + TROWS * HD * 2);
-  };
-  if constexpr (RING) {
-    issue(0, 0);
-    if (ntiles > 1) issue(1, 1);
-  } else {
-    stage_load(sk, kbase, rs, 0, tid);
-    stage_load(sv, vbase, rs, 0, tid);
-    stage_store(sk, smem, tid);
-    stage_store(sv, smem + TROWS * HD, tid);
-    __syncthreads();
-  }
-  int sl = 0;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store(sv, smem + TROWS * HD, tid);
+  __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
-    if constexpr (RING) {
-      if (more)
-        vm_wait<4>();  // this wave's pieces of tile t have landed (t + 1's 4 may still fly)
-      else
-        vm_wait<0>();
-      __syncthreads();  // ... and every other wave's; slot (sl + 2) % 3 is free again
-      if (t + 2 < ntiles) issue(t + 2, sl == 0 ? 2 : sl - 1);
-    }
-    const bf16* Kt = RING ? smem + sl * SLOT : smem + (t & 1) * 2 * TROWS * HD;
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
     const bf16* Vt = Kt + TROWS * HD;
-    if (!RING && more) {
+    if (more) {
       stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
       stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
     }
@@ -1092,13 +674,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
       for (int ksub = 0; ksub < 2; ++ksub) {
         f32x16 s = zero16(), dp = zero16();
-        prio_hi<PRIO>();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
           dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
         }
-        prio_lo<PRIO>();
         auto softmax_grad = [&](auto masked) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -1114,28 +694,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           softmax_grad(std::true_type{});
         else
           softmax_grad(std::false_type{});
-        prio_hi<PRIO>();
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 dsb = pack8(s, sst);
           a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
           a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
         }
-        prio_lo<PRIO>();
       }
     }
-    if constexpr (RING) {
-      sl = sl == 2 ? 0 : sl + 1;
-    } else {
-      if (more) {
-        bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-        stage_store(sk, Kn, tid);
-        stage_store(sv, Kn + TROWS * HD, tid);
-      }
-      __syncthreads();
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store(sv, Kn + TROWS * HD, tid);
     }
+    __syncthreads();
   }
-  if constexpr (RING) __syncthreads();  // the epilogue's column sums reuse the ring
   bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
   store_acc_rows(qrow, a0, 0, hh, scale);
   store_acc_rows(qrow, a1, 32, hh, scale);
@@ -1157,30 +730,10 @@ static int attn_order() {
   static const int o = env_int("PDO_ATTN_ORDER", 0);
   return o;
 }
-// PDO_ATTN_PRIO bit 0: forward, bit 1: dQ, bit 2: dK/dV raise the wave priority around their MFMA runs
-static int attn_prio() {
-  static const int p = env_int("PDO_ATTN_PRIO", 0);
-  return p;
-}
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
-  static const int variant = env_int("PDO_ATTN_FWD", 1);
-  if (variant == 3) {
-    attn_fwd3_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-    return 0;
-  }
-  if (variant == 2 && S % 256 == 0) {
-    attn_fwd2_d64<<<B * H * (S / 256), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-    return 0;
-  }
-  const int grid = B * H * (S / 128);
-  if (variant == 4)
-    attn_fwd_d64<0, 1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else if (attn_prio() & 1)
-    attn_fwd_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else
-    attn_fwd_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  attn_fwd_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   return 0;
 }
 
@@ -1189,27 +742,17 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  static const int dq3 = env_int("PDO_ATTN_DQ3", 0);
-  if (dq3)
-    attn_bwd_dq_d64<0, 1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                                dbias_part, attn_order());
-  else if (attn_prio() & 2)
-    attn_bwd_dq_d64<1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                             dbias_part, attn_order());
-  else
-    attn_bwd_dq_d64<0><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                             dbias_part, attn_order());
-  // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step
+  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
+                                        attn_order());
+  // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step;
+  // PDO_ATTN_DKDV3=0 = the 2-waves-per-SIMD build of the same body (A/B alternative)
   static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 1);
   if (dkdv3)
     attn_bwd_dkdv3_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
                                              attn_order());
-  else if (attn_prio() & 4)
-    attn_bwd_dkdv_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                               dbias_part, attn_order());
   else
-    attn_bwd_dkdv_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                               dbias_part, attn_order());
+    attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
+                                            attn_order());
   return 0;
 }
 

@@ -365,47 +365,6 @@ at::Tensor transpose(at::Tensor x, std::optional<at::Tensor> out) {
   return y;
 }
 
-// ---------------------------------------------------------------- hipBLASLt fused MLP epilogues
-constexpr int kEpiGeluAuxBias = 164;  // HIPBLASLT_EPILOGUE_GELU_AUX_BIAS
-constexpr int kEpiDGeluBGrad = 208;   // HIPBLASLT_EPILOGUE_DGELU_BGRAD
-constexpr int kEpiDGelu = 192;        // HIPBLASLT_EPILOGUE_DGELU
-constexpr size_t kLtWorkspace = 64ull << 20;
-
-// h = gelu(x·wᵀ + b), h_pre = x·wᵀ + b   (x [T,K], w [N,K], b [N]); empty list = no solution
-std::vector<at::Tensor> linear_gelu(at::Tensor x, at::Tensor w, at::Tensor b) {
-  CHECK_IN(x); CHECK_IN(w); CHECK_IN(b); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1) && b.numel() == w.size(0));
-  const long long T = x.size(0), K = x.size(1), N = w.size(0);
-  auto h = at::empty({T, N}, x.options());
-  auto hp = at::empty({T, N}, x.options());
-  auto ws = at::empty({(long long)kLtWorkspace}, x.options().dtype(at::kByte));
-  int rc = pdo::lt_matmul(x.get_device(), kEpiGeluAuxBias, 1, 0, N, T, K, bp(w), K, bp(x), K, bp(h), N, b.data_ptr(),
-                          0, hp.data_ptr(), N, ws.data_ptr(), kLtWorkspace, cur_stream());
-  if (rc != 0) return {};
-  return {h, hp};
-}
-
-// dh_pre = (dy·w2) ⊙ gelu'(h_pre), db = Σ_t dh_pre   (dy [T,N2], w2 [N2,N], h_pre [T,N])
-std::vector<at::Tensor> matmul_dgelu(at::Tensor dy, at::Tensor w2, at::Tensor h_pre) {
-  CHECK_IN(dy); CHECK_IN(w2); CHECK_IN(h_pre); CHECK_BF16(dy); CHECK_BF16(w2); CHECK_BF16(h_pre);
-  TORCH_CHECK(dy.dim() == 2 && w2.dim() == 2 && dy.size(1) == w2.size(0) && h_pre.size(0) == dy.size(0) &&
-              h_pre.size(1) == w2.size(1));
-  const long long T = dy.size(0), N2 = dy.size(1), N = w2.size(1);
-  auto dh = at::empty({T, N}, dy.options());
-  auto db = at::empty({N}, dy.options());
-  auto ws = at::empty({(long long)kLtWorkspace}, dy.options().dtype(at::kByte));
-  int rc = pdo::lt_matmul(dy.get_device(), kEpiDGeluBGrad, 0, 0, N, T, N2, bp(w2), N, bp(dy), N2, bp(dh), N,
-                          db.data_ptr(), 0, h_pre.data_ptr(), N, ws.data_ptr(), kLtWorkspace, cur_stream());
-  if (rc != 0) {
-    // gfx950 hipBLASLt has DGELU_BGRAD only for small n: DGELU in the GEMM, bias grad by the HIP column reduction
-    rc = pdo::lt_matmul(dy.get_device(), kEpiDGelu, 0, 0, N, T, N2, bp(w2), N, bp(dy), N2, bp(dh), N, nullptr, 0,
-                        h_pre.data_ptr(), N, ws.data_ptr(), kLtWorkspace, cur_stream());
-    if (rc != 0) return {};
-    db = bias_grad(dh, c10::nullopt);
-  }
-  return {dh, db};
-}
-
 // ---------------------------------------------------------------- NHWC BatchNorm + ReLU (+ residual)
 // x: channels_last bf16 [N,C,H,W] (memory NHWC); w,b,running_*: fp32 [C]
 std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor w, at::Tensor b,
@@ -545,6 +504,20 @@ std::vector<at::Tensor> attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, 
 void scale_(at::Tensor x, double s) {
   CHECK_IN(x); CHECK_BF16(x);
   CHECK_RC(pdo::scale_bf16(bp(x), x.numel(), (float)s, cur_stream()), "scale_bf16");
+}
+
+// x *= s[0] in place (s: fp32 device scalar, e.g. the loss gradient)
+void scale_dev_(at::Tensor x, at::Tensor s) {
+  CHECK_IN(x); CHECK_BF16(x); CHECK_IN(s);
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() >= 1, "scale must be an fp32 device scalar");
+  CHECK_RC(pdo::scale_dev_bf16(bp(x), x.numel(), fp(s), cur_stream()), "scale_dev_bf16");
+}
+
+// g += h; h = 0 (bf16, same length)
+void fold_zero(at::Tensor g, at::Tensor h) {
+  CHECK_IN(g); CHECK_IN(h); CHECK_BF16(g); CHECK_BF16(h);
+  TORCH_CHECK(g.numel() == h.numel(), "fold_zero: length mismatch");
+  CHECK_RC(pdo::fold_zero_bf16(bp(g), bp(h), g.numel(), cur_stream()), "fold_zero_bf16");
 }
 
 // flat[off_i : off_i + n_i] = scale * t_i for every tensor (one launch);
@@ -719,25 +692,12 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
-  m.def("linear_gelu", &linear_gelu);
-  m.def("lt_last_error", [] { return std::string(pdo::lt_last_error()); });
-  // raw probe: epilogue id on D[m,n] = op(A)op(B) with optional bias/aux (diagnostics)
-  m.def("lt_probe", [](int epi, int ta, int tb, int64_t m_, int64_t n_, int64_t k_, bool bias, bool aux, bool bias_f32) {
-    auto o = at::TensorOptions().device(at::kCUDA).dtype(at::kBFloat16);
-    auto A = at::randn({m_ * k_}, o), B = at::randn({k_ * n_}, o), D = at::empty({m_ * n_}, o);
-    auto bb = at::zeros({m_}, bias_f32 ? o.dtype(at::kFloat) : o);
-    auto ax = at::randn({m_ * n_}, o);
-    auto ws = at::empty({(int64_t)kLtWorkspace}, o.dtype(at::kByte));
-    int rc = pdo::lt_matmul(A.get_device(), epi, ta, tb, m_, n_, k_, bp(A), ta ? k_ : m_, bp(B), tb ? n_ : k_, bp(D), m_,
-                            bias ? bb.data_ptr() : nullptr, bias_f32, aux ? ax.data_ptr() : nullptr, m_, ws.data_ptr(),
-                            kLtWorkspace, cur_stream());
-    return std::make_tuple(rc, std::string(pdo::lt_last_error()));
-  });
-  m.def("matmul_dgelu", &matmul_dgelu);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("n_head"),
         py::arg("with_bias_grad") = false, py::arg("db_out") = py::none());
   m.def("scale_", &scale_);
+  m.def("scale_dev_", &scale_dev_);
+  m.def("fold_zero", &fold_zero);
   m.def("flatten_scale", &flatten_scale);
   m.def("cast_scale_bf16_f32", &cast_scale_bf16_f32);
   m.def("cast_f32_bf16", &cast_f32_bf16);

@@ -66,6 +66,41 @@ __global__ __launch_bounds__(256) void cast_scale_bf16_f32_kernel(const bf16* __
   }
 }
 
+// x *= *s (an fp32 device scalar: the loss gradient, no host sync), fp32 math
+__global__ __launch_bounds__(256) void scale_dev_kernel(bf16* __restrict__ x, long long nvec, const float* __restrict__ s) {
+  const float f = *s;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    bf16x8* p = reinterpret_cast<bf16x8*>(x) + i;
+    *p = to_bf16(to_f32(*p) * f);
+  }
+}
+
+// g += h; h = 0 (a split parameter's head-gradient slot folded into its
+// gradient after the all-reduce drain, parallel/flat.py fold_split)
+__global__ __launch_bounds__(256) void fold_zero_kernel(bf16* __restrict__ g, bf16* __restrict__ h, long long nvec) {
+  const bf16x8 z = to_bf16(f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    bf16x8* pg = reinterpret_cast<bf16x8*>(g) + i;
+    bf16x8* ph = reinterpret_cast<bf16x8*>(h) + i;
+    *pg = to_bf16(to_f32(*pg) + to_f32(*ph));
+    *ph = z;
+  }
+}
+
+int scale_dev_bf16(bf16* x, long long n, const float* s, hipStream_t st) {
+  if (n % 8) return -2;
+  if (n == 0) return 0;
+  scale_dev_kernel<<<stream_grid(n / 8, 256), 256, 0, st>>>(x, n / 8, s);
+  return 0;
+}
+
+int fold_zero_bf16(bf16* g, bf16* h, long long n, hipStream_t st) {
+  if (n % 8) return -2;
+  if (n == 0) return 0;
+  fold_zero_kernel<<<stream_grid(n / 8, 256), 256, 0, st>>>(g, h, n / 8);
+  return 0;
+}
+
 template <typename T>
 static int multi_tensor(bool flatten, T* flat, long long total, int n, void* dev_meta, float scale, hipStream_t st) {
   if (total <= 0 || n <= 0) return 0;

@@ -217,14 +217,15 @@ __global__ __launch_bounds__(NTHR) void gemm_dw_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
-// 4-wave mainloop (gemm_dw4.hip) where its contract holds: impl 3 = variant 2
-// (half-buffer refill, two barriers per tile, 32x32x16 MFMAs), impl 4 (default)
-// = the same schedule on 16x16x32 MFMAs (isolated: qkv 333 -> 325 us, proj 125 ->
-// 118, fc1 404 -> 400, fc2 409 -> 403; step 144.7 -> 143.4 ms, profiles/r3_dw4_m16.md).
-// PDO_DW_IMPL overrides (A/B in the step: tools/gpu.sh 'stepab:PDO_DW_IMPL=3 PDO_DW_IMPL=4')
+// 4-wave mainloop (gemm_dw4.hip) where its contract holds: impl 1 (default) =
+// the half-buffer refill schedule on 16x16x32 MFMAs, impl 2 = the same on
+// 32x32x16 (isolated: qkv 333 -> 325 us, proj 125 -> 118, fc1 404 -> 400, fc2
+// 409 -> 403 for impl 1; step 144.7 -> 143.4 ms, profiles/r3_dw4_m16.md);
+// impl 0 = the 8-wave loop below.
+// PDO_DW_IMPL overrides (A/B in the step: tools/gpu.sh 'stepab:PDO_DW_IMPL=1 PDO_DW_IMPL=2')
 static int g_dw_impl = [] {
   const char* e = getenv("PDO_DW_IMPL");
-  return e && *e ? atoi(e) : 4;
+  return e && *e ? atoi(e) : 1;
 }();
 void gemm_dw_set_impl(int impl) { g_dw_impl = impl; }
 int gemm_dw_get_impl() { return g_dw_impl; }

@@ -9,17 +9,16 @@
 // accumulator file), and one instruction stream per wave interleaves MFMAs,
 // transposed reads and DMA:
 //
-//   tile t (64 tokens, LDS buffer t&1), 64 MFMAs per wave:
-//   block 0 (tokens 0-31): 16 groups of {2 MFMAs on fragments F0; 1 fragment
-//            of F1 (tokens 32-63) read; 1 DMA piece of tile t+1 (the first
-//            E pieces went out at the end of tile t-1)}
-//   block 1 (tokens 32-63): 16 groups of {2 MFMAs on F1}; after group BAR the
-//            wave retires its DMA (vmcnt(0)) and reads (lgkmcnt(0)), one
-//            s_barrier; the remaining groups read F0 of tile t+1 and issue the
-//            first E = 15 - BAR DMA pieces of tile t+2 into buffer t&1.
+//   tile t (64 tokens, LDS buffer t&1), two barriers per tile: each 32-token
+//   half of a buffer is refilled with tile t+2 as soon as every wave has read
+//   it, so every DMA piece has ≈ 1.5 tiles of lead (hipBLASLt's gfx950 loop
+//   does the same with three barriers).
 //
-// RAW / WAR: as gemm_nt4.hip (one barrier per tile; a buffer is refilled only
-// after the barrier that follows every wave's last read of it).
+// RAW / WAR: a buffer half is refilled only after the barrier that follows
+// every wave's last read of it; a tile is read only after every wave retired
+// its own DMA of it and passed a barrier.  (Round 4 housekeeping: the
+// one-barrier schedules of round 2 measured slower and were removed,
+// profiles/r2_gemm_nt4.md.)
 #include <type_traits>
 
 #include "common.h"
@@ -57,7 +56,6 @@ __device__ __forceinline__ bf16x8 frag(const bf16* T) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BAR>
 __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int ksteps_total,
                                                            int splits, bf16* __restrict__ C, int ldc,
@@ -156,8 +154,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
   f32x16 acc[4][4];  // first written by mma0 in tile 0's block 0
   bf16x8 f0[16], f1[16];
 
-  if constexpr (BAR < 0) {
-    // ---- half-buffer refill schedule (BAR < 0): each 32-token half of a buffer is
+  {
+    // ---- half-buffer refill schedule: each 32-token half of a buffer is
     // refilled as soon as every wave has read it — tile t+2's first half during
     // block 0 of tile t (after barrier B0: F0(t) reads done), its second half during
     // block 1 (after B1: F1(t) reads done).  Tile t+1's data therefore has ≈1.5 tiles
@@ -238,80 +236,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
     }
     tileH(nk - 2, B0{}, T_{}, F_{}, F_{});
     tileH(nk - 1, B1{}, F_{}, F_{}, F_{});
-  } else {
-  {
-    const Src s0 = srcs(0);
-#pragma unroll
-    for (int p = 0; p < 16; ++p) dma(s0, B0{}, p);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) f0[q] = rd(B0{}, 0, q);
-
-  constexpr int E = 15 - BAR;
-  auto tile = [&](int t, auto buf_tag, auto more_tag, auto first_tag, auto ein_tag, auto eout_tag) {
-    constexpr int BUF = decltype(buf_tag)::value;
-    constexpr bool MORE = decltype(more_tag)::value;
-    constexpr bool FIRST = decltype(first_tag)::value;
-    constexpr bool EIN = decltype(ein_tag)::value;
-    constexpr bool EOUT = decltype(eout_tag)::value;
-    constexpr int P0 = EIN ? E : 0;
-    using NB = std::integral_constant<int, BUF ^ 1>;
-    using SB = std::integral_constant<int, BUF>;
-    Src sn{}, sn2{};
-    if constexpr (MORE) sn = srcs(t + 1);
-    if constexpr (EOUT) sn2 = srcs(t + 2);
-    // ---- block 0: MFMAs on F0 (k-steps 0, 1), F1 reads, DMA of tile t+1
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int ks = g >> 3, mb = (g >> 1) & 3, nb0 = 2 * (g & 1);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (FIRST && ks == 0) mma0(acc[mb][nb0 + u], f0[8 * ks + mb], f0[8 * ks + 4 + nb0 + u]);
-        else mma(acc[mb][nb0 + u], f0[8 * ks + mb], f0[8 * ks + 4 + nb0 + u]);
-      }
-      f1[g] = rd(buf_tag, 1, g);
-      if constexpr (MORE) {
-        if (P0 + g < 16) dma(sn, NB{}, P0 + g);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- block 1: MFMAs on F1 (k-steps 2, 3); barrier; F0 reads of tile t+1
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int ks = g >> 3, mb = (g >> 1) & 3, nb0 = 2 * (g & 1);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) mma(acc[mb][nb0 + u], f1[8 * ks + mb], f1[8 * ks + 4 + nb0 + u]);
-      if constexpr (MORE) {
-        if (g == BAR) {
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_barrier();
-        }
-        if (g > BAR) {
-          if constexpr (EOUT) dma(sn2, SB{}, g - BAR - 1);
-          constexpr int RPG = 16 / (15 - BAR);
-#pragma unroll
-          for (int u = 0; u < RPG; ++u) f0[RPG * (g - BAR - 1) + u] = rd(NB{}, 0, RPG * (g - BAR - 1) + u);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  // nk is even and ≥ 4 (host contract)
-  tile(0, B0{}, T_{}, T_{}, F_{}, T_{});
-  tile(1, B1{}, T_{}, F_{}, T_{}, T_{});
-  for (int t = 2; t < nk - 2; t += 2) {
-    tile(t, B0{}, T_{}, F_{}, T_{}, T_{});
-    tile(t + 1, B1{}, T_{}, F_{}, T_{}, T_{});
-  }
-  tile(nk - 2, B0{}, T_{}, F_{}, T_{}, F_{});
-  tile(nk - 1, B1{}, F_{}, F_{}, F_{}, F_{});
   }
 
   // ---- epilogue: acc[mb][nb][r] = C[m0 + wm·128 + 32mb + (r&3) + 8(r>>2) + 4hh][n0 + wn·128 + 32nb + (l&31)]
@@ -341,7 +265,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4_kernel(const bf16* __restric
 }
 
 // ============================================================================
-// The half-buffer-refill schedule on v_mfma_f32_16x16x32_bf16 (variant 3).
+// The half-buffer-refill schedule on v_mfma_f32_16x16x32_bf16 (variant 0, the default).
 // Same tile (256 × 256 per workgroup, 128 × 128 per wave), same DMA and
 // barriers; each wave's outputs are 8 × 8 accumulators of 16 × 16 (still 256
 // AGPRs), a 32-token block is ONE k-step (8 A + 8 B fragments, 64 MFMAs of
@@ -583,14 +507,10 @@ int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, i
     stride = (long long)M * N;
     acc = 0;
   }
-  if (variant == 1)
-    gemm_dw4_kernel<7><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
-  else if (variant == 2)  // half-buffer refill schedule (two barriers per tile, ≈1.5 tiles of DMA lead)
-    gemm_dw4_kernel<-1><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
-  else if (variant == 3)  // variant 2's schedule on 16x16x32 MFMAs
-    gemm_dw4m16_kernel<<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+  if (variant == 1)  // the same schedule on 32x32x16 MFMAs (A/B alternative)
+    gemm_dw4_kernel<<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   else
-    gemm_dw4_kernel<11><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+    gemm_dw4m16_kernel<<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   if (splits > 1) return splitk_add(ws, splits, (long long)M * N, C, accumulate, st);
   return 0;
 }

@@ -227,30 +227,20 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
-// impl 0 = the 8-wave ring below, impl v + 1 = gemm_nt4 schedule variant v,
-// impl 13 = per epilogue: the mirrored row-accumulator schedule (variant 11),
-// the unmirrored one (variant 9) for the GELU epilogue; impl 16 (default) =
-// persistent tiles, per K: unmirrored (variant 13) for K ≤ 1024, mirrored
-// (variant 12) above (tools/nt4_probe.py, profiles/r3_gemm_nt4_rows.md).
-// PDO_NT_IMPL overrides (A/B in the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=13 PDO_NT_IMPL=16')
+// impl 0 = the 8-wave ring below; impl 1 (default) = the 4-wave persistent
+// mainloop (gemm_nt4.hip) wherever K allows it; impl 2 = impl 1 with the
+// deferred store drain (its A/B alternative, profiles/r3_nt4_deferred_drain.md).
+// PDO_NT_IMPL overrides (A/B in the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=1 PDO_NT_IMPL=2')
 static int g_impl = [] {
   const char* e = getenv("PDO_NT_IMPL");
-  return e && *e ? atoi(e) : 16;
+  return e && *e ? atoi(e) : 1;
 }();
 
-static int nt4_variant(int epi, int K) {
-  if (g_impl == 13) return epi == 2 ? 9 : 11;
-  if (g_impl == 16) return K <= 1024 ? 13 : 12;
-  if (g_impl == 17) return K <= 1024 ? 15 : 14;  // impl 16 with the deferred store drain
-  return g_impl - 1;
-}
-
-// N % 256 = 128 (the 50304-column LM head) only on the 4-wave row-accumulator variants
+// N % 256 = 128 (the 50304-column LM head) only on the 4-wave mainloop
 static bool nt4_path(int K) { return g_impl >= 1 && K % 128 == 0 && K >= 256; }
 
 int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
-  const bool nok = N % BN == 0 || (N % BN == BN / 2 && nt4_path(K) && gemm_nt4_half_n(nt4_variant(0, K)) &&
-                                   gemm_nt4_half_n(nt4_variant(2, K)));
+  const bool nok = N % BN == 0 || (N % BN == BN / 2 && nt4_path(K));
   return M > 0 && N > 0 && K >= 64 && M % BM == 0 && nok && K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          ldc % 4 == 0 && lda >= K && ldb >= K && ldc >= N;
 }
@@ -266,7 +256,7 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
   if ((epi == 2 || epi == 3) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
   if (nt4_path(K))
-    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, nt4_variant(epi, K));
+    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, g_impl == 2 ? 1 : 0);
   const long long grid = (long long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;

@@ -39,11 +39,6 @@ void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, 
 void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* scratch, hipStream_t st);
 int bias_grad_scratch_floats(long long N, int F);
 int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st, int accumulate = 0);
-// hipBLASLt column-major matmul with epilogue (blaslt.hip); <0 = no solution
-int lt_matmul(int dev, int epi, int ta, int tb, long long m, long long n, long long k, const bf16* A, long long lda,
-              const bf16* B, long long ldb, bf16* D, long long ldd, const void* bias, int bias_is_f32, void* aux,
-              long long ldaux, void* ws, size_t ws_bytes, hipStream_t st);
-const char* lt_last_error();
 // NHWC BatchNorm (+ReLU, +residual) training forward / backward (batchnorm.hip)
 int bn_fwd_scratch_floats(long long M, int C);
 int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float* running_mean, float* running_var,
@@ -79,10 +74,9 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
 // gemm_nt4.hip: the same contract on the 4-wave / 128 × 128-per-wave mainloop
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
              const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant = 0);
-// the gemm_nt4 variants that also take N % 256 = 128 (half-width last tile column)
-int gemm_nt4_half_n(int variant);
-// which mainloop gemm_nt() runs: 0 = 8-wave ring (gemm_nt.hip), 1.. = 4-wave (gemm_nt4.hip)
-// schedule variant impl - 1
+// (N % 256 = 128 allowed: half-width last tile column; variant 1 = deferred store drain)
+// which mainloop gemm_nt() runs: 0 = 8-wave ring (gemm_nt.hip), 1 = 4-wave
+// (gemm_nt4.hip, default), 2 = 4-wave with the deferred store drain
 void gemm_nt_set_impl(int impl);
 int gemm_nt_get_impl();
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
@@ -129,5 +123,7 @@ int bucket_copy(int dtype, bool flatten, void* flat, long long total, int n, voi
                 hipStream_t st);
 int cast_scale_bf16_f32(const bf16* src, float* dst, long long n, float s, hipStream_t st);
 int scale_bf16(bf16* x, long long n, float s, hipStream_t st);
+int scale_dev_bf16(bf16* x, long long n, const float* s, hipStream_t st);
+int fold_zero_bf16(bf16* g, bf16* h, long long n, hipStream_t st);
 
 }  // namespace pdo

@@ -34,6 +34,16 @@ dead peer is the usual cause: its lease expires), otherwise count a restart
 (``max_restarts``) and bump ``inc`` so every peer re-forms the world.
 Workers resume from the newest checkpoint, whose flat-arena layout does not
 depend on the world size.
+
+xGMI layout (``--nproc-per-pod N``): a member is a pod holding N GPUs (one
+pod per node, ``amd.com/gpu: 8``), so RCCL connects its local ranks peer to
+peer over xGMI instead of through sockets between one-GPU pods.  ``np`` stays
+the pod count (the controller's ``worker.replicas``); each generation is a
+world of np·N ranks, pod rank p's local rank i being global rank p·N + i.  The
+agent never touches HIP: it forks its N workers fresh for every generation
+(new processes, so every RCCL communicator and HIP context is new), and the
+first local rank to fail takes its siblings down — a failure of the pod, as
+one worker's failure was with N = 1.
 """
 from __future__ import annotations
 
@@ -59,8 +69,9 @@ def _log(msg):
 
 class ElasticAgent:
     def __init__(self, kv: KVClient, job_id: str, member_id: int, host: str, port: int, np_default: int,
-                 timeout: float = 60.0, ttl: int = 6, poll: float = 0.25, max_restarts: int = 3):
+                 timeout: float = 60.0, ttl: int = 6, poll: float = 0.25, max_restarts: int = 3, nproc: int = 1):
         self.kv = kv
+        self.nproc = max(1, int(nproc))
         self.job = job_id
         self.id = int(member_id)
         self.host, self.port = host, int(port)
@@ -75,7 +86,7 @@ class ElasticAgent:
         self._ka = None
         self._lease_lost = threading.Event()
         self.reregistrations = 0
-        self.proc: Optional[subprocess.Popen] = None
+        self.procs: List[subprocess.Popen] = []
         self.history: List[dict] = []
 
     # ------------------------------------------------------------ membership
@@ -199,30 +210,48 @@ class ElasticAgent:
         return len(mem) < np_ or self.plan(np_, mem)[0] != world["gen"]
 
     # ------------------------------------------------------------ supervision
-    def spawn(self, world: dict, worker_argv: List[str]) -> subprocess.Popen:
-        env = dict(os.environ)
-        env.update({"RANK": str(world["rank"]), "WORLD_SIZE": str(world["np"]), "LOCAL_RANK": "0",
-                    "LOCAL_WORLD_SIZE": "1", "MASTER_ADDR": world["master_addr"],
-                    "MASTER_PORT": str(world["master_port"]), "PDO_ELASTIC_GEN": f"{world['gen']:08x}"})
-        cmd = [sys.executable, "-m", "paddle_operator_amd.launch", "--worker"] + worker_argv
-        # own session so stop_worker() can signal the worker's whole group; but
-        # a pod kill (SIGKILL to the agent's group, as a container runtime
-        # would kill the container) must take the worker down too
-        return subprocess.Popen(cmd, env=env, start_new_session=True, preexec_fn=_die_with_parent)
+    def spawn(self, world: dict, worker_argv: List[str]) -> List[subprocess.Popen]:
+        """This pod's nproc local ranks of generation ``world``."""
+        n = self.nproc
+        procs = []
+        for i in range(n):
+            env = dict(os.environ)
+            env.update({"RANK": str(world["rank"] * n + i), "WORLD_SIZE": str(world["np"] * n),
+                        "LOCAL_RANK": str(i), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": world["master_addr"],
+                        "MASTER_PORT": str(world["master_port"]), "PDO_ELASTIC_GEN": f"{world['gen']:08x}"})
+            cmd = [sys.executable, "-m", "paddle_operator_amd.launch", "--worker"] + worker_argv
+            # own session so stop_workers() can signal the worker's whole group; but
+            # a pod kill (SIGKILL to the agent's group, as a container runtime
+            # would kill the container) must take the worker down too
+            procs.append(subprocess.Popen(cmd, env=env, start_new_session=True, preexec_fn=_die_with_parent))
+        return procs
 
-    def stop_worker(self, grace: float = 20.0):
-        p = self.proc
-        if p is None or p.poll() is not None:
-            return
-        try:
-            os.killpg(p.pid, signal.SIGTERM)
-        except ProcessLookupError:
-            return
-        try:
-            p.wait(grace)
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            p.wait()
+    def poll_workers(self) -> Optional[int]:
+        """None while any local rank runs and none failed; else the pod's exit
+        status — 0 once every local rank finished, or the first failure's."""
+        rcs = [p.poll() for p in self.procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            return bad[0]
+        return 0 if all(rc == 0 for rc in rcs) else None
+
+    def stop_workers(self, grace: float = 20.0):
+        live = [p for p in self.procs if p.poll() is None]
+        for p in live:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        t_end = time.time() + grace
+        for p in live:
+            try:
+                p.wait(max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
 
     def run(self, worker_argv: List[str]) -> int:
         self.register()
@@ -234,21 +263,23 @@ class ElasticAgent:
                 if world is None:
                     _log(f"rendezvous timed out after {self.timeout}s")
                     return 3
-                _log(f"gen {world['gen']:08x}: rank {world['rank']}/{world['np']} master "
-                     f"{world['master_addr']}:{world['master_port']} (rdzv {time.time() - t0:.2f}s)")
+                _log(f"gen {world['gen']:08x}: pod rank {world['rank']}/{world['np']} × {self.nproc} local "
+                     f"master {world['master_addr']}:{world['master_port']} (rdzv {time.time() - t0:.2f}s)")
                 self.history.append(world)
-                self.proc = self.spawn(world, worker_argv)
+                self.procs = self.spawn(world, worker_argv)
                 while True:
-                    rc = self.proc.poll()
+                    rc = self.poll_workers()
                     if rc is not None:
                         break
                     self.ensure_registered()
                     if self.changed(world):
                         if self.gen_done(world):
-                            rc = self.proc.wait()  # generation completed: let this worker finish too
+                            # generation completed: let this pod's workers finish too
+                            rcs = [p.wait() for p in self.procs]
+                            rc = next((r for r in rcs if r), 0)
                             break
-                        _log("membership/np changed → stopping worker for re-rendezvous")
-                        self.stop_worker()
+                        _log("membership/np changed → stopping workers for re-rendezvous")
+                        self.stop_workers()
                         rc = None
                         break
                     time.sleep(self.poll)
@@ -257,6 +288,7 @@ class ElasticAgent:
                 if rc == 0:
                     self.kv.put(self.prefix + f"done/{self.id:06d}", json.dumps({"gen": world["gen"]}))
                     return 0
+                self.stop_workers(5.0)  # a failed local rank takes its siblings down
                 # a dead peer usually takes this worker down with it before
                 # its lease has expired: give the membership one TTL to move
                 t_end = time.time() + self.ttl + 2 * self.poll
@@ -271,7 +303,7 @@ class ElasticAgent:
                     return rc
                 self.bump()
         finally:
-            self.stop_worker(5.0)
+            self.stop_workers(5.0)
             self.deregister()
 
 
@@ -285,7 +317,21 @@ def _die_with_parent():
 
 
 def _strip(argv: List[str]) -> List[str]:
-    return [a for a in argv if a not in ("--elastic", "--worker")]
+    """Worker argv: the agent's own flags removed (each worker is one rank)."""
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a in ("--elastic", "--worker"):
+            continue
+        if a == "--nproc-per-pod":
+            skip = True
+            continue
+        if a.startswith("--nproc-per-pod="):
+            continue
+        out.append(a)
+    return out
 
 
 def run_agent(args, jenv, argv: List[str]) -> int:
@@ -294,6 +340,6 @@ def run_agent(args, jenv, argv: List[str]) -> int:
         raise SystemExit("elastic mode needs PADDLE_ELASTIC_SERVER (or PDO_KV)")
     agent = ElasticAgent(KVClient(eps), jenv.elastic_job_id or jenv.job_key(), jenv.trainer_id, jenv.pod_ip,
                          jenv.port, jenv.elastic_np or jenv.trainers_num, timeout=float(jenv.elastic_timeout),
-                         ttl=int(os.environ.get("PDO_ELASTIC_TTL", "6")))
+                         ttl=int(os.environ.get("PDO_ELASTIC_TTL", "6")), nproc=getattr(args, "nproc_per_pod", 1))
     signal.signal(signal.SIGTERM, lambda *a: sys.exit(143))
     return agent.run(_strip(argv))

@@ -253,7 +253,10 @@ def _comm_diag(trainer, fence, dev, step_s, nosync_steps=3, iters=10):
     flat = getattr(trainer, "flat", None)
     if flat is not None and getattr(flat, "buckets", None):
         esz = flat.params.element_size()
-        out["buckets"] = {"count": len(flat.buckets), "bytes": [int(bk.numel * esz) for bk in flat.buckets]}
+        out["buckets"] = {"count": len(flat.buckets), "bytes": [int(bk.numel * esz) for bk in flat.buckets],
+                          # split tied weights: their head-gradient slot is bucket 0
+                          "split": [a.name for a in getattr(flat, "aux_slots", [])],
+                          "first": [s.name for s in flat.buckets[0].slots][:4]}
     sizes_mib = (4, 8, 16, 32, 64, 128, 256) if dev.type == "cuda" else (1, 2, 4, 8)
     buf = torch.ones((max(sizes_mib) << 20) // 2, dtype=torch.bfloat16, device=dev)
     sweep = []
@@ -309,11 +312,29 @@ def spawn_local(args, jenv, argv) -> int:
     if ids and len(ids) < n:
         raise RuntimeError(f"--nproc-per-pod {n} but the pod was given {len(ids)} GPU(s) ({gpus})")
     kids = {}
+
+    def forward(signum, frame):
+        for p in kids:
+            try:
+                os.killpg(p, signum)
+            except ProcessLookupError:
+                pass
+    # forwarding is in place before the first fork, and the signals are held
+    # while the loop forks: a SIGTERM during startup (pod deleted while its ranks
+    # launch) reaches every rank already forked instead of killing the supervisor
+    # with the default action and orphaning them
+    sigs = {signal.SIGTERM, signal.SIGINT}
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    signal.pthread_sigmask(signal.SIG_BLOCK, sigs)
     for i in range(n):
         env = jenv.torch_env(i, n)
         pid = os.fork()
         if pid == 0:
             os.setpgid(0, 0)
+            signal.signal(signal.SIGTERM, signal.SIG_DFL)
+            signal.signal(signal.SIGINT, signal.default_int_handler)
+            signal.pthread_sigmask(signal.SIG_UNBLOCK, sigs)
             os.environ.update(env)
             os.environ["PDO_LOCAL_CHILD"] = "1"
             try:
@@ -329,16 +350,12 @@ def spawn_local(args, jenv, argv) -> int:
             sys.stderr.flush()
             os._exit(int(rc or 0))
         kids[pid] = i
+        try:  # parent side too: no window where a forwarded signal misses the new group
+            os.setpgid(pid, pid)
+        except OSError:
+            pass
+    signal.pthread_sigmask(signal.SIG_UNBLOCK, sigs)
     log(f"pod {jenv.trainer_id}: {n} local ranks {env['WORLD_SIZE']}-world, pids {list(kids)}")
-
-    def forward(signum, frame):
-        for p in kids:
-            try:
-                os.killpg(p, signum)
-            except ProcessLookupError:
-                pass
-    signal.signal(signal.SIGTERM, forward)
-    signal.signal(signal.SIGINT, forward)
     rc = 0
     while kids:
         pid, status = os.wait()
@@ -434,10 +451,10 @@ def main(argv=None) -> int:
     jenv.check_supported()
     log(f"role={jenv.role} id={jenv.trainer_id} mode={jenv.mode} elastic={jenv.elastic} workload={args.workload}")
     ps = jenv.mode == "PS" or args.workload in ("wide_deep", "deepfm") and jenv.pserver_endpoints
-    if args.nproc_per_pod > 1 and not ps and os.environ.get("PDO_LOCAL_CHILD") != "1":
-        if jenv.elastic or args.elastic:
-            raise NotImplementedError("--nproc-per-pod > 1 with an elastic job: one rank per pod there")
+    if (args.nproc_per_pod > 1 and not ps and os.environ.get("PDO_LOCAL_CHILD") != "1"
+            and not (jenv.elastic or args.elastic)):
         return spawn_local(args, jenv, argv)  # before any thread or HIP call in this process
+    # elastic + --nproc-per-pod N: the agent below forks N fresh local ranks per generation
     _hang_dump()
     if ps:
         return run_ps(args, jenv)

@@ -93,8 +93,20 @@ SLOT_RESPAWN = os.environ.get("PDO_SLOT_RESPAWN", "handoff")
 # right after another on the same GPU finds its slot still re-warming (HIP +
 # RCCL init, ≈ 1 s: bench.py 'ready_b2b'); a second slot serves it warm.  Each
 # slot holds a HIP context and a 1-rank communicator on the GPU ('mem_mb' in
-# the status table, well under 1 GB of the 288 GB).
-SLOTS_PER_GPU = max(1, int(os.environ.get("PDO_SLOTS_PER_GPU", "2")))
+# the status table, well under 1 GB of the 288 GB).  Unset, the default follows
+# the number of warm devices (slots_per_gpu): two up to 2 GPUs, one above, so a
+# full 8-GPU node runs at most rank + slot = 2 processes per GPU — the layout
+# bench.py measures.
+_SLOTS_ENV = os.environ.get("PDO_SLOTS_PER_GPU", "")
+
+
+def slots_per_gpu(n_devices: int) -> int:
+    if _SLOTS_ENV.strip():
+        return max(1, int(_SLOTS_ENV))
+    return 2 if n_devices <= 2 else 1
+
+
+SLOTS_PER_GPU = slots_per_gpu(1)
 
 
 def runtime_key(env: Dict[str, str]) -> tuple:
@@ -297,12 +309,13 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
     signal.signal(signal.SIGTERM, lambda *a: stop.append(1))
     last_activity = time.time()
     key = runtime_key(dict(os.environ))
-    slots: Dict[str, List[_Slot]] = {}  # device -> its warm slots (≤ SLOTS_PER_GPU)
+    slots: Dict[str, List[_Slot]] = {}  # device -> its warm slots (≤ per_gpu)
     slot_pids: Dict[int, _Slot] = {}
     slot_fails: Dict[str, int] = {}
     pending: Dict[str, list] = {}      # device -> [(conn, req, fds, t_park)] waiting for a warming slot
     rank_dev: Dict[int, str] = {}      # rank pid -> GPU whose slot it took (SLOT_RESPAWN = exit)
     served = {"warm": 0, "cold": 0, "park_timeouts": 0, "warm_timeouts": 0}
+    per_gpu = slots_per_gpu(len(warm_devices or ()))
 
     def log(msg):
         print(f"[pdo-zygote] {msg}", flush=True)
@@ -311,7 +324,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
         return next((s for s in slots.get(dev, ()) if s.ready), None)
 
     def spawn_slot(dev):
-        if stop or slot_fails.get(dev, 0) >= SLOT_RETRIES or len(slots.get(dev, ())) >= SLOTS_PER_GPU:
+        if stop or slot_fails.get(dev, 0) >= SLOT_RETRIES or len(slots.get(dev, ())) >= per_gpu:
             return
         a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_STREAM)
         pid = os.fork()
@@ -419,13 +432,13 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                     "n_ready": sum(x.ready for x in lst), **(sl.info or last_info.get(d, {}))}
         return {"pid": os.getpid(), "served": served,
                 "slots": {d: one(d, lst) for d, lst in slots.items() if lst},
-                "slots_per_gpu": SLOTS_PER_GPU,
+                "slots_per_gpu": per_gpu,
                 "respawn": SLOT_RESPAWN, "park_s": SLOT_PARK_S,
                 "devices": list(warm_devices or []), "failed": slot_fails}
 
     last_info = {}
     for dev in warm_devices or []:
-        for _ in range(SLOTS_PER_GPU):
+        for _ in range(per_gpu):
             spawn_slot(dev)
     while not stop:
         for skey, _ in sel.select(timeout=0.01):

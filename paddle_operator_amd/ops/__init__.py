@@ -155,12 +155,14 @@ def add_layer_norm(x, r, w, b, eps=1e-5, rbias=None):
 # ----------------------------------------------------------------------------
 
 class _LinearFn(torch.autograd.Function):
-    """y = x W^T (+ b) on hipBLASLt (bias fused in the GEMM epilogue).
+    """y = x W^T (+ b) on the hand-written gemm_nt (csrc/hip/gemm_nt4.hip, bias
+    fused in the register epilogue) where its shape contract holds.
 
-    Backward writes dW straight into the parameter's slice of the flat
-    gradient arena (``addmm_`` with beta=1 — no separate gradient tensor, no
-    AccumulateGrad add kernel) and then signals the bucketed all-reduce that
-    the parameter is ready.  The bias gradient is a HIP column reduction."""
+    Backward: dX on gemm_nt (as F.linear(dY, Wᵀ)), dW on gemm_dw4 written
+    straight into the parameter's slice of the flat gradient arena (no
+    separate gradient tensor, no AccumulateGrad add kernel), then the bucketed
+    all-reduce is signalled that the parameter is ready.  The bias gradient is
+    a HIP column reduction."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -249,13 +251,11 @@ def _fwd_gemm(x, w, b=None):
 
 
 def _input_grad(dy2, w):
-    """dX = dY·W as the forward's GEMM form F.linear(dY, Wᵀ).
+    """dX = dY·W as the forward's GEMM form F.linear(dY, Wᵀ) on gemm_nt.
 
-    hipBLASLt's gfx950 kernels for the "NN" layout of dY·W reach 1.1-1.3 PF on
-    these shapes, the forward's "TN" family 1.35-1.9 PF (tuned tables).  The
-    explicit Wᵀ copy is ≤ 8 M elements per projection; it runs in the LDS-tiled
-    HIP transpose (csrc/hip/transpose.hip) at the HBM rate — PyTorch's strided
-    copy took ≈25 µs per projection weight, 2.4 ms per GPT-2-medium step."""
+    gemm_nt reads both operands K-contiguous; the explicit Wᵀ copy is ≤ 8 M
+    elements per projection and runs in the LDS-tiled HIP transpose
+    (csrc/hip/transpose.hip) at the HBM rate."""
     if _DX_TN[0] and dy2.is_cuda:
         return _fwd_gemm(dy2, transpose(w))
     return dy2 @ w
@@ -393,78 +393,10 @@ class _BiasGeluFn(torch.autograd.Function):
         return dx.view(ctx.shape), db
 
 
-class _NoFusedEpilogue(RuntimeError):
-    pass
-
-
-_ZB = {}
-
-
-def _zeros_like_bias(b):
-    z = _ZB.get((b.device, b.numel()))
-    if z is None:
-        z = torch.zeros_like(b)
-        _ZB[(b.device, b.numel())] = z
-    return z
-
-
-class _MLPFn(torch.autograd.Function):
-    """m = gelu(x·W1ᵀ + b1)·W2ᵀ — the GPT-2 MLP without its output bias (folded
-    into the next add+LayerNorm).  Both GELU passes run inside hipBLASLt
-    epilogues (csrc/hip/blaslt.hip): fc1 forward = GELU_AUX_BIAS (writes h
-    and the pre-activation), fc2's input-gradient GEMM = DGELU_BGRAD (writes
-    dh_pre and db1).  No standalone bias-GELU kernels, one fewer pass over the
-    [tokens, 4C] activation each way."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2):
-        m = _native.require_hip()
-        x2 = x.reshape(-1, x.shape[-1])
-        r = m.linear_gelu(x2, w1, b1)
-        if r:
-            h, hp = r
-        else:
-            # gfx950 hipBLASLt has no GELU_AUX_BIAS: bias in the GEMM epilogue
-            # (hp = x·W1ᵀ + b1 is the aux the backward's DGELU epilogue reads), GELU by HIP
-            hp = F.linear(x2, w1, b1)
-            h = m.bias_gelu_fwd(hp, _zeros_like_bias(b1))
-        y = h @ w2.t()
-        ctx.save_for_backward(x2, w1, w2, h, hp)
-        ctx.shape = x.shape
-        return y.view(*x.shape[:-1], w2.shape[0])
-
-    @staticmethod
-    def backward(ctx, dy):
-        m = _native.require_hip()
-        x2, w1, w2, h, hp = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        dw2 = _weight_grad(w2, dy2, h) if ctx.needs_input_grad[3] else None
-        r = m.matmul_dgelu(dy2, w2, hp)
-        if r:
-            dh, db1 = r
-        else:  # no DGELU epilogue: plain GEMM + HIP bias-GELU backward on the post-bias pre-activation
-            dh, db1 = m.bias_gelu_bwd((dy2 @ w2).contiguous(), hp, _zeros_like_bias(b1_like(w1)))
-        dw1 = _weight_grad(w1, dh, x2) if ctx.needs_input_grad[1] else None
-        dx = _input_grad(dh, w1).view(ctx.shape) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1, dw2
-
-
-# Off by default (measured on gfx950, ROCm 7.2 hipBLASLt): GELU_AUX_BIAS has no
-# solution at any GPT-2 shape, DGELU_BGRAD only for small n, and the DGELU-only
-# path ran the whole step at 299k vs 373k tok/s unfused (slow epilogue
-# kernels) with a derivative that disagrees with tanh-GELU (tests/test_ops_gpu.py
-# test_gpt2_tiny_hip_vs_torch).  The HIP bias-GELU kernels run at HBM roofline.
-_FUSED_MLP = [os.environ.get("PDO_FUSED_MLP", "0") == "1"]
-
-
-def b1_like(w1):
-    return w1[:, 0]
-
-
 class _GeluLinearFn(torch.autograd.Function):
     """y = gelu(hp + b1)·W2ᵀ, the back half of the GPT-2 MLP.
 
-    Forward is the HIP bias-GELU kernel + hipBLASLt.  Backward runs fc2's
+    Forward is the HIP bias-GELU kernel + gemm_nt.  Backward runs fc2's
     input-gradient GEMM on gemm_nt (csrc/hip/gemm_nt.hip) with the bias-GELU
     backward fused into its epilogue — dhp = (dY·W2) ⊙ gelu'(hp + b1) and the
     b1 gradient from the tile's fp32 column partials — so the [tokens, 4C]
@@ -562,14 +494,9 @@ def _nt_dgelu_ok(hp, w2) -> bool:
 
 
 def mlp(x, w1, b1, w2):
-    """GPT-2 MLP branch without the output bias (see _MLPFn)."""
-    if use_hip(x) and _FUSED_MLP[0]:
-        try:
-            return _MLPFn.apply(x, w1, b1, w2)
-        except _NoFusedEpilogue as e:
-            _FUSED_MLP[0] = False
-            if os.environ.get("PDO_VERBOSE"):
-                print(f"[pdo] fused MLP disabled: {e}")
+    """GPT-2 MLP branch without the output bias (folded into the next
+    add+LayerNorm): both GELU passes inside gemm_nt epilogues (_NTMLPFn) where
+    the shapes allow, else the HIP bias-GELU kernels around plain GEMMs."""
     if (_NT_GELU[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.is_contiguous()
             and _nt_dgelu_ok(x, w2)
             and _native.require_hip().gemm_nt_supported(x.numel() // x.shape[-1], w1.shape[0], w1.shape[1])):
@@ -733,7 +660,11 @@ class _LMHeadXentFn(torch.autograd.Function):
         inv_cnt = (1.0 / valid.clamp(min=1.0)).reshape(1)
         logits = torch.empty(chunk, Vp, device=h.device, dtype=h.dtype)
         dh = torch.empty_like(h2)
-        dw = torch.empty(Vp, C, device=h.device, dtype=h.dtype)
+        # a split tied weight (parallel/flat.py): dW goes straight into its
+        # head-gradient arena slot, all-reduced as bucket 0 once the backward starts
+        sp = getattr(w, "_pdo_split", None)
+        ctx.split = sp
+        dw = sp.grad if sp is not None else torch.empty(Vp, C, device=h.device, dtype=h.dtype)
         loss_sum = torch.zeros((), device=h.device, dtype=torch.float32)
         for c0 in range(0, N, chunk):
             hc, tc = h2[c0:c0 + chunk], t[c0:c0 + chunk]
@@ -754,15 +685,72 @@ class _LMHeadXentFn(torch.autograd.Function):
                     dw.copy_(dl.t() @ hc)
                 else:
                     dw.addmm_(dl.t(), hc)
-        ctx.save_for_backward(dh, dw)
+        ctx.save_for_backward(dh, dw if sp is None else None)
         ctx.shape = h.shape
         return loss_sum if fused else loss_sum / valid
 
     @staticmethod
     def backward(ctx, dloss):
         dh, dw = ctx.saved_tensors
-        d = dloss.to(dh.dtype)
-        return (dh * d).view(ctx.shape), dw * d, None, None, None
+        # scaled in fp32, rounded once: a non-unit dloss (1/accum_steps) is not
+        # first rounded to bf16
+        d = dloss.float()
+        sp = ctx.split
+        if sp is not None:
+            _native.require_hip().scale_dev_(sp.grad, d.reshape(1).contiguous())
+            sp.ready(sp)
+            return (dh.float() * d).to(dh.dtype).view(ctx.shape), None, None, None, None
+        return ((dh.float() * d).to(dh.dtype).view(ctx.shape), (dw.float() * d).to(dw.dtype),
+                None, None, None)
+
+
+class _SplitHeadLinearFn(torch.autograd.Function):
+    """logits = h·Wᵀ for a split tied weight outside _LMHeadXentFn's contract
+    (CPU, unsupported shapes): the backward adds dW into the weight's
+    head-gradient slot (parallel/flat.py AuxGrad) and signals it ready, instead
+    of accumulating into the gradient the embedding also writes."""
+
+    @staticmethod
+    def forward(ctx, h, w, sp):
+        ctx.save_for_backward(h, w)
+        ctx.sp = sp
+        return _fwd_gemm(h, w) if h.is_cuda else F.linear(h, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, w = ctx.saved_tensors
+        sp = ctx.sp
+        V, C = w.shape
+        dy2 = dy.reshape(-1, V)
+        h2 = h.reshape(-1, C)
+        dh = (_input_grad(dy2.contiguous(), w) if dy.is_cuda else dy2 @ w).view(h.shape)
+        g = sp.grad.view(V, C)
+        if not (dy.is_cuda and dy2.dtype == torch.bfloat16 and _HIP_DW[0] and dy2.is_contiguous()
+                and h2.is_contiguous() and _native.require_hip().gemm_dw(dy2, h2, g, True)):
+            g.addmm_(dy2.t().to(g.dtype), h2.to(g.dtype))
+        sp.ready(sp)
+        return dh, None, None
+
+
+def _lm_head_loss_only(h, w, target, vocab: int, chunk: int):
+    """Loss of the tied LM head without gradients (no_grad / eval): the logits
+    GEMM and the statistics pass per chunk — no dX / dW GEMMs, no [Vp, C]
+    gradient buffer."""
+    m = _native.require_hip()
+    h2 = h.reshape(-1, h.shape[-1])
+    t = target.reshape(-1)
+    N = h2.shape[0]
+    logits = torch.empty(min(chunk, N), w.shape[0], device=h.device, dtype=h.dtype)
+    loss_sum = torch.zeros((), device=h.device, dtype=torch.float32)
+    cnt = torch.zeros((), device=h.device, dtype=torch.float32)
+    for c0 in range(0, N, chunk):
+        hc, tc = h2[c0:c0 + chunk], t[c0:c0 + chunk]
+        lg = logits[:hc.shape[0]]
+        m.gemm_nt(hc, w, None, lg)
+        _, _, st = m.xent_fwd(lg, tc, vocab)  # (chunk mean loss, chunk valid count)
+        loss_sum += st[0] * st[1]
+        cnt += st[1]
+    return loss_sum / cnt.clamp(min=1.0)
 
 
 # PDO_LM_CHUNK=tokens: the chunked LM head + cross-entropy (_LMHeadXentFn); -1
@@ -787,7 +775,12 @@ def lm_head_xent(h, w, target, vocab: int):
             and h.is_contiguous() and w.is_contiguous()
             and _native.require_hip().gemm_nt_supported(ch, w.shape[0], w.shape[1])
             and _native.require_hip().gemm_nt_supported(ch, w.shape[1], w.shape[0])):
+        if not (torch.is_grad_enabled() and (h.requires_grad or w.requires_grad)):
+            return _lm_head_loss_only(h, w, target, vocab, ch)
         return _LMHeadXentFn.apply(h, w, target, vocab, ch)
+    sp = getattr(w, "_pdo_split", None)
+    if sp is not None and torch.is_grad_enabled() and w.requires_grad:
+        return cross_entropy(_SplitHeadLinearFn.apply(h, w, sp), target, vocab)
     return cross_entropy(linear(h, w), target, vocab)
 
 

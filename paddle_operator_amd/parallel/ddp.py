@@ -11,6 +11,11 @@ NCCL all-reduce to the Paddle image).  Design for MI355X:
   its own HIP stream, overlapping the backward GEMMs of the earlier layers;
 * bucket size: ``utils.topology.bucket_bytes_for`` (a link-model heuristic,
   see its docstring; the callers pass it in);
+* the tied embedding's gradient is split (``FlatParams(split=("wte",))``): the
+  LM-head half is bucket 0, all-reduced as soon as the LM head's backward has
+  written it, so it overlaps the whole backward instead of waiting for the
+  embedding backward at the very end (the last bucket keeps only the
+  embedding half);
 * reduction precision (``grad_reduce``):
 
   - ``"bf16"`` (default for a bf16 arena): RCCL sums the bf16 bucket in
@@ -79,6 +84,8 @@ class BucketedDDP:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._hook))
                 # ops that write gradients straight into the arena signal here
                 s.param._pdo_ready = self._hook
+            for a in flat.aux_slots:  # a split parameter's head-gradient slot (bucket 0)
+                a.param.ready = self._hook
 
     # -- API --------------------------------------------------------------
     def broadcast_params(self, src: int = 0):
@@ -107,16 +114,17 @@ class BucketedDDP:
         self._staged = False
 
     def finish(self):
-        """Call after backward: launch stragglers, make the compute stream wait."""
-        if not (self.enabled and self._sync):
-            return
-        while self._next < len(self.flat.buckets):
-            self._launch(self._next)
-        for w in self._works:
-            w.wait()
-        self._works = []
-        if self._staged:
-            self._cast_back()
+        """Call after backward: launch stragglers, make the compute stream wait,
+        then fold split parameters' head-gradient slots into their gradients."""
+        if self.enabled and self._sync:
+            while self._next < len(self.flat.buckets):
+                self._launch(self._next)
+            for w in self._works:
+                w.wait()
+            self._works = []
+            if self._staged:
+                self._cast_back()
+        self.flat.fold_split()
 
     @property
     def grad_scale(self) -> float:

@@ -15,7 +15,14 @@ SURVEY §2.4 "GPU collectives — no call site in the reference"):
   k+1 and the all-reduce of bucket k overlaps the backward of the layers below;
 * every parameter starts on a ``ALIGN``-element boundary (2 KiB in bf16): 16-B
   vector loads are always aligned and the per-chunk weight-decay table needs
-  one float per ``ALIGN`` elements.
+  one float per ``ALIGN`` elements;
+* ``split`` names (the tied ``wte``): the parameter's gradient has two
+  producers far apart in the backward — the LM head (first node of the
+  backward) and the embedding (last).  The LM-head part gets its own arena slot
+  at the FRONT of the ready order (``AuxGrad``, bucket 0), so its all-reduce
+  overlaps the whole backward; only the embedding part stays in the last
+  bucket.  ``fold_split()`` adds the reduced head part into the parameter's
+  gradient and zeroes the slot (the optimizer never sees it).
 """
 from __future__ import annotations
 
@@ -57,6 +64,19 @@ def _noop_ready(p):
     return None
 
 
+class AuxGrad:
+    """Second gradient slot of a ``split`` parameter (see module docstring).
+
+    ``grad`` is its arena view (same shape as the parameter); the op that
+    produces this part of the gradient writes (or adds) into it and calls
+    ``ready(self)`` — BucketedDDP counts it like a parameter of bucket 0."""
+
+    def __init__(self, name: str, grad: torch.Tensor):
+        self.name = name
+        self.grad = grad
+        self.ready = _noop_ready
+
+
 def default_no_decay(name: str, p: torch.Tensor) -> bool:
     """Biases, norm weights and 1-D params are not decayed."""
     return p.dim() < 2
@@ -66,7 +86,7 @@ class FlatParams:
     """Owns the flat buffers of a model. See module docstring."""
 
     def __init__(self, model: nn.Module, dtype=torch.bfloat16, device=None,
-                 bucket_bytes: int = 64 << 20, late: tuple = (), no_decay=default_no_decay):
+                 bucket_bytes: int = 64 << 20, late: tuple = (), no_decay=default_no_decay, split: tuple = ()):
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         if not named:
             raise ValueError("model has no trainable parameters")
@@ -79,7 +99,17 @@ class FlatParams:
         self.dtype = dtype
         self.device = device
         self.slots: list[Slot] = []
+        # split parameters' second gradient slots first (ready first: bucket 0)
+        params = dict(named)
+        unknown = set(split) - set(params)
+        if unknown:
+            raise ValueError(f"split names not among the trainable parameters: {sorted(unknown)}")
+        self.aux_slots: list[Slot] = []
         off = 0
+        for n in split:
+            p = params[n]
+            self.aux_slots.append(Slot(n + "#head", None, off, p.numel(), p.shape, False))
+            off = _round_up(off + p.numel(), ALIGN)
         for n, p in order:
             self.slots.append(Slot(n, p, off, p.numel(), p.shape, not no_decay(n, p)))
             off = _round_up(off + p.numel(), ALIGN)
@@ -103,6 +133,12 @@ class FlatParams:
             # in several places (tied embeddings) keep autograd accumulation
             s.param._pdo_direct = s.name not in late_set
             s.param._pdo_ready = _noop_ready
+            s.param._pdo_split = None
+        by_name = {s.name: s for s in self.slots}
+        for a in self.aux_slots:
+            owner = by_name[a.name[:-len("#head")]]
+            a.param = AuxGrad(a.name, self._view(self.grads, a))
+            owner.param._pdo_split = a.param
         # one weight-decay flag per ALIGN-element chunk
         wd = torch.zeros(off // ALIGN, dtype=torch.float32)
         for s in self.slots:
@@ -122,7 +158,7 @@ class FlatParams:
         esz = torch.empty((), dtype=self.dtype).element_size()
         cap = max(ALIGN, bucket_bytes // esz)
         buckets, cur = [], None
-        for s in self.slots:
+        for s in self.aux_slots + self.slots:
             if cur is None:
                 cur = Bucket(len(buckets), s.offset, s.offset)
             cur.slots.append(s)
@@ -144,8 +180,25 @@ class FlatParams:
     def zero_grad(self):
         self.grads.zero_()
 
+    def fold_split(self):
+        """Add each split parameter's head slot into its gradient and zero the
+        slot (after the all-reduce drain; every micro-step, so gradient
+        accumulation under no_sync sums both parts)."""
+        for a in self.aux_slots:
+            owner = next(s for s in self.slots if s.name == a.name[:-len("#head")])
+            g = self._view(self.grads, owner).view(-1)
+            h = self.grads[a.offset:a.offset + a.numel]
+            if g.is_cuda and g.dtype == torch.bfloat16:
+                from .. import _native
+                _native.require_hip().fold_zero(g, h)
+            else:
+                g.add_(h)
+                h.zero_()
+
     def rebind_grads(self):
         """Re-point .grad at the arena (after anything replaced it)."""
+        for a in self.aux_slots:
+            a.param.grad = self._view(self.grads, a)
         for s in self.slots:
             g = s.param.grad
             view = self._view(self.grads, s)

@@ -95,7 +95,12 @@ class GPT2Trainer:
             bucket_bytes = bucket_bytes_for(world, nbytes)
         else:
             bucket_bytes = bucket_mb << 20
-        self.flat = FlatParams(model, dtype=dtype, device=self.device, bucket_bytes=bucket_bytes, late=("wte",))
+        # the tied wte gradient in two slots: the LM-head half is bucket 0 (its
+        # all-reduce overlaps the whole backward), the embedding half the last
+        # bucket (PDO_SPLIT_WTE=0: one slot, all of it in the last bucket)
+        split = ("wte",) if os.environ.get("PDO_SPLIT_WTE", "1") != "0" else ()
+        self.flat = FlatParams(model, dtype=dtype, device=self.device, bucket_bytes=bucket_bytes, late=("wte",),
+                               split=split)
         self.ddp = BucketedDDP(self.flat)
         self.opt = FlatAdamW(self.flat, lr=lr)
         self.gen = torch.Generator(device=self.device)

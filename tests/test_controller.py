@@ -445,6 +445,63 @@ def test_exec_agent_elastic_scale_kill_scale_in(tmp_path):
         cl.stop()
 
 
+def test_exec_agent_elastic_nproc_per_pod_2(tmp_path):
+    """Elastic jobs in the xGMI layout: pods of 2 local ranks each (the
+    one-pod-per-node layout, --nproc-per-pod N).  np counts pods; each
+    generation is a world of np × 2 ranks, forked fresh by every pod's agent.
+    Scale 2 → 3 pods (world 4 → 6), kill a pod (its agent and both of its
+    ranks; OnFailure restarts it in place), scale back to 2 (world 4); every
+    re-formed world resumes from the newest checkpoint."""
+    port = _free_port()
+    cl = LocalCluster(mode="fast", agent="exec", sandbox_root=str(tmp_path), elastic_kv=True,
+                      kv_endpoint=f"127.0.0.1:{port}")
+    cl.serve(f"127.0.0.1:{port}")
+    args = ["--workload", "resnet50", "--tiny", "--steps", "90", "--throttle-ms", "60", "--nproc-per-pod", "2",
+            "--ckpt-dir", str(tmp_path / "ckpt"), "--ckpt-every", "5"]
+    cont = _launcher_container(args)
+    cont["env"] = [e for e in cont["env"] if e["name"] != "OMP_NUM_THREADS"] + [
+        {"name": "OMP_NUM_THREADS", "value": "1"}, {"name": "PDO_ELASTIC_TTL", "value": "2"}]
+    cl.create(T.paddlejob("en", worker={"replicas": 2, "template": {"spec": {"containers": [cont]}}}, elastic=1,
+                          clean_pod_policy="Never"))
+
+    def log(i):
+        d = cl.sandbox(f"en-worker-{i}")
+        p = os.path.join(d, "paddle.log") if d else ""
+        return open(p).read() if p and os.path.exists(p) else ""
+
+    def world(n):  # every rank of one n-rank generation reported ready → its gen
+        recs = [_ready_rec(cl, "en", r) or {} for r in range(n)]
+        return recs[0]["gen"] if all(r.get("world") == n for r in recs) and \
+            len({r.get("gen") for r in recs}) == 1 else None
+
+    try:
+        assert cl.wait(lambda: world(4) is not None, timeout=150), log(0)[-3000:]
+        assert cl.wait(lambda: list((tmp_path / "ckpt").glob("ckpt-*.pt")), timeout=120)
+        cl.scale("en", "worker", 3)
+        assert cl.wait(lambda: world(6) is not None, timeout=150), log(0)[-3000:]
+        gen_before = world(6)
+        # the scaled-in generation's ranks: pod p holds global ranks 2p, 2p + 1
+        recs = [_ready_rec(cl, "en", r) for r in range(6)]
+        assert [r["local_rank"] for r in recs] == [0, 1] * 3, recs
+        # pod kill: SIGKILL to en-worker-1's process group (agent + both local ranks)
+        assert cl.kill("en-worker-1", 9)
+        assert cl.wait(lambda: world(6) not in (None, gen_before), timeout=150), log(0)[-3000:]
+        assert cl.get("Pod", "en-worker-1")["status"]["containerStatuses"][0]["restartCount"] >= 1
+        cl.scale("en", "worker", 2)
+        ok = cl.wait_phase("en", T.Phase.Completed, timeout=240)
+        assert ok, (cl.job("en")["status"], log(0)[-3000:], log(1)[-3000:])
+        assert cl.kv_get("/paddle/default-en/np") == "2"
+        readies = [json.loads(l[10:]) for i in range(2) for l in log(i).splitlines()
+                   if l.startswith("PDO_READY ")]
+        worlds = [r["world"] for r in readies if r["rank"] == 0]
+        # 4 ranks, 6, 6 again after the kill, 4 after the scale-in
+        assert worlds[0] == 4 and worlds[-1] == 4 and worlds.count(6) >= 2, worlds
+        assert readies[-1]["resume_step"] >= 5
+        assert len({r["pid"] for r in readies if r["world"] == 4 and r["gen"] == readies[-1]["gen"]}) == 4
+    finally:
+        cl.stop()
+
+
 def test_zygote_warm_launch_and_kill(tmp_path):
     """bin/pdo-launch forks ranks from the per-node zygote; a pod kill reaches the rank."""
     pdo_launch = os.path.join(REPO, "bin", "pdo-launch")

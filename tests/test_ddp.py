@@ -35,7 +35,7 @@ def _batch(cfg, B=4, S=32):
     return idx[:, :-1], idx[:, 1:]
 
 
-def _ddp_worker(rank, world, port, outdir):
+def _ddp_worker(rank, world, port, outdir, split=()):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PDO_OPS="torch")
     torch.set_num_threads(2)
     from paddle_operator_amd.models.gpt2 import GPT2, GPT2Config
@@ -45,9 +45,15 @@ def _ddp_worker(rank, world, port, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = GPT2Config.named("gpt2-tiny")
     model = GPT2(cfg)
-    flat = FlatParams(model, dtype=torch.float32, device="cpu", bucket_bytes=64 << 10, late=("wte",))
+    flat = FlatParams(model, dtype=torch.float32, device="cpu", bucket_bytes=64 << 10, late=("wte",), split=split)
     ddp = BucketedDDP(flat)
     assert len(flat.buckets) > 4  # many buckets → out-of-order readiness is exercised
+    if split:  # the LM-head half of the tied weight is bucket 0, the embedding half the last
+        assert [s.name for s in flat.buckets[0].slots] == ["wte#head"]
+        assert "wte" in [s.name for s in flat.buckets[-1].slots]
+        launched = []
+        orig = ddp._launch
+        ddp._launch = lambda i: (launched.append((i, len(ddp._seen))), orig(i))[1]
     x, y = _batch(cfg)
     per = x.shape[0] // world
     sl = slice(rank * per, (rank + 1) * per)
@@ -56,16 +62,25 @@ def _ddp_worker(rank, world, port, outdir):
         ddp.prepare()
         model(x[sl], y[sl]).backward()
         ddp.finish()
+        if split:
+            # bucket 0 went out after the first gradient of the backward (the head's),
+            # long before the last bucket; the slot is folded and zeroed afterwards
+            assert launched[0] == (0, 1), launched
+            assert float(flat.aux_slots[0].param.grad.abs().max()) == 0.0
+            launched.clear()
     torch.save({n: (p.grad * ddp.grad_scale).clone() for n, p in model.named_parameters()},
                os.path.join(outdir, f"g{rank}.pt"))
     dist.destroy_process_group()
 
 
-def test_bucketed_ddp_matches_full_batch(tmp_path):
+@pytest.mark.parametrize("split", [(), ("wte",)])
+def test_bucketed_ddp_matches_full_batch(tmp_path, split):
+    """split = ("wte",): the tied weight's LM-head gradient in its own first
+    bucket (parallel/flat.py AuxGrad), folded after the drain — same gradients."""
     os.environ["PDO_OPS"] = "torch"
     from paddle_operator_amd.models.gpt2 import GPT2, GPT2Config
 
-    mp.start_processes(_ddp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, start_method="spawn")
+    mp.start_processes(_ddp_worker, args=(2, _free_port(), str(tmp_path), split), nprocs=2, start_method="spawn")
     cfg = GPT2Config.named("gpt2-tiny")
     ref = GPT2(cfg)  # same deterministic init as the ranks
     x, y = _batch(cfg)

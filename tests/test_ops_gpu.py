@@ -320,6 +320,14 @@ def test_lm_head_xent_chunked(cuda, N, C, V, chunk, fused):
     assert abs(loss.item() - lossf.item()) < 2e-3 * max(1.0, lossf.item())
     assert rel_err(hh.grad, hf.grad) < 3e-2
     assert rel_err(ww.grad[:V], wf.grad[:V]) < 3e-2
+    # no_grad (validation loss): the loss-only path, same value
+    ops._LM_CHUNK[0] = chunk
+    try:
+        with torch.no_grad():
+            loss_ng = ops.lm_head_xent(hh, ww, tgt, V)
+    finally:
+        ops._LM_CHUNK[0] = prev
+    assert abs(loss_ng.item() - lossf.item()) < 2e-3 * max(1.0, lossf.item())
 
 
 def test_embedding(cuda):
@@ -477,28 +485,6 @@ def test_gpt2_medium_width_hip_vs_fp32(cuda):
     errs = {n: rel_err(p.grad, dict(ref.named_parameters())[n].grad) for n, p in m.named_parameters()}
     bad = {n: e for n, e in errs.items() if not e < 5e-2}
     assert not bad, bad
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("T,C", [(2048, 256), (8192, 1024)])
-def test_fused_mlp_epilogues(cuda, T, C):
-    """hipBLASLt GELU_AUX_BIAS / DGELU_BGRAD MLP matches an fp32 reference."""
-    ops = _ops()
-    g = torch.Generator(device=cuda).manual_seed(12)
-    x = torch.randn(T, C, device=cuda, generator=g).bfloat16().requires_grad_()
-    w1 = (0.05 * torch.randn(4 * C, C, device=cuda, generator=g)).bfloat16().requires_grad_()
-    b1 = (0.1 * torch.randn(4 * C, device=cuda, generator=g)).bfloat16().requires_grad_()
-    w2 = (0.05 * torch.randn(C, 4 * C, device=cuda, generator=g)).bfloat16().requires_grad_()
-    y = ops.mlp(x, w1, b1, w2)  # default path: GEMMs + HIP bias-GELU kernels
-    dy = torch.randn_like(y)
-    y.backward(dy)
-    ref = [t.detach().float().requires_grad_() for t in (x, w1, b1, w2)]
-    yf = torch.nn.functional.gelu(ref[0] @ ref[1].t() + ref[2], approximate="tanh") @ ref[3].t()
-    yf.backward(dy.float())
-    assert rel_err(y, yf) < 2e-2
-    for t, r, name in zip((x, w1, b1, w2), ref, ("dx", "dw1", "db1", "dw2")):
-        e = rel_err(t.grad, r.grad)
-        assert e < 3e-2, f"{name} rel err {e}"
 
 
 @pytest.mark.gpu
@@ -666,7 +652,7 @@ def test_gemm_dw4_half_height_edge(cuda, T, M, N, acc, splits):
     ref = base.float() + dy.float().t() @ x.float()
     prev = m.gemm_dw_impl(-1)
     try:
-        for impl in (1, 2, 3, 4):
+        for impl in (1, 2):
             m.gemm_dw_impl(impl)
             out = base.clone()
             assert m.gemm_dw(dy, x, out, True, splits)
@@ -680,7 +666,7 @@ def test_gemm_dw4_half_height_edge(cuda, T, M, N, acc, splits):
 @pytest.mark.parametrize("T,M,N,acc", [(8192, 4096, 4096, True), (65536, 1024, 3072, False), (16384, 512, 768, True),
                                        (16384, 3072, 1024, True)])  # last: 48 tiles → 5 uneven slices
 def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
-    """The 4-wave dW mainloop (gemm_dw4.hip, all four variants incl. the 16x16x32 one; split-K or
+    """The 4-wave dW mainloop (gemm_dw4.hip, both schedules: 16x16x32 and 32x32x16 MFMAs; split-K or
     in-kernel accumulate at one split) and the 8-wave one against fp32."""
     from paddle_operator_amd import _native
     m = _native.require_hip()
@@ -692,7 +678,7 @@ def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
     ref = base.float() + dy.float().t() @ x.float()
     prev = m.gemm_dw_impl(0)
     try:
-        for impl in (0, 1, 2, 3, 4):
+        for impl in (0, 1, 2):
             m.gemm_dw_impl(impl)
             out = base.clone()
             assert m.gemm_dw(dy, x, out, True)

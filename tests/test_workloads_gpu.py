@@ -39,10 +39,27 @@ def test_launcher_gpt2_single_gpu(cuda, tmp_path):
     assert os.path.exists(tmp_path / "ck" / "ckpt-00000003.pt")
 
 
+@pytest.fixture
+def deterministic_convs():
+    """MIOpen's GemmK-split weight-gradient solvers (igemm_wrw_*_gkgs) sum with
+    float atomics, so two runs of the same bf16 convolution backward differ in
+    the last bits (2e-4 relative on an 8→32 1×1 downsample, GPUTEST_r03).  The
+    deterministic flag makes MIOpen pick an atomic-free solver."""
+    old = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    yield
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+
+
 @pytest.mark.gpu
-def test_resnet_arena_grads_match_autograd(cuda):
+def test_resnet_arena_grads_match_autograd(cuda, deterministic_convs):
     """BN γ/β gradients written straight into the flat arena by the HIP backward
-    (ops.bn_act direct path) equal autograd's accumulated gradients."""
+    (ops.bn_act direct path) equal autograd's accumulated gradients.
+
+    Both models run the same kernels on the same input, so the gradients agree
+    to rounding; the bound (2e-3, a quarter of a bf16 ulp) still fails any
+    gradient the arena path drops, doubles or mis-places (O(1) errors), and
+    does not depend on which convolution solver a box picks."""
     import copy
 
     from paddle_operator_amd.models.resnet import resnet18_like_tiny
@@ -66,5 +83,5 @@ def test_resnet_arena_grads_match_autograd(cuda):
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert pa.grad.data_ptr() >= flat.grads.data_ptr(), n
         err = (pa.grad.float() - pb.grad.float()).norm() / (pb.grad.float().norm() + 1e-12)
-        assert err < 1e-5, f"{n}: {err}"
+        assert err < 2e-3, f"{n}: {err}"
 

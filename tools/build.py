@@ -59,9 +59,7 @@ def torch_flags():
     ]
     lib = os.path.join(tdir, "lib")
     ldflags = [f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-               "-ltorch_python", f"-Wl,-rpath,{lib}",
-               # the SAME hipBLASLt torch uses (one copy per process)
-               os.path.join(lib, "libhipblaslt.so")]
+               "-ltorch_python", f"-Wl,-rpath,{lib}"]
     return cflags, ldflags
 
 
