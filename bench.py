@@ -115,13 +115,17 @@ def parse_args(argv=None):
     # multi-rank launched GPU path (agent GPU accounting, DDP hooks over the HIP
     # kernels, per-rank records, comm diagnostics) on a 1-GPU box; not a benchmark
     ap.add_argument("--rehearse-shared-gpu", action="store_true", help=argparse.SUPPRESS)
+    # with --cpu: the node offers N virtual GPUs (agent GPU accounting, one warm
+    # slot per "GPU" in the zygote's CPU test mode, amd.com/gpu requests) while the
+    # ranks run on CPU over gloo — the N-rank launched path's rehearsal (CPU tests)
+    ap.add_argument("--virtual-gpus", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
 class Launcher:
     """One in-process local backend; launches PaddleJobs and reads pdo-kv."""
 
-    def __init__(self, mode, zygote, gpus, sandbox, extra_args=(), nproc=1):
+    def __init__(self, mode, zygote, gpus, sandbox, extra_args=(), nproc=1, cpu_threads=0):
         from paddle_operator_amd.controller import LocalCluster
         from paddle_operator_amd.kv.client import KVClient
 
@@ -131,6 +135,7 @@ class Launcher:
         self.zygote = zygote
         self.extra_args = list(extra_args)
         self.nproc = nproc  # ranks per pod (--nproc-per-pod; amd.com/gpu per pod)
+        self.cpu_threads = cpu_threads  # --virtual-gpus: CPU ranks behind GPU requests
         self.cl = LocalCluster(mode=mode, agent="exec", sandbox_root=sandbox,
                                nodes=[{"name": "node0", "gpus": gpus}],
                                kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote)
@@ -150,8 +155,8 @@ class Launcher:
         from paddle_operator_amd.api import types as T
         env = [{"name": "PYTHONPATH", "value": REPO}, {"name": "PDO_KV", "value": f"127.0.0.1:{self.port}"},
                {"name": "PDO_PYTHON", "value": sys.executable}, {"name": "PDO_OPS", "value": ops}]
-        if not self.gpus:
-            env.append({"name": "OMP_NUM_THREADS", "value": "2"})
+        if not self.gpus or self.cpu_threads:
+            env.append({"name": "OMP_NUM_THREADS", "value": str(self.cpu_threads or 2)})
         c = {"name": "paddle", "image": "pdo/launcher:rocm",
              "command": [os.path.join(REPO, "bin", "pdo-launch")] + list(args), "env": env}
         if self.gpus:
@@ -290,6 +295,13 @@ def orchestrate(a):
         os.environ.setdefault("PDO_HANG_DUMP_S", "60")  # rank stacks in the pod logs (launch/run.py)
         extra_args = ["--backend", "gloo"]
         detected = N
+    if a.virtual_gpus:
+        if not a.cpu:
+            log("--virtual-gpus needs --cpu")
+            return 2
+        os.environ["PDO_SLOT_TEST"] = "cpu"  # warm slots without HIP (launch/zygote.py)
+        extra_args = ["--backend", "gloo"]
+        detected = N
     if detected and detected < N:
         log(f"--gpus {N} but only {detected} GPU(s) visible")
         return 2
@@ -306,7 +318,8 @@ def orchestrate(a):
     out = {}
     try:
         nproc = N if a.pod_layout == "one-pod" else 1
-        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode), extra_args, nproc)
+        L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode), extra_args, nproc,
+                     cpu_threads=1 if a.virtual_gpus else 0)
         try:
             trials = []
             for t in range(a.ready_trials):

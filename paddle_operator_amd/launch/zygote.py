@@ -185,6 +185,13 @@ def _become_rank(req, fds, warm=False):
         os.chdir(req.get("cwd") or "/")
         os.environ.clear()
         os.environ.update(req.get("env") or {})
+        # torch sized its intra-op pool when the ZYGOTE imported it (its
+        # environment, typically every CPU); the pod's OMP_NUM_THREADS must still
+        # hold in the rank — 8 forked CPU ranks on 8 CPUs each ran 8 spinning
+        # OpenMP threads: 16 s per tiny ResNet step instead of 10 ms
+        omp = (os.environ.get("OMP_NUM_THREADS") or "").strip()
+        if omp.isdigit() and int(omp) > 0 and "torch" in sys.modules:
+            sys.modules["torch"].set_num_threads(int(omp))
         argv = list(req.get("argv") or [])
         sys.argv = ["pdo-launch"] + argv
         sys.stdout = os.fdopen(1, "w", buffering=1, closefd=False)

@@ -161,6 +161,33 @@ def test_bench_one_pod_layout_two_ranks():
     assert rec["config"]["pod_layout"] == "1x2" and "replicas=1 x 2" in rec["config"]["launch"]
 
 
+@pytest.mark.parametrize("layout", ["per-gpu", "one-pod"])
+def test_bench_eight_ranks_virtual_gpus(layout):
+    """The 8-GPU launched path on CPU: the node offers 8 (virtual) GPUs, so the
+    agent's GPU accounting, the warm launcher's one-slot-per-GPU pool (above 2
+    GPUs) and the 8-rank comm block all run as on a full MI355X node; the ranks
+    themselves train the tiny ResNet over gloo.  Both pod layouts: 8 × 1 GPU and
+    1 × 8 GPUs (--nproc-per-pod 8)."""
+    env = _bench_env()
+    env.pop("PDO_SLOTS_PER_GPU", None)
+    args = ["--gpus", "8", "--cpu", "--virtual-gpus", "--workload", "resnet50", "--tiny", "--micro-batch", "2",
+            "--steps", "2", "--warmup", "1", "--ready-trials", "2", "--compat-trials", "0", "--train-ready-trials", "1",
+            "--b2b-trials", "1", "--ops", "torch", "--pod-layout", layout]
+    r = subprocess.run([sys.executable, "bench.py"] + args, cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8" and rec["config"]["global_batch"] == 16
+    assert rec["config"]["pod_layout"] == ("8x1" if layout == "per-gpu" else "1x8")
+    slots = rec["warm_slots"]["node0"]
+    assert sorted(slots, key=int) == [str(i) for i in range(8)]
+    assert all(sl["n"] == 1 for sl in slots.values()), slots  # one warm slot per GPU above 2 GPUs
+    c = rec["comm"]
+    assert c["ranks"] == 8 and c["buckets"]["count"] >= 1 and len(c["allreduce_sweep"]) == 4
+    assert c["nosync_step_ms_max"] < 5000  # forked ranks honour the pod's OMP_NUM_THREADS
+    assert rec["ready"]["trials"] == 2 and rec["ready_b2b"]["trials"] == 1
+
+
 @pytest.mark.slow
 def test_bench_contract_torchrun_two_ranks():
     """Under the driver's torchrun wrapper: rank 0 launches, rank 1 only waits; one JSON line."""
