@@ -316,6 +316,60 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
   }
 }
 
+// forward finalize from the convolution epilogue's per-M-tile partials
+// ([G][2][C]: Σv and Σ(v − mean_tile)² over the tile's rows, conv.hip): a
+// block per 8 channels, 32 tile lanes × 8 channels.  Two plain reductions
+// (no sequential merge): mean = Σ sum_i / M, then M2 = Σ (M2_i + n_i·(mean_i − mean)²)
+__global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __restrict__ part, int G, int tile_rows,
+                                                                long long M, int C, const float* __restrict__ w,
+                                                                const float* __restrict__ b, float eps,
+                                                                float momentum, float* __restrict__ running_mean,
+                                                                float* __restrict__ running_var,
+                                                                float* __restrict__ mean_out,
+                                                                float* __restrict__ invstd_out,
+                                                                float* __restrict__ ss) {
+  const int ch = threadIdx.x & 7, tl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + ch;
+  __shared__ float red[32][8];
+  __shared__ float bc[8];
+  float s = 0.f;
+  for (int i = tl; i < G; i += 32) s += part[(size_t)i * 2 * C + c];
+  red[tl][ch] = s;
+  __syncthreads();
+  if (tl == 0) {
+    float t = 0.f;
+    for (int k = 0; k < 32; ++k) t += red[k][ch];
+    bc[ch] = t / (float)M;
+  }
+  __syncthreads();
+  const float mean = bc[ch];
+  float q = 0.f;
+  for (int i = tl; i < G; i += 32) {
+    const long long r0 = (long long)i * tile_rows;
+    const float n = (float)(M - r0 < tile_rows ? M - r0 : tile_rows);
+    const float d = part[(size_t)i * 2 * C + c] / n - mean;
+    q += part[(size_t)i * 2 * C + C + c] + n * d * d;
+  }
+  __syncthreads();
+  red[tl][ch] = q;
+  __syncthreads();
+  if (tl != 0) return;
+  float t = 0.f;
+  for (int k = 0; k < 32; ++k) t += red[k][ch];
+  const float var = fmaxf(t / (float)M, 0.f);
+  const float inv = rsqrtf(var + eps);
+  mean_out[c] = mean;
+  invstd_out[c] = inv;
+  const float sc = w[c] * inv;
+  ss[c] = sc;
+  ss[C + c] = b[c] - mean * sc;
+  if (running_mean) {
+    const float unb = M > 1 ? (float)M / (float)(M - 1) : 1.f;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + (momentum * unb) * var;
+  }
+}
+
 int pick_tx(int C) {
   const int c8 = C / 8;
   if (c8 >= 32) return 32;
@@ -365,6 +419,21 @@ int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float
   else bn_stats_kernel<8><<<grid, BN_THREADS, 0, st>>>(x, M, C, rpg, part);
   bn_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, gy, x, M, C, w, b, eps, momentum, running_mean, running_var, mean,
                                              invstd, ss);
+  const long long n8 = M * C / 8;
+  const unsigned g = apply_grid(n8);
+  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);
+  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);
+  return 0;
+}
+
+// BatchNorm forward whose statistics came with the producing convolution
+// (conv.hip tile partials): finalize + apply, no statistics pass over x
+int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
+                 const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
+                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st) {
+  if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1) return -2;
+  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
+                                                  running_var, mean, invstd, ss);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
   if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);

@@ -427,6 +427,85 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, a
   return {dx, dres, dw, db};
 }
 
+// ---------------------------------------------------------------- NHWC implicit-GEMM convolutions (conv.hip)
+// x: channels_last bf16 [N, C, H, W]; w: channels_last bf16 [K, C, R, S] (OHWI memory)
+bool conv_ok(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t R, int64_t S, int64_t stride,
+             int64_t pad) {
+  return pdo::conv_supported((int)N, (int)H, (int)W, (int)C, (int)K, (int)R, (int)S, (int)stride, (int)pad) != 0;
+}
+
+// y = conv(x, w); with_stats: also the per-M-tile BatchNorm partials [tiles, 2, K] (+ tile rows)
+std::vector<at::Tensor> conv_fwd(at::Tensor x, at::Tensor w, int64_t stride, int64_t pad, bool with_stats) {
+  CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_fwd: channels_last bf16 input");
+  TORCH_CHECK(w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(1) == x.size(1),
+              "conv_fwd: channels_last bf16 weight [K, C, R, S]");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int K = (int)w.size(0), R = (int)w.size(2), S = (int)w.size(3);
+  const int Ho = (H + 2 * (int)pad - R) / (int)stride + 1, Wo = (W + 2 * (int)pad - S) / (int)stride + 1;
+  auto y = at::empty({N, K, Ho, Wo}, x.options(), at::MemoryFormat::ChannelsLast);
+  at::Tensor st;
+  if (with_stats) st = at::empty({pdo::conv_fwd_tiles((long long)N * Ho * Wo, K), 2, K}, x.options().dtype(at::kFloat));
+  CHECK_RC(pdo::conv_fwd_nhwc(bp(x), N, H, W, C, bp(w), K, R, S, (int)stride, (int)pad, bp(y),
+                              with_stats ? fp(st) : nullptr, cur_stream()), "conv_fwd_nhwc");
+  return {y, st};
+}
+
+int64_t conv_tile_rows(int64_t K) { return pdo::conv_fwd_tile_rows((int)K); }
+
+// Wᵀ of a channels_last [K, C, R, S] weight: [C, R·S·K] (the input-gradient GEMM's B)
+at::Tensor conv_weight_t(at::Tensor w) {
+  CHECK_BF16(w);
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast));
+  const int K = (int)w.size(0), C = (int)w.size(1), T = (int)(w.size(2) * w.size(3));
+  auto wt = at::empty({C, (int64_t)T * K}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  CHECK_RC(pdo::conv_weight_t(bp(w), bp(wt), K, T, C, cur_stream()), "conv_weight_t");
+  return wt;
+}
+
+// dx [N, C, H, W] (channels_last) of y = conv(x, w) from dy and wt = conv_weight_t(w)
+at::Tensor conv_dgrad(at::Tensor dy, at::Tensor wt, int64_t C, int64_t R, int64_t S, int64_t H, int64_t W,
+                      int64_t stride, int64_t pad) {
+  CHECK_BF16(dy); CHECK_BF16(wt);
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad: channels_last bf16 dy");
+  const int N = (int)dy.size(0), K = (int)dy.size(1);
+  TORCH_CHECK(wt.is_contiguous() && wt.size(0) == C && wt.size(1) == R * S * K, "conv_dgrad: wt [C, R*S*K]");
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  CHECK_RC(pdo::conv_dgrad_nhwc(bp(dy), N, (int)H, (int)W, (int)C, bp(wt), K, (int)R, (int)S, (int)stride, (int)pad,
+                                bp(dx), cur_stream()), "conv_dgrad_nhwc");
+  return dx;
+}
+
+// BatchNorm (+ residual) (+ ReLU) forward from conv_fwd's tile statistics
+std::vector<at::Tensor> bn_act_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t tile_rows,
+                                         c10::optional<at::Tensor> res, at::Tensor w, at::Tensor b,
+                                         c10::optional<at::Tensor> rm, c10::optional<at::Tensor> rv, double eps,
+                                         double momentum, bool relu) {
+  CHECK_BF16(x); CHECK_F32(w); CHECK_F32(b); CHECK_F32(stats);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_act_fwd_tiles: channels_last bf16 input");
+  const long long C = x.size(1), M = x.numel() / C;
+  TORCH_CHECK(stats.dim() == 3 && stats.size(1) == 2 && stats.size(2) == C &&
+              stats.size(0) == (M + tile_rows - 1) / tile_rows, "bn_act_fwd_tiles: stats [tiles, 2, C]");
+  auto y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  auto mean = at::empty({C}, w.options()), invstd = at::empty({C}, w.options());
+  auto ss = at::empty({2 * C}, w.options());
+  const bf16* rp = nullptr;
+  if (res && res->defined()) {
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(at::MemoryFormat::ChannelsLast));
+    CHECK_BF16((*res));
+    rp = bp(*res);
+  }
+  float* rmp = rm && rm->defined() ? fp(*rm) : nullptr;
+  float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
+  CHECK_RC(pdo::bn_fwd_tiles(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), rp, fp(w), fp(b), rmp, rvp, M,
+                             (int)C, (float)eps, (float)momentum, relu ? 1 : 0, bp(y), fp(mean), fp(invstd), fp(ss),
+                             cur_stream()), "bn_fwd_tiles");
+  return {y, mean, invstd};
+}
+
 // ---------------------------------------------------------------- NHWC max-pool 3×3/2
 std::vector<at::Tensor> maxpool3s2_fwd(at::Tensor x) {
   CHECK_BF16(x);
@@ -689,6 +768,13 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),
         py::arg("db_out") = py::none());
   m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_fwd_tiles", &bn_act_fwd_tiles);
+  m.def("conv_ok", &conv_ok);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("with_stats") = false);
+  m.def("conv_tile_rows", &conv_tile_rows);
+  m.def("conv_weight_t", &conv_weight_t);
+  m.def("conv_dgrad", &conv_dgrad);
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);

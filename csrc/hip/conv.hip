@@ -1,0 +1,464 @@
+// SPDX-License-Identifier: Apache-2.0
+// NHWC implicit-GEMM convolutions (3×3 and strided 1×1) for ResNet-50 on gfx950.
+//
+// The reference's ResNet-50 configs (deploy/examples/resnet.yaml:1-29,
+// deploy/elastic/resnet.yaml:1-37) launch a training image; here that data
+// plane runs on hand-written CDNA4 kernels instead of MIOpen's igemm solvers
+// and their zero-fill / cast passes.
+//
+// One mainloop serves the forward and the input gradient: the output is a
+// [tokens × Kout] GEMM whose A operand is gathered from an NHWC activation by
+// a per-launch TAP TABLE (per tap: the input-pixel offset relative to the
+// token's base pixel, and the column of B where that tap's weights start):
+//
+//   forward      token (n, ho, wo), base pixel (ho·st − pad, wo·st − pad),
+//                taps (r, s), B = W [Kout][R][S][C] (channels_last OHWI)
+//   dgrad, st 1  token (n, h, w), taps (pad − r, pad − s), B = Wᵀ [C][R·S][Kout]
+//   dgrad, st 2  one launch per output parity class (h % 2, w % 2): token
+//                (n, a, b) → pixel (2a + ph, 2b + pw); only the taps with
+//                (ph + pad − r) even reach it, at dY pixel a + (ph + pad − r)/2
+//                — no MFMA is spent on the zeros of a strided transposed conv
+//
+// Mainloop (gemm_nt4's operand handling at a smaller tile): a workgroup of 4
+// waves owns BM × BN outputs (256 × 64 for Kout = 64, else 128 × 128), each
+// wave 64 × 64 = 4 × 4 blocks of v_mfma_f32_16x16x32_bf16; k-step = 64
+// channels of one tap.  Both operands reach LDS by LDS-DMA (1 KiB = 8 rows of
+// 128 B per wave-instruction), two stages, one tile of lead:
+//   * A rows are gathered: every lane of a piece computes its row's source
+//     pixel for the k-step's tap; the load is a buffer_load … lds whose offset
+//     is pushed past the buffer's range for a padding pixel or a row past the
+//     last token, so the hardware writes zeros — no zero-fill pass;
+//   * B rows are weight rows, permuted in LDS (physical row 16j + c of a wave's
+//     64-column slice holds column 4c + j) so a lane's accumulators hold 4
+//     consecutive output channels: the epilogue stores 8 B per lane straight
+//     from registers, 128 B per row.
+// LDS rows are 128 B with the 16-B chunk c of row r at c ^ ((r >> 1) & 7) (the
+// swizzle is applied on the per-lane source address): the 16 rows a
+// ds_read_b128 lane group touches land on 16 distinct bank slots.
+//
+// BatchNorm statistics in the forward epilogue: per M-tile and channel the
+// sum and the centred sum of squares of the bf16-rounded outputs
+// ([tiles][2][Kout], batchnorm.hip bn_fwd_tiles merges them), so the
+// BatchNorm forward needs no statistics pass over the activation.
+#include <stdlib.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace pdo {
+
+namespace {
+
+constexpr int CNT = 256;
+constexpr unsigned OOB = 0x80000000u;  // ≥ any buffer's num_records: the load returns zeros
+
+template <typename Fn, int... I>
+__device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+struct ConvArgs {
+  const bf16* x;         // A source, NHWC [N][IH][IW][C]
+  const bf16* w;         // B [Kout][ldb], row = output channel
+  bf16* y;               // output rows [N][OH][OW][Kout]
+  float* stats;          // nullptr, or per-M-tile BatchNorm partials [tiles][2][Kout]
+  long long M;           // tokens
+  int C, Kout, ldb;
+  int IH, IW;
+  int TA, TB;            // token t = (n·TA + a)·TB + b
+  float inv_TA, inv_TB;  // for the float-reciprocal divisions below
+  int ist, ipad;         // base pixel (a·ist − ipad, b·ist − ipad)
+  int OH, OW, ost, oph, opw;  // output pixel (a·ost + oph, b·ost + opw)
+  int ident;             // output row = token (forward)
+  unsigned xbytes;
+  int ntaps;
+  int dh[9], dw[9], bcol[9];
+};
+
+// q = x / d, r = x - q·d for 0 ≤ x < 2^24 (exact via a float reciprocal + one correction)
+__device__ __forceinline__ void divmod(int x, int d, float inv, int& q, int& r) {
+  q = (int)((float)x * inv);
+  r = x - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  } else if (r >= d) {
+    ++q;
+    r -= d;
+  }
+}
+
+__device__ __forceinline__ void bufld(unsigned voff, __amdgpu_buffer_rsrc_t rs, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "s"(lds_byte)
+               : "memory");
+}
+__device__ __forceinline__ void glds(unsigned voff, const void* sbase, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase),
+               "s"(lds_byte)
+               : "memory");
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
+  constexpr int WN = BN / 64, WM = BM / 64;
+  static_assert(WM * WN == 4, "4 waves of 64 × 64");
+  constexpr int PA = BM / 8, PB = BN / 8;   // 1-KiB pieces per k-step
+  constexpr int NA = PA / 4, NB = PB / 4;   // per wave
+  constexpr int STAGE = (BM + BN) * 128;    // bytes per stage
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int ntn = a.Kout / BN;
+  const long long ntm = (a.M + BM - 1) / BM;
+  // bijective XCD remap: blocks b and b + 8 share an XCD, so each XCD walks a
+  // contiguous range of tiles — the ntn tiles of one token range share its L2
+  long long id = blockIdx.x;
+  {
+    const long long nwg = ntm * ntn, q = nwg >> 3, r = nwg & 7, x = id & 7, slot = id >> 3;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+  }
+  const int tn = (int)(id % ntn);
+  const long long tm = id / ntn;
+  const long long m0 = tm * BM;
+  const int n0 = tn * BN;
+
+  // ---- A pieces: this wave's pieces p = w + 4i (i < NA): rows 8p + (l >> 3)
+  int hb[NA], wb[NA], base[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = 8 * (w + 4 * i) + (lane >> 3);
+    const long long t = m0 + m;
+    const int cg = (lane & 7) ^ ((m >> 1) & 7);
+    if (t < a.M) {
+      int q, bb, n, aa;
+      divmod((int)t, a.TB, a.inv_TB, q, bb);
+      divmod(q, a.TA, a.inv_TA, n, aa);
+      hb[i] = aa * a.ist - a.ipad;
+      wb[i] = bb * a.ist - a.ipad;
+      base[i] = ((n * a.IH + hb[i]) * a.IW + wb[i]) * a.C + cg * 8;
+    } else {
+      hb[i] = -(1 << 20);  // fails every bounds check
+      wb[i] = 0;
+      base[i] = 0;
+    }
+  }
+  // ---- B pieces: p = w + 4(NA + i) - PA of the B tile; physical row pr ↔ column
+  unsigned voffB[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int pr = 8 * (w + 4 * i) + (lane >> 3);
+    const int q = pr & 63;
+    const int col = n0 + 64 * (pr >> 6) + 4 * (q & 15) + (q >> 4);
+    const int cg = (lane & 7) ^ ((pr >> 1) & 7);
+    voffB[i] = (unsigned)((col * a.ldb + cg * 8) * 2);
+  }
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int CC = a.C >> 6;
+  const int nk = a.ntaps * CC;
+
+  auto issue = [&](int kt, int stage) {
+    const int tap = kt / CC, cc = kt - tap * CC;
+    const int dh = a.dh[tap], dw = a.dw[tap];
+    const int coff = (dh * a.IW + dw) * a.C + cc * 64;
+    const unsigned sb = lds0 + (unsigned)(stage * STAGE);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int hi = hb[i] + dh, wi = wb[i] + dw;
+      const bool ok = (unsigned)hi < (unsigned)a.IH && (unsigned)wi < (unsigned)a.IW;
+      const unsigned v = ok ? (unsigned)((base[i] + coff) * 2) : OOB;
+      bufld(v, rsX, sb + (unsigned)((w + 4 * i) * 1024));
+    }
+    const bf16* bsrc = a.w + a.bcol[tap] + cc * 64;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) glds(voffB[i], bsrc, sb + (unsigned)(BM * 128 + (w + 4 * i) * 1024));
+  };
+
+  // ---- fragment offsets (bytes within a stage)
+  const int sw = (lane >> 1) & 7;
+  const int ch0 = ((lane >> 4) ^ sw) << 4, ch1 = ((4 + (lane >> 4)) ^ sw) << 4;
+  const int rA = (wm * 64 + (lane & 15)) * 128, rB = BM * 128 + (wn * 64 + (lane & 15)) * 128;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) {
+      issue(kt + 1, (kt + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory");  // k-step kt landed (kt + 1 flies)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+    const char* st = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk ? ch1 : ch0;
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + rA + i * 2048 + ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + rB + j * 2048 + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's reads of this stage precede its refill (k-step kt + 2)
+  }
+
+  // ---- epilogue: acc[i][j][e] = C[m = wm·64 + 16i + 4(l >> 4) + e][col n0 + wn·64 + 4(l & 15) + j]
+  const int g4 = lane >> 4;
+  const int col = n0 + wn * 64 + 4 * (lane & 15);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = wm * 64 + 16 * i + 4 * g4 + e;
+      const long long t = m0 + m;
+      if (t >= a.M) continue;
+      long long row;
+      if (a.ident) {
+        row = t;
+      } else {
+        int q, bb, n, aa;
+        divmod((int)t, a.TB, a.inv_TB, q, bb);
+        divmod(q, a.TA, a.inv_TA, n, aa);
+        row = ((long long)n * a.OH + aa * a.ost + a.oph) * a.OW + bb * a.ost + a.opw;
+      }
+      const bf16x4 v = {(bf16)acc[i][0][e], (bf16)acc[i][1][e], (bf16)acc[i][2][e], (bf16)acc[i][3][e]};
+      *reinterpret_cast<bf16x4*>(a.y + row * a.Kout + col) = v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cs[j] += (float)v[j];
+    }
+  if (!a.stats) return;
+  // ---- BatchNorm partials of this M-tile: Σv and Σ(v − mean_tile)² per channel
+  const int rows = (int)(a.M - m0 < BM ? a.M - m0 : BM);
+  float* red = reinterpret_cast<float*>(smem);  // [WM][BN] (the last k-step's barrier freed the stages)
+  auto tile_sum = [&](float (&v)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] += __shfl_xor(v[j], 16, 64);
+      v[j] += __shfl_xor(v[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wm * BN + wn * 64 + 4 * lane + j] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int u = 0; u < WM; ++u) s += red[u * BN + wn * 64 + 4 * (lane & 15) + j];
+      v[j] = s;
+    }
+    __syncthreads();
+  };
+  tile_sum(cs);
+  float mean[4], cq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) mean[j] = cs[j] / (float)rows;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long t = m0 + wm * 64 + 16 * i + 4 * g4 + e;
+      if (t >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = (float)(bf16)acc[i][j][e] - mean[j];
+        cq[j] += d * d;
+      }
+    }
+  tile_sum(cq);
+  if (wm == 0 && lane < 16) {
+    float* p = a.stats + (size_t)tm * 2 * a.Kout + col;
+    *reinterpret_cast<f32x4*>(p) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    *reinterpret_cast<f32x4*>(p + a.Kout) = f32x4{cq[0], cq[1], cq[2], cq[3]};
+  }
+}
+
+// Wᵀ for the input gradient: w [K][T][C] → wt [C][T][K] (T = R·S taps), bf16
+__global__ __launch_bounds__(256) void conv_wt_kernel(const bf16* __restrict__ w, bf16* __restrict__ wt, int K, int T,
+                                                      int C) {
+  const long long n = (long long)K * T * C;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long long kt = i / C;
+    const int t = (int)(kt % T), k = (int)(kt / T);
+    wt[((long long)c * T + t) * K + k] = w[i];
+  }
+}
+
+template <int BM, int BN>
+int launch_igemm(const ConvArgs& a, hipStream_t st) {
+  const long long tiles = ((a.M + BM - 1) / BM) * (a.Kout / BN);
+  if (tiles > 0x7fffffffLL) return -2;
+  conv_igemm_kernel<BM, BN><<<(unsigned)tiles, CNT, 0, st>>>(a);
+  return 0;
+}
+
+int run_igemm(ConvArgs& a, hipStream_t st, int* tile_rows) {
+  a.inv_TA = 1.f / (float)a.TA;
+  a.inv_TB = 1.f / (float)a.TB;
+  if (a.Kout == 64) {
+    if (tile_rows) *tile_rows = 256;
+    return launch_igemm<256, 64>(a, st);
+  }
+  if (tile_rows) *tile_rows = 128;
+  return launch_igemm<128, 128>(a, st);
+}
+
+bool shape_ok(int C, int Kout, int R, int S, int stride, int pad) {
+  return C % 64 == 0 && Kout % 64 == 0 && (Kout == 64 || Kout % 128 == 0) && R == S && (R == 1 || R == 3) &&
+         (stride == 1 || stride == 2) && pad == (R - 1) / 2;
+}
+
+}  // namespace
+
+int conv_supported(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
+  if (!shape_ok(C, Kout, R, S, stride, pad)) return 0;
+  const long long xb = (long long)N * H * W * C * 2;
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const long long M = (long long)N * Ho * Wo;
+  if (xb >= (1ll << 31) || M >= (1 << 24) || (long long)N * H * W >= (1 << 24)) return 0;
+  const long long yb = M * Kout * 2;
+  return yb < (1ll << 31);
+}
+
+int conv_fwd_tiles(long long M, int Kout) { return (int)((M + (Kout == 64 ? 255 : 127)) / (Kout == 64 ? 256 : 128)); }
+int conv_fwd_tile_rows(int Kout) { return Kout == 64 ? 256 : 128; }
+
+int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int Kout, int R, int S, int stride, int pad,
+                  bf16* y, float* tile_stats, hipStream_t st) {
+  if (!conv_supported(N, H, W, C, Kout, R, S, stride, pad)) return -2;
+  ConvArgs a{};
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  a.x = x;
+  a.w = w;
+  a.y = y;
+  a.stats = tile_stats;
+  a.M = (long long)N * Ho * Wo;
+  a.C = C;
+  a.Kout = Kout;
+  a.ldb = R * S * C;
+  a.IH = H;
+  a.IW = W;
+  a.TA = Ho;
+  a.TB = Wo;
+  a.ist = stride;
+  a.ipad = pad;
+  a.OH = Ho;
+  a.OW = Wo;
+  a.ost = 1;
+  a.ident = 1;
+  a.xbytes = (unsigned)((long long)N * H * W * C * 2);
+  a.ntaps = R * S;
+  for (int r = 0; r < R; ++r)
+    for (int s = 0; s < S; ++s) {
+      const int t = r * S + s;
+      a.dh[t] = r;
+      a.dw[t] = s;
+      a.bcol[t] = t * C;
+    }
+  return run_igemm(a, st, nullptr);
+}
+
+int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t st) {
+  conv_wt_kernel<<<stream_grid((long long)Kout * T * C, 256), 256, 0, st>>>(w, wt, Kout, T, C);
+  return 0;
+}
+
+// dx [N][H][W][C] from dy [N][Ho][Wo][Kout] and wt = Wᵀ [C][R·S][Kout]; every
+// element of dx is written (parity classes without taps get zeros by a memset)
+int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
+                    int pad, bf16* dx, hipStream_t st) {
+  if (!conv_supported(N, H, W, C, Kout, R, S, stride, pad)) return -2;
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  if ((long long)N * Ho * Wo * Kout * 2 >= (1ll << 31)) return -2;
+  ConvArgs a{};
+  a.x = dy;
+  a.w = wt;
+  a.y = dx;
+  a.C = Kout;      // A channels = dY's
+  a.Kout = C;      // output columns = dX's channels
+  a.ldb = R * S * Kout;
+  a.IH = Ho;
+  a.IW = Wo;
+  a.ist = 1;
+  a.ipad = 0;
+  a.OH = H;
+  a.OW = W;
+  a.xbytes = (unsigned)((long long)N * Ho * Wo * Kout * 2);
+  if (!shape_ok(Kout, C, R, S, 1, pad)) return -2;  // the roles of C and Kout swap here
+  if (stride == 1) {
+    a.M = (long long)N * H * W;
+    a.TA = H;
+    a.TB = W;
+    a.ost = 1;
+    a.ident = 1;
+    a.ntaps = R * S;
+    for (int r = 0; r < R; ++r)
+      for (int s = 0; s < S; ++s) {
+        const int t = r * S + s;
+        a.dh[t] = pad - r;
+        a.dw[t] = pad - s;
+        a.bcol[t] = t * Kout;
+      }
+    return run_igemm(a, st, nullptr);
+  }
+  // stride 2: one launch per parity class of the output pixel
+  bool zero_needed = false;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      int n = 0;
+      for (int r = 0; r < R; ++r)
+        for (int s = 0; s < S; ++s)
+          if (((ph + pad - r) & 1) == 0 && ((pw + pad - s) & 1) == 0) ++n;
+      if (n == 0) zero_needed = true;
+    }
+  if (zero_needed && hipMemsetAsync(dx, 0, (size_t)N * H * W * C * 2, st) != hipSuccess) return -5;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      ConvArgs c = a;
+      c.TA = (H - ph + 1) / 2;
+      c.TB = (W - pw + 1) / 2;
+      if (c.TA <= 0 || c.TB <= 0) continue;
+      c.M = (long long)N * c.TA * c.TB;
+      c.ost = 2;
+      c.oph = ph;
+      c.opw = pw;
+      c.ident = 0;
+      c.ntaps = 0;
+      for (int r = 0; r < R; ++r)
+        for (int s = 0; s < S; ++s) {
+          if (((ph + pad - r) & 1) || ((pw + pad - s) & 1)) continue;
+          c.dh[c.ntaps] = (ph + pad - r) / 2;
+          c.dw[c.ntaps] = (pw + pad - s) / 2;
+          c.bcol[c.ntaps] = (r * S + s) * Kout;
+          ++c.ntaps;
+        }
+      if (c.ntaps == 0) continue;
+      const int rc = run_igemm(c, st, nullptr);
+      if (rc) return rc;
+    }
+  return 0;
+}
+
+}  // namespace pdo

@@ -40,6 +40,18 @@ void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* s
 int bias_grad_scratch_floats(long long N, int F);
 int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st, int accumulate = 0);
 // NHWC BatchNorm (+ReLU, +residual) training forward / backward (batchnorm.hip)
+// conv.hip: NHWC implicit-GEMM convolutions (3×3 / strided 1×1, C % 64, Kout 64 or % 128)
+int conv_supported(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad);
+int conv_fwd_tiles(long long M, int Kout);
+int conv_fwd_tile_rows(int Kout);
+int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int Kout, int R, int S, int stride, int pad,
+                  bf16* y, float* tile_stats, hipStream_t st);
+int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t st);
+int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
+                    int pad, bf16* dx, hipStream_t st);
+int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
+                 const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
+                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st);
 int bn_fwd_scratch_floats(long long M, int C);
 int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float* running_mean, float* running_var,
            long long M, int C, float eps, float momentum, int relu, bf16* y, float* mean, float* invstd,

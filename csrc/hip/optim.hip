@@ -3,6 +3,8 @@
 // One pass: bf16 grad → ×(grad_scale · clip_coef) → fp32 moments/master →
 // bf16 compute copy.  The clip coefficient is read from device memory
 // (written by `sumsq`), so clipping costs no host synchronisation.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -68,6 +70,74 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16* __restrict__ p, const 
   }
 }
 
+// The same update, two 8-element vectors per thread per iteration with every
+// load of both issued before any math (14 loads in flight per lane instead of
+// 7), and non-temporal loads / stores: each byte of the 10 GB step is touched
+// once, so none of it is worth an L2 / MALL line (the next step's forward
+// re-reads the bf16 parameters, not the fp32 state).
+__device__ __forceinline__ f32x4 ntld4(const f32x4* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void ntst4(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
+
+__global__ __launch_bounds__(256) void adamw2_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
+                                                     float* __restrict__ master, float* __restrict__ m1,
+                                                     float* __restrict__ m2, const float* __restrict__ decay_chunks,
+                                                     const float* __restrict__ normsq, long long npair, float lr,
+                                                     float b1, float b2, float eps, float wd, float inv_bc1,
+                                                     float inv_sqrt_bc2, float grad_scale, float clip) {
+  float coef = grad_scale;
+  if (clip > 0.f) {
+    const float norm = sqrtf(normsq[0]);
+    coef *= fminf(1.f, clip / (norm + 1e-6f));
+  }
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < npair; q += stride) {
+    // vectors i0 = q and i1 = q + npair: two coalesced sweeps of the arena halves
+    const long long iv[2] = {q, q + npair};
+    bf16x8 gb[2];
+    f32x4 w[2][2], a[2][2], v[2][2];
+    float dec[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long long i = iv[u];
+      gb[u] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(g) + i);
+      const f32x4* mp = reinterpret_cast<const f32x4*>(master) + 2 * i;
+      const f32x4* ap = reinterpret_cast<const f32x4*>(m1) + 2 * i;
+      const f32x4* vp = reinterpret_cast<const f32x4*>(m2) + 2 * i;
+      w[u][0] = ntld4(mp);
+      w[u][1] = ntld4(mp + 1);
+      a[u][0] = ntld4(ap);
+      a[u][1] = ntld4(ap + 1);
+      v[u][0] = ntld4(vp);
+      v[u][1] = ntld4(vp + 1);
+      dec[u] = decay_chunks[i >> 7];  // 1024 elements per chunk = 128 vectors
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long long i = iv[u];
+      const f32x8 gr = to_f32(gb[u]) * coef;
+      const float shrink = 1.f - lr * wd * dec[u];
+      f32x8 wo;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 ah = a[u][h], vh = v[u][h], wh = w[u][h];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float gj = gr[4 * h + j];
+          ah[j] = b1 * ah[j] + (1.f - b1) * gj;
+          vh[j] = b2 * vh[j] + (1.f - b2) * gj * gj;
+          const float upd = (ah[j] * inv_bc1) / (sqrtf(vh[j]) * inv_sqrt_bc2 + eps);
+          wh[j] = wh[j] * shrink - lr * upd;
+          wo[4 * h + j] = wh[j];
+        }
+        ntst4(reinterpret_cast<f32x4*>(master) + 2 * i + h, wh);
+        ntst4(reinterpret_cast<f32x4*>(m1) + 2 * i + h, ah);
+        ntst4(reinterpret_cast<f32x4*>(m2) + 2 * i + h, vh);
+      }
+      reinterpret_cast<bf16x8*>(p)[i] = to_bf16(wo);
+    }
+  }
+}
+
 int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, float* out, hipStream_t st) {
   if (n % 8) return -2;
   int G = stream_grid(n / 8, 256);
@@ -82,8 +152,21 @@ int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, cons
                float bc2, float grad_scale, float clip, hipStream_t st) {
   if (n % 1024) return -2;
   const long long nvec = n / 8;
-  adamw_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr, b1, b2,
-                                                        eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
+  // PDO_ADAMW=2: two vectors per lane with non-temporal loads / stores — measured
+  // 3.21 ms vs 1.98 for the plain kernel in the GPT-2-medium step (round 4,
+  // profiles/r4b_step_kernels.md): off
+  static const int v1 = [] {
+    const char* e = getenv("PDO_ADAMW");
+    return e && *e ? (atoi(e) == 2 ? 0 : 1) : 1;
+  }();
+  if (v1 == 1 || nvec % 2) {
+    adamw_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr, b1, b2,
+                                                          eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
+    return 0;
+  }
+  const long long npair = nvec / 2;
+  adamw2_kernel<<<stream_grid(npair, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, npair, lr, b1,
+                                                          b2, eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
   return 0;
 }
 

@@ -1,0 +1,88 @@
+"""NHWC implicit-GEMM convolutions (csrc/hip/conv.hip) against fp32 PyTorch references.
+
+Shapes are ResNet-50's (3×3 stride 1 / 2, strided 1×1 downsample) at small
+batch, plus partial last M-tiles (token count not a multiple of the tile).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from paddle_operator_amd import _native
+    return _native.require_hip()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _mk(N, C, H, K, R, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(N, C, H, H, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda", generator=g) / (C * R * R) ** 0.5).bfloat16()
+    return x, w.contiguous(memory_format=torch.channels_last)
+
+
+# (N, C, H, K, R, stride): 3×3 s1 (Kout 64 → 256×64 tiles; 128 → 128×128), 3×3 s2, 1×1 s2 downsample,
+# H = 7 / 5 with N = 3: token counts that leave a partial last tile
+SHAPES = [(2, 64, 16, 64, 3, 1), (2, 128, 14, 128, 3, 1), (2, 128, 16, 128, 3, 2), (3, 64, 7, 128, 3, 1),
+          (2, 256, 14, 512, 1, 2), (3, 128, 5, 256, 3, 2), (2, 512, 7, 512, 3, 1)]
+
+
+@pytest.mark.parametrize("N,C,H,K,R,stride", SHAPES)
+def test_conv_fwd_and_tile_stats(hip, N, C, H, K, R, stride):
+    x, w = _mk(N, C, H, K, R, 1)
+    pad = (R - 1) // 2
+    assert hip.conv_ok(N, H, H, C, K, R, R, stride, pad)
+    y, st = hip.conv_fwd(x, w, stride, pad, True)
+    ref = F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 1e-2
+    # tile statistics reproduce the per-channel mean / biased variance of the bf16 output
+    rows = hip.conv_tile_rows(K)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, K)
+    M = yf.shape[0]
+    assert st.shape == ((M + rows - 1) // rows, 2, K)
+    mean = st[:, 0].sum(0) / M
+    n = torch.tensor([min(rows, M - i * rows) for i in range(st.shape[0])], device="cuda", dtype=torch.float32)
+    var = (st[:, 1].sum(0) + (n[:, None] * (st[:, 0] / n[:, None] - mean) ** 2).sum(0)) / M
+    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(var, yf.var(0, unbiased=False), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,C,H,K,R,stride", SHAPES)
+def test_conv_dgrad(hip, N, C, H, K, R, stride):
+    x, w = _mk(N, C, H, K, R, 2)
+    pad = (R - 1) // 2
+    xf = x.float().requires_grad_()
+    ref = F.conv2d(xf, w.float(), stride=stride, padding=pad)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    dy = torch.randn(ref.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    ref.backward(dy.float())
+    wt = hip.conv_weight_t(w)
+    assert wt.shape == (C, R * R * K)
+    dx = hip.conv_dgrad(dy, wt, C, R, R, H, H, stride, pad)
+    assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(dx, xf.grad) < 1e-2
+
+
+def test_bn_from_tile_stats_matches_stats_pass(hip):
+    """BatchNorm forward from the conv epilogue's tile partials equals the
+    stats-pass BatchNorm (bn_act_fwd) on the same activation."""
+    x, w = _mk(4, 64, 14, 64, 3, 5)
+    y, st = hip.conv_fwd(x, w, 1, 1, True)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    gamma = torch.rand(64, device="cuda", generator=g) + 0.5
+    beta = torch.randn(64, device="cuda", generator=g) * 0.1
+    rm1, rv1 = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    a, m_a, i_a = hip.bn_act_fwd(y, None, gamma, beta, rm1, rv1, 1e-5, 0.1, True)
+    b, m_b, i_b = hip.bn_act_fwd_tiles(y, st, hip.conv_tile_rows(64), None, gamma, beta, rm2, rv2, 1e-5, 0.1, True)
+    torch.testing.assert_close(m_b, m_a, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(i_b, i_a, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rv2, rv1, rtol=1e-3, atol=1e-5)
+    assert _rel(b, a) < 1e-2

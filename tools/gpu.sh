@@ -62,7 +62,7 @@ run_step() {
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 "$R/tools/$s" "${rest[@]}" ) \
         > "$O/$tag.log" 2>&1 || { tail -30 "$O/$tag.log"; return 1; }
       local db; db=$(find "$d" -name '*.db' | head -1)
-      local steps=1; [[ $kind == step ]] && steps=9  # 2 warmup + 7 timed steps are all traced
+      local steps=0; [[ $kind == step ]] && steps=9  # 2 warmup + 7 timed steps are all traced; 0 = count AdamW dispatches
       python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/$tag.md" && rm -rf "$d"
       tail -5 "$O/$tag.log"; head -45 "$O/$tag.md" ;;
     pmc)

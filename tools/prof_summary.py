@@ -37,7 +37,7 @@ def short(name: str) -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--steps", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=0, help="traced steps (0: count the AdamW dispatches)")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--title", default="")
     a = ap.parse_args()
@@ -51,7 +51,13 @@ def main():
         agg[k][0] += 1
         agg[k][1] += dur
     total = sum(v[1] for v in agg.values())
+    if a.steps <= 0:
+        # traced steps = optimizer dispatches (one fused AdamW per step); a plain
+        # trace without an optimizer has no step column
+        a.steps = sum(1 for r in rows if "adamw" in r[0])
     print(f"# rocprofv3 kernel summary {a.title}\n")
+    if a.steps:
+        print(f"ms/step = total ms / {a.steps} traced steps (optimizer dispatches)\n")
     print(f"dispatches: {len(rows)}  kernel time: {total/1e6:.2f} ms  span: {(t1-t0)/1e6:.2f} ms\n")
     hdr = "| kernel | calls | total ms | mean us | % |"
     if a.steps:
