@@ -478,6 +478,31 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor wt, int64_t C, int64_t R, int64_
   return dx;
 }
 
+// dw (fp32 [K, C, R, S] channels_last, e.g. the flat arena's slice) (+)= the weight
+// gradient of y = conv(x, w) for dy; without `out` a new fp32 tensor
+at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                      c10::optional<at::Tensor> out) {
+  CHECK_BF16(dy); CHECK_BF16(x);
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_wgrad: channels_last bf16 dy, x");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
+  at::Tensor dw;
+  const bool acc = out.has_value() && out->defined();
+  if (acc) {
+    dw = *out;
+    CHECK_F32(dw);
+    TORCH_CHECK(dw.numel() == (int64_t)K * C * R * S && dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_wgrad: out must be a channels_last fp32 [K, C, R, S]");
+  } else {
+    dw = at::empty({K, C, R, S}, x.options().dtype(at::kFloat), at::MemoryFormat::ChannelsLast);
+  }
+  auto scratch = at::empty({pdo::conv_wgrad_scratch_floats(N, H, W, C, K, (int)R, (int)S, (int)stride, (int)pad)},
+                           x.options().dtype(at::kFloat));
+  CHECK_RC(pdo::conv_wgrad_nhwc(bp(dy), bp(x), N, H, W, C, K, (int)R, (int)S, (int)stride, (int)pad, fp(dw),
+                                acc ? 1 : 0, fp(scratch), cur_stream()), "conv_wgrad_nhwc");
+  return dw;
+}
+
 // BatchNorm (+ residual) (+ ReLU) forward from conv_fwd's tile statistics
 std::vector<at::Tensor> bn_act_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t tile_rows,
                                          c10::optional<at::Tensor> res, at::Tensor w, at::Tensor b,
@@ -775,6 +800,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("conv_tile_rows", &conv_tile_rows);
   m.def("conv_weight_t", &conv_weight_t);
   m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
+        py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);

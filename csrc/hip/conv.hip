@@ -54,6 +54,7 @@ namespace {
 
 constexpr int CNT = 256;
 constexpr unsigned OOB = 0x80000000u;  // ≥ any buffer's num_records: the load returns zeros
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
 
 template <typename Fn, int... I>
 __device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, I...>) {
@@ -306,6 +307,169 @@ __global__ __launch_bounds__(256) void conv_wt_kernel(const bf16* __restrict__ w
   }
 }
 
+// ============================================================================
+// weight gradient: dW[co][tap][ci] = Σ_t dY[t][co] · X[pixel(t, tap)][ci]
+// Token-major GEMM (the reduction runs over the forward's output tokens): a
+// workgroup owns BMW output channels × BNW input channels of ONE tap and a
+// slice of the tokens (split-K, fp32 partials [slice][Kout][T·C] folded by
+// conv_wgrad_reduce in a fixed order — deterministic).  Per 64-token k-step
+// both operands reach LDS as they lie in memory, rows = tokens: dY rows
+// straight, X rows gathered per token for the tap (buffer_load … lds, zeros
+// for padding pixels and tokens past M).  Fragments are read with
+// ds_read_b64_tr_b16 (lane group g takes tokens 4g..4g+3 and 16+4g.. of 16
+// columns — the same token permutation for both operands), so the MFMA
+// v_mfma_f32_16x16x32_bf16 sums over tokens.  LDS rows of 128 / 256 B with
+// the 32-B column group XORed by the row (128 B: bits of (r >> 1) & 3, 256 B:
+// r & 7): the 8 rows a transposed read touches per half-wave hit 8 distinct
+// bank groups.
+// ============================================================================
+struct WgradArgs {
+  const bf16* dy;        // [M][Kout]
+  const bf16* x;         // NHWC [N][IH][IW][C]
+  float* part;           // [splits][Kout][T·C]
+  long long M;
+  int Kout, C, T, S;     // T taps, S = kernel width (tap = r·S + s)
+  int IH, IW, TA, TB;    // forward output grid: token t = (n·TA + ho)·TB + wo
+  float inv_TA, inv_TB;
+  int st, pad;
+  unsigned xbytes, dybytes;
+  int splits, ksteps;
+};
+
+template <int ROWB>
+__device__ __forceinline__ int wswz(int r) {
+  return ROWB == 256 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1);
+}
+
+template <int BMW, int BNW>
+__global__ __launch_bounds__(CNT, 2) void conv_wgrad_kernel(const WgradArgs a) {
+  constexpr int RA = BMW * 2, RB = BNW * 2;          // LDS row bytes
+  constexpr int LA = BMW / 8, LB = BNW / 8;          // lanes per row (16 B each)
+  constexpr int PA = BMW / 8, PB = BNW / 8;          // 1-KiB pieces per 64-token k-step
+  constexpr int NA = PA / 4, NB = PB / 4;            // per wave
+  constexpr int SA = 64 * RA, STAGE = 64 * (RA + RB);
+  constexpr int MI = BMW / 32, NJ = BNW / 32;        // 16×16 blocks per wave (wave tile BMW/2 × BNW/2)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int tiles_m = a.Kout / BMW, tiles_n = a.T * a.C / BNW;
+  int id = blockIdx.x;
+  const int split = id / (tiles_m * tiles_n);
+  id -= split * tiles_m * tiles_n;
+  const int tm = id % tiles_m, tn = id / tiles_m;
+  const int co0 = tm * BMW;
+  const int ncol0 = tn * BNW, tap = ncol0 / a.C, ci0 = ncol0 - tap * a.C;
+  const int r = tap / a.S, s = tap - r * a.S;
+  const int kq = a.ksteps / a.splits, kr = a.ksteps % a.splits;
+  const int k0 = split * kq + min(split, kr), nk = kq + (split < kr ? 1 : 0);
+
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // per-lane constant parts of the pieces: row in the tile, source chunk
+  auto issue = [&](int kt, int stage) {
+    const long long t0 = (long long)kt * 64;
+    const unsigned sb = lds0 + (unsigned)(stage * STAGE);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int p = w + 4 * i;
+      const int row = p * (64 / LA) + lane / LA;
+      const int c = (lane % LA) ^ wswz<RA>(row);
+      const long long t = t0 + row;
+      const unsigned v = t < a.M ? (unsigned)((t * a.Kout + co0 + c * 8) * 2) : OOB;
+      bufld(v, rsY, sb + (unsigned)(p * 1024));
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int p = w + 4 * i;
+      const int row = p * (64 / LB) + lane / LB;
+      const int c = (lane % LB) ^ wswz<RB>(row);
+      const long long t = t0 + row;
+      unsigned v = OOB;
+      if (t < a.M) {
+        int q, wo, n, ho;
+        divmod((int)t, a.TB, a.inv_TB, q, wo);
+        divmod(q, a.TA, a.inv_TA, n, ho);
+        const int hi = ho * a.st - a.pad + r, wi = wo * a.st - a.pad + s;
+        if ((unsigned)hi < (unsigned)a.IH && (unsigned)wi < (unsigned)a.IW)
+          v = (unsigned)(((((long long)n * a.IH + hi) * a.IW + wi) * a.C + ci0 + c * 8) * 2);
+      }
+      bufld(v, rsX, sb + (unsigned)(SA + p * 1024));
+    }
+  };
+  // transposed fragment of the 16 columns cb..cb+15, tokens 32kk + {4g..4g+3, 16+4g..}
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  auto frag = [&](const char* T, int cb, int kk, auto rowb) -> bf16x8 {
+    constexpr int RW = decltype(rowb)::value;
+    const int col = cb + 4 * p4;
+    const int r0 = 32 * kk + 4 * g + q4, r1 = r0 + 16;
+    const char* a0 = T + r0 * RW + (((col >> 3) ^ wswz<RW>(r0)) << 4) + (col & 7) * 2;
+    const char* a1 = T + r1 * RW + (((col >> 3) ^ wswz<RW>(r1)) << 4) + (col & 7) * 2;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a0);
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a1);
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  using IRA = std::integral_constant<int, RA>;
+  using IRB = std::integral_constant<int, RB>;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(k0, 0);
+  for (int k = 0; k < nk; ++k) {
+    if (k + 1 < nk) {
+      issue(k0 + k + 1, (k + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* TA_ = smem + (k & 1) * STAGE;
+    const char* TB_ = TA_ + SA;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 fa[MI], fb[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = frag(TA_, wm * (BMW / 2) + 16 * i, kk, IRA{});
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = frag(TB_, wn * (BNW / 2) + 16 * j, kk, IRB{});
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // acc[i][j][e] = dW[co0 + wm·BMW/2 + 16i + 4g + e][tap·C + ci0 + wn·BNW/2 + 16j + (l & 15)]
+  const long long ldo = (long long)a.T * a.C;
+  float* out = a.part + (size_t)split * a.Kout * ldo;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = co0 + wm * (BMW / 2) + 16 * i + 4 * g + e;
+      float* orow = out + co * ldo + ncol0 + wn * (BNW / 2) + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) orow[16 * j] = acc[i][j][e];
+    }
+}
+
+// out[i] (+)= Σ_s part[s][i], s in order (fp32, 4 per lane)
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int splits,
+                                                                long long n4, float* __restrict__ out,
+                                                                int accumulate) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    f32x4 v = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < splits; ++k) v += reinterpret_cast<const f32x4*>(part)[(long long)k * n4 + i];
+    reinterpret_cast<f32x4*>(out)[i] = v;
+  }
+}
+
 template <int BM, int BN>
 int launch_igemm(const ConvArgs& a, hipStream_t st) {
   const long long tiles = ((a.M + BM - 1) / BM) * (a.Kout / BN);
@@ -458,6 +622,65 @@ int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, 
       const int rc = run_igemm(c, st, nullptr);
       if (rc) return rc;
     }
+  return 0;
+}
+
+// split count of conv_wgrad: ≈ 2 workgroups per CU over the output tiles, ≥ 8
+// 64-token k-steps per slice
+static void wgrad_cfg(int Kout, int C, int T, long long M, int* bmw, int* bnw, int* splits) {
+  *bmw = Kout % 128 == 0 ? 128 : 64;
+  *bnw = C % 128 == 0 ? 128 : 64;
+  const long long tiles = (long long)(Kout / *bmw) * (T * C / *bnw);
+  const long long ks = (M + 63) / 64;
+  long long sp = (512 + tiles - 1) / tiles;
+  if (sp > ks / 8) sp = ks / 8;
+  if (sp > 64) sp = 64;
+  if (sp < 1) sp = 1;
+  *splits = (int)sp;
+}
+
+long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  int bm, bn, sp;
+  wgrad_cfg(Kout, C, R * S, (long long)N * Ho * Wo, &bm, &bn, &sp);
+  return (long long)sp * Kout * R * S * C;
+}
+
+// dw [Kout][R][S][C] fp32 (+)= Σ_t dy[t] ⊗ x[pixel(t, tap)]; scratch: conv_wgrad_scratch_floats
+int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
+                    int pad, float* dw, int accumulate, float* scratch, hipStream_t st) {
+  if (!conv_supported(N, H, W, C, Kout, R, S, stride, pad)) return -2;
+  WgradArgs a{};
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  a.dy = dy;
+  a.x = x;
+  a.part = scratch;
+  a.M = (long long)N * Ho * Wo;
+  a.Kout = Kout;
+  a.C = C;
+  a.T = R * S;
+  a.S = S;
+  a.IH = H;
+  a.IW = W;
+  a.TA = Ho;
+  a.TB = Wo;
+  a.inv_TA = 1.f / (float)Ho;
+  a.inv_TB = 1.f / (float)Wo;
+  a.st = stride;
+  a.pad = pad;
+  a.xbytes = (unsigned)((long long)N * H * W * C * 2);
+  a.dybytes = (unsigned)(a.M * Kout * 2);
+  a.ksteps = (int)((a.M + 63) / 64);
+  int bm, bn;
+  wgrad_cfg(Kout, C, a.T, a.M, &bm, &bn, &a.splits);
+  const long long grid = (long long)(Kout / bm) * (a.T * C / bn) * a.splits;
+  if (grid > 0x7fffffffLL) return -2;
+  if (bm == 128 && bn == 128) conv_wgrad_kernel<128, 128><<<(unsigned)grid, CNT, 0, st>>>(a);
+  else if (bm == 128) conv_wgrad_kernel<128, 64><<<(unsigned)grid, CNT, 0, st>>>(a);
+  else if (bn == 128) conv_wgrad_kernel<64, 128><<<(unsigned)grid, CNT, 0, st>>>(a);
+  else conv_wgrad_kernel<64, 64><<<(unsigned)grid, CNT, 0, st>>>(a);
+  const long long n4 = (long long)Kout * a.T * C / 4;
+  conv_wgrad_reduce_kernel<<<stream_grid(n4, 256), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
   return 0;
 }
 

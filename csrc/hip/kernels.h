@@ -49,6 +49,9 @@ int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int 
 int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t st);
 int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
                     int pad, bf16* dx, hipStream_t st);
+long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad);
+int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
+                    int pad, float* dw, int accumulate, float* scratch, hipStream_t st);
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
                  float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st);

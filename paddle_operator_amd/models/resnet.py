@@ -2,11 +2,13 @@
 elastic ResNet-50) — written out here because torchvision is not part of the
 image.  Standard v1.5 bottleneck architecture (stride on the 3×3 conv).
 
-MI355X choices: channels_last activations + bf16 autocast so MIOpen picks
-its NHWC implicit-GEMM convolutions on the matrix cores; BatchNorm (fp32
-statistics and affine params) fused with ReLU and the residual add into HIP
-kernels (ops.bn_act); parameters live in a flat fp32 arena (parallel.flat) so
-the gradient all-reduce buckets are slices.
+MI355X choices: channels_last bf16 activations; the 3×3 and strided 1×1
+convolutions on the hand-written NHWC implicit GEMM (csrc/hip/conv.hip, BatchNorm
+statistics from its epilogue), the 1×1 stride-1 ones as token-major GEMMs
+(gemm_nt4 / gemm_dw4), only the 7×7 stem (3 input channels) on MIOpen;
+BatchNorm (fp32 statistics and affine params) fused with ReLU and the residual
+add into HIP kernels (ops.bn_act); parameters live in a flat fp32 arena
+(parallel.flat) so the gradient all-reduce buckets are slices.
 """
 from __future__ import annotations
 
@@ -35,11 +37,13 @@ class Bottleneck(nn.Module):
         # BN + ReLU (+ residual add) fused into one HIP pass each (ops.bn_act)
         # 1×1 stride-1 convolutions as token-major GEMMs (ops.conv1x1: gemm_nt4 /
         # gemm_dw4 / MIOpen per product, whichever measured faster at the shape)
+        # 3×3 and strided 1×1 convolutions on the NHWC implicit GEMM with the
+        # BatchNorm statistics in its epilogue (ops.conv_bn_act, csrc/hip/conv.hip)
         idt = x
         out = ops.bn_act(self.bn1, ops.conv1x1(self.conv1, x))
-        out = ops.bn_act(self.bn2, self.conv2(out))
+        out = ops.conv_bn_act(self.conv2, self.bn2, out)
         if self.downsample is not None:
-            idt = ops.bn_act(self.downsample[1], ops.conv1x1(self.downsample[0], x), relu=False)
+            idt = ops.conv_bn_act(self.downsample[0], self.downsample[1], x, relu=False)
         return ops.bn_act(self.bn3, ops.conv1x1(self.conv3, out), relu=True, residual=idt)
 
 

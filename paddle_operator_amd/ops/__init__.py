@@ -830,12 +830,18 @@ class _BNActFn(torch.autograd.Function):
     """y = act(BN(x) [+ residual]) with batch statistics (csrc/hip/batchnorm.hip).
 
     Without a residual the backward recomputes the ReLU mask from x, so only
-    x (the conv output autograd keeps anyway) and two [C] vectors are saved."""
+    x (the conv output autograd keeps anyway) and two [C] vectors are saved.
+    ``stats``: the producing convolution's per-tile partials (conv.hip), so the
+    forward skips its statistics pass over x."""
 
     @staticmethod
-    def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu):
+    def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu, stats=None, tile_rows=0):
         m = _native.require_hip()
-        y, mean, invstd = m.bn_act_fwd(x, residual, w, b, running_mean, running_var, eps, momentum, relu)
+        if stats is not None:
+            y, mean, invstd = m.bn_act_fwd_tiles(x, stats, tile_rows, residual, w, b, running_mean, running_var, eps,
+                                                 momentum, relu)
+        else:
+            y, mean, invstd = m.bn_act_fwd(x, residual, w, b, running_mean, running_var, eps, momentum, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
         keep_y = relu and ctx.has_res
@@ -856,7 +862,7 @@ class _BNActFn(torch.autograd.Function):
             pw._pdo_ready(pw)
             pb._pdo_ready(pb)
             dw = db = None
-        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None
+        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None
 
 
 _BN_FUSED = [os.environ.get("PDO_BN_FUSED", "1") != "0"]
@@ -954,6 +960,84 @@ def conv1x1(conv: torch.nn.Conv2d, x):
             and (x.shape[0] * x.shape[2] * x.shape[3]) % 256 == 0):
         return _Conv1x1Fn.apply(x, conv.weight)
     return conv(x)
+
+
+class _ConvFn(torch.autograd.Function):
+    """y = conv2d(x, w) for a channels_last bf16 activation on the hand-written
+    NHWC implicit GEMM (csrc/hip/conv.hip): 3×3 stride 1 / 2 and strided 1×1,
+    forward (+ BatchNorm tile statistics, a second non-differentiable output),
+    input gradient (Wᵀ built per backward, stride-2 parity classes) and weight
+    gradient (split-K, fp32 — straight into the flat fp32 arena when the
+    parameter allows it).  Replaces MIOpen's igemm fwd / bwd / wrw solvers and
+    their zero-fill / cast passes on ResNet-50 (profiles/r3t_resnet50_kernels.md)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, want_stats):
+        m = _native.require_hip()
+        wb = w.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y, st = m.conv_fwd(x, wb, stride, pad, want_stats)
+        ctx.save_for_backward(x, wb)
+        ctx.stride, ctx.pad = stride, pad
+        ctx.wparam = w
+        if st is not None:
+            ctx.mark_non_differentiable(st)
+        return y, st
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        m = _native.require_hip()
+        x, wb = ctx.saved_tensors
+        K, C, R, S = wb.shape
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = m.conv_dgrad(dy, m.conv_weight_t(wb), C, R, S, x.shape[2], x.shape[3], ctx.stride, ctx.pad)
+        if ctx.needs_input_grad[1]:
+            p = ctx.wparam
+            if (_direct_ok(p) and p.grad.dtype == torch.float32
+                    and p.grad.is_contiguous(memory_format=torch.channels_last)):
+                m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad, out=p.grad)
+                p._pdo_ready(p)
+            else:
+                dw = m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad).to(p.dtype)
+        return dx, dw, None, None, None
+
+
+_HIP_CONV = [os.environ.get("PDO_HIP_CONV", "1") != "0"]
+
+
+def _hip_conv_ok(conv: torch.nn.Conv2d, x) -> bool:
+    if not (_HIP_CONV[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.groups == 1 and conv.bias is None
+            and conv.dilation == (1, 1) and conv.kernel_size[0] == conv.kernel_size[1]
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]):
+        return False
+    R, st, pad = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+    if R == 1 and st == 1:
+        return False  # 1×1 stride 1: the token-major GEMM path (conv1x1)
+    N, C, H, W = x.shape
+    return bool(_native.require_hip().conv_ok(N, H, W, C, conv.out_channels, R, R, st, pad))
+
+
+def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
+    """act(BN(conv(x)) [+ residual]) — on the HIP implicit-GEMM convolution with
+    the BatchNorm statistics taken in its epilogue where the shapes allow;
+    otherwise the 1×1 GEMM path / the framework convolution + ops.bn_act."""
+    if _hip_conv_ok(conv, x) and bn.training and _BN_FUSED[0] and bn.weight is not None and \
+            bn.weight.dtype == torch.float32 and (residual is None or (
+                residual.dtype == torch.bfloat16 and residual.is_contiguous(memory_format=torch.channels_last))):
+        y, st = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True)
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        rows = _native.require_hip().conv_tile_rows(conv.out_channels)
+        return _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu,
+                              st, rows)
+    if conv.kernel_size == (1, 1) and conv.stride == (1, 1):
+        y = conv1x1(conv, x)
+    elif _hip_conv_ok(conv, x):
+        y = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], False)[0]
+    else:
+        y = conv(x)
+    return bn_act(bn, y, relu=relu, residual=residual)
 
 
 class _MaxPool3s2Fn(torch.autograd.Function):
