@@ -230,6 +230,21 @@ std::vector<at::Tensor> embed_bwd(at::Tensor dy, at::Tensor idx, int64_t Vp, int
   return {dwte, dwpe};
 }
 
+// d(wte) accumulated into `dwte` (the gradient arena's bf16 [Vp, C] slice) from the
+// stably sorted token ids (keys, perm = torch.sort(idx.flatten(), stable=True));
+// returns d(wpe)
+at::Tensor embed_bwd_sorted(at::Tensor dy, at::Tensor keys, at::Tensor perm, at::Tensor dwte, int64_t P) {
+  CHECK_IN(dy); CHECK_IN(keys); CHECK_IN(perm); CHECK_IN(dwte);
+  CHECK_BF16(dy); CHECK_I64(keys); CHECK_I64(perm); CHECK_BF16(dwte);
+  TORCH_CHECK(dy.dim() == 3 && keys.numel() == dy.size(0) * dy.size(1) && perm.numel() == keys.numel());
+  const int B = dy.size(0), S = dy.size(1), C = dy.size(2);
+  TORCH_CHECK(S <= P && dwte.dim() == 2 && dwte.size(1) == C);
+  auto dwpe = at::empty({P, C}, dy.options());
+  CHECK_RC(pdo::embed_bwd_sorted(bp(dy), keys.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), bp(dwte), bp(dwpe), B,
+                                 S, C, (int)dwte.size(0), (int)P, 1, cur_stream()), "embed_bwd_sorted");
+  return dwpe;
+}
+
 // ---------------------------------------------------------------- optimizer
 void sumsq(at::Tensor g, at::Tensor out, double scale) {
   CHECK_IN(g); CHECK_IN(out); CHECK_BF16(g); CHECK_F32(out);
@@ -770,6 +785,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("xent_fused", &xent_fused);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
+  m.def("embed_bwd_sorted", &embed_bwd_sorted);
   m.def("sumsq", &sumsq);
   m.def("adamw_flat", &adamw_flat);
   m.def("splitk_add", &splitk_add);

@@ -3,7 +3,9 @@
 // Forward: one wave per token row, y = wte[idx] + wpe[pos] with 16-B vectors.
 // Backward: d(wte) by f32 atomics shaped as 256 contiguous bytes per wave
 // instruction (one row segment per instruction, the fast atomic shape on
-// MI355X) into a zeroed f32 table, then one vectorised cast to bf16;
+// MI355X) into a zeroed f32 table, then one vectorised cast to bf16 — or,
+// deterministic and cheaper (embed_bwd_sorted), a segmented sum over the
+// stably sorted token ids straight into the gradient rows;
 // d(wpe) is a deterministic per-position sum over the batch.
 #include "common.h"
 #include "kernels.h"
@@ -47,6 +49,31 @@ __global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const bf16* __restri
   }
 }
 
+// d(wte) without atomics: the token ids sorted stably (keys) with their row
+// indices (perm); the wave at the first position of each run of equal keys
+// sums the run's dy rows in sorted (= row) order and adds the sum into that
+// token's gradient row — deterministic, no [Vp, C] fp32 table, no memset, no
+// cast pass; rows of tokens absent from the batch are not touched
+__global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(const bf16* __restrict__ dy,
+                                                               const int64_t* __restrict__ keys,
+                                                               const int64_t* __restrict__ perm,
+                                                               bf16* __restrict__ g, int N, int C, int Vp,
+                                                               int accumulate) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= N) return;
+  const int64_t tok = keys[i];
+  if (i > 0 && keys[i - 1] == tok) return;  // not the start of a run
+  if (tok < 0 || tok >= Vp) return;
+  bf16* out = g + (size_t)tok * C;
+  for (int c8 = lane; c8 < (C >> 3); c8 += 64) {
+    f32x8 t = accumulate ? to_f32(reinterpret_cast<const bf16x8*>(out)[c8]) : f32x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = i; j < N && keys[j] == tok; ++j)
+      t += to_f32(reinterpret_cast<const bf16x8*>(dy + (size_t)perm[j] * C)[c8]);
+    reinterpret_cast<bf16x8*>(out)[c8] = to_bf16(t);
+  }
+}
+
 __global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ in, bf16* __restrict__ out,
                                                           long long nvec) {
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
@@ -74,6 +101,18 @@ int embed_bwd(const bf16* dy, const int64_t* idx, float* acc, bf16* dwte, bf16* 
   f32_to_bf16_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(acc, dwte, nvec);
   hipMemsetAsync(dwpe, 0, (size_t)P * C * sizeof(bf16), st);
   embed_bwd_wpe_kernel<<<S, 256, 0, st>>>(dy, dwpe, B, S, C);
+  return 0;
+}
+
+int embed_bwd_sorted(const bf16* dy, const int64_t* keys, const int64_t* perm, bf16* dwte, bf16* dwpe, int B, int S,
+                     int C, int Vp, int P, int accumulate, hipStream_t st) {
+  if (C % 8) return -2;
+  const int N = B * S;
+  embed_bwd_sorted_kernel<<<(N + 3) / 4, 256, 0, st>>>(dy, keys, perm, dwte, N, C, Vp, accumulate);
+  if (dwpe) {
+    hipMemsetAsync(dwpe, 0, (size_t)P * C * sizeof(bf16), st);
+    embed_bwd_wpe_kernel<<<S, 256, 0, st>>>(dy, dwpe, B, S, C);
+  }
   return 0;
 }
 

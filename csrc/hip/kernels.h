@@ -116,6 +116,8 @@ int xent_bwd(const bf16* logits, const int64_t* tgt, const float* lse, const flo
 int embed_fwd(const int64_t* idx, const bf16* wte, const bf16* wpe, bf16* y, int B, int S, int C, hipStream_t st);
 int embed_bwd(const bf16* dy, const int64_t* idx, float* acc, bf16* dwte, bf16* dwpe, int B, int S, int C, int Vp,
               int P, hipStream_t st);
+int embed_bwd_sorted(const bf16* dy, const int64_t* keys, const int64_t* perm, bf16* dwte, bf16* dwpe, int B, int S,
+                     int C, int Vp, int P, int accumulate, hipStream_t st);
 int cast_f32_bf16(const float* in, bf16* out, long long n, hipStream_t st);
 
 // optim.hip

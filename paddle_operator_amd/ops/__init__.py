@@ -694,14 +694,17 @@ class _LMHeadXentFn(torch.autograd.Function):
         dh, dw = ctx.saved_tensors
         # scaled in fp32, rounded once: a non-unit dloss (1/accum_steps) is not
         # first rounded to bf16
-        d = dloss.float()
+        # in place, one pass each: x = bf16(f32(x) · dloss) with dloss read on device
+        m = _native.require_hip()
+        d = dloss.float().reshape(1).contiguous()
+        m.scale_dev_(dh, d)
         sp = ctx.split
         if sp is not None:
-            _native.require_hip().scale_dev_(sp.grad, d.reshape(1).contiguous())
+            m.scale_dev_(sp.grad, d)
             sp.ready(sp)
-            return (dh.float() * d).to(dh.dtype).view(ctx.shape), None, None, None, None
-        return ((dh.float() * d).to(dh.dtype).view(ctx.shape), (dw.float() * d).to(dw.dtype),
-                None, None, None)
+            return dh.view(ctx.shape), None, None, None, None
+        m.scale_dev_(dw, d)
+        return dh.view(ctx.shape), dw, None, None, None
 
 
 class _SplitHeadLinearFn(torch.autograd.Function):
@@ -804,12 +807,25 @@ class _EmbedFn(torch.autograd.Function):
         ctx.wte_shape = wte.shape
         ctx.wpe_shape = wpe.shape
         ctx.dtype = wte.dtype
+        ctx.wte = wte
         return y
 
     @staticmethod
     def backward(ctx, dy):
         m = _native.require_hip()
         (idx,) = ctx.saved_tensors
+        wte = ctx.wte
+        g = wte.grad
+        # split tied weight (parallel/flat.py): the LM head's part of the gradient has
+        # its own slot, so the embedding is this slot's only producer — add straight
+        # into it (sorted segmented sum, deterministic), no fp32 table, no
+        # AccumulateGrad add
+        if (getattr(wte, "_pdo_split", None) is not None and g is not None and g.dtype == torch.bfloat16
+                and g.is_contiguous() and ctx.dtype == torch.bfloat16 and not torch.is_grad_enabled()):
+            keys, perm = torch.sort(idx.reshape(-1), stable=True)
+            dwpe = m.embed_bwd_sorted(dy.contiguous(), keys, perm, g, ctx.wpe_shape[0])
+            wte._pdo_ready(wte)
+            return None, None, dwpe
         dwte, dwpe = m.embed_bwd(dy.contiguous(), idx, ctx.wte_shape[0], ctx.wpe_shape[0])
         return None, dwte.to(ctx.dtype), dwpe.to(ctx.dtype)
 

@@ -349,6 +349,30 @@ def test_embedding(cuda):
     assert rel_err(wpe.grad, pf.grad) < 2e-2
 
 
+def test_embedding_sorted_backward_into_arena(cuda):
+    """The deterministic sorted segmented d(wte) (split tied weight: written
+    straight into the gradient slot) equals the fp32-atomic table path, adds
+    onto what the slot holds, and leaves rows of absent tokens untouched."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    B, S, C, Vp, P = 4, 128, 256, 1024, 256
+    g = torch.Generator(device=cuda).manual_seed(14)
+    idx = torch.randint(0, 300, (B, S), device=cuda, generator=g)
+    idx[1, :40] = 5  # a long run of one token
+    dy = torch.randn(B, S, C, device=cuda, generator=g).bfloat16()
+    ref_wte, ref_wpe = m.embed_bwd(dy, idx, Vp, P)
+    base = torch.randn(Vp, C, device=cuda, generator=g).bfloat16()
+    slot = base.clone()
+    keys, perm = torch.sort(idx.reshape(-1), stable=True)
+    dwpe = m.embed_bwd_sorted(dy, keys, perm, slot, P)
+    torch.testing.assert_close((slot.float() - base.float()), ref_wte.float(), atol=3e-2, rtol=2e-2)
+    assert torch.equal(slot[300:], base[300:])  # tokens ≥ 300 never occur
+    assert torch.equal(dwpe, ref_wpe)
+    slot2 = base.clone()
+    m.embed_bwd_sorted(dy, keys, perm, slot2, P)
+    assert torch.equal(slot, slot2)  # deterministic
+
+
 def _attn_ref(qkv, H):
     B, S, C3 = qkv.shape
     C = C3 // 3
