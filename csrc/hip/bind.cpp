@@ -266,6 +266,16 @@ void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor master, at::Tensor m1, at
                            cur_stream()), "adamw_flat");
 }
 
+void sgd_flat(at::Tensor w, at::Tensor g, at::Tensor buf, at::Tensor decay, double lr, double mom, double wd,
+              double grad_scale) {
+  CHECK_IN(w); CHECK_IN(g); CHECK_IN(buf); CHECK_IN(decay);
+  CHECK_F32(w); CHECK_F32(g); CHECK_F32(buf); CHECK_F32(decay);
+  const long long n = w.numel();
+  TORCH_CHECK(g.numel() == n && buf.numel() == n && n % 1024 == 0 && decay.numel() == n / 1024);
+  CHECK_RC(pdo::sgd_flat(fp(w), fp(g), fp(buf), fp(decay), n, (float)lr, (float)mom, (float)wd, (float)grad_scale,
+                         cur_stream()), "sgd_flat");
+}
+
 // out (+)= sum over the leading dim of part [s, ...] (split-K weight gradients)
 void splitk_add(at::Tensor part, at::Tensor out, bool accumulate) {
   CHECK_IN(part); CHECK_BF16(part); CHECK_BF16(out);
@@ -788,6 +798,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("embed_bwd_sorted", &embed_bwd_sorted);
   m.def("sumsq", &sumsq);
   m.def("adamw_flat", &adamw_flat);
+  m.def("sgd_flat", &sgd_flat);
   m.def("splitk_add", &splitk_add);
   m.def("transpose", &transpose, py::arg("x"), py::arg("out") = py::none());
   m.def("gemm_dw", &gemm_dw, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = true,

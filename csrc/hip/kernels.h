@@ -118,6 +118,8 @@ int embed_bwd(const bf16* dy, const int64_t* idx, float* acc, bf16* dwte, bf16* 
               int P, hipStream_t st);
 int embed_bwd_sorted(const bf16* dy, const int64_t* keys, const int64_t* perm, bf16* dwte, bf16* dwpe, int B, int S,
                      int C, int Vp, int P, int accumulate, hipStream_t st);
+int sgd_flat(float* w, const float* g, float* buf, const float* decay_chunks, long long n, float lr, float mom,
+             float wd, float grad_scale, hipStream_t st);
 int cast_f32_bf16(const float* in, bf16* out, long long n, hipStream_t st);
 
 // optim.hip

@@ -138,6 +138,32 @@ __global__ __launch_bounds__(256) void adamw2_kernel(bf16* __restrict__ p, const
   }
 }
 
+// Momentum SGD over a flat fp32 arena (ResNet-50, workloads/resnet.py): one
+// pass, g' = g·grad_scale + wd·decay·w, buf = mom·buf + g', w −= lr·buf —
+// the four bulk torch ops of the reference formula in one read of (w, g, buf)
+// and one write of (w, buf)
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                  float* __restrict__ buf, const float* __restrict__ decay_chunks,
+                                                  long long n4, float lr, float mom, float wd, float grad_scale) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float dec = decay_chunks[i >> 8];  // 1024 elements per chunk = 256 f32x4
+    const f32x4 gi = reinterpret_cast<const f32x4*>(g)[i] * grad_scale;
+    f32x4 wi = reinterpret_cast<const f32x4*>(w)[i];
+    f32x4 b = reinterpret_cast<const f32x4*>(buf)[i];
+    b = mom * b + (gi + (wd * dec) * wi);
+    wi = wi - lr * b;
+    reinterpret_cast<f32x4*>(buf)[i] = b;
+    reinterpret_cast<f32x4*>(w)[i] = wi;
+  }
+}
+
+int sgd_flat(float* w, const float* g, float* buf, const float* decay_chunks, long long n, float lr, float mom,
+             float wd, float grad_scale, hipStream_t st) {
+  if (n % 1024) return -2;
+  sgd_kernel<<<stream_grid(n / 4, 256), 256, 0, st>>>(w, g, buf, decay_chunks, n / 4, lr, mom, wd, grad_scale);
+  return 0;
+}
+
 int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, float* out, hipStream_t st) {
   if (n % 8) return -2;
   int G = stream_grid(n / 8, 256);

@@ -25,7 +25,8 @@ from ..parallel.flat import FlatParams
 
 
 class FlatSGD:
-    """Momentum SGD over the flat fp32 arena (3 bulk ops per step)."""
+    """Momentum SGD over the flat fp32 arena: one fused HIP pass on the GPU
+    (csrc/hip/optim.hip sgd_flat), the reference's bulk ops on CPU."""
 
     def __init__(self, flat: FlatParams, lr=0.1, momentum=0.9, weight_decay=5e-5):
         self.flat, self.lr, self.mom, self.wd = flat, lr, momentum, weight_decay
@@ -36,6 +37,12 @@ class FlatSGD:
     @torch.no_grad()
     def step(self, grad_scale=1.0):
         g = self.flat.grads
+        if g.is_cuda and g.dtype == torch.float32:
+            from .. import _native
+            _native.require_hip().sgd_flat(self.flat.params, g, self.buf, self.flat.decay_chunks, self.lr, self.mom,
+                                           self.wd, grad_scale)
+            self.step_count += 1
+            return
         if grad_scale != 1.0:
             g.mul_(grad_scale)
         g.addcmul_(self.decay, self.flat.params, value=self.wd)

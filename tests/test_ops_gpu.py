@@ -373,6 +373,25 @@ def test_embedding_sorted_backward_into_arena(cuda):
     assert torch.equal(slot, slot2)  # deterministic
 
 
+def test_sgd_flat_matches_reference(cuda):
+    """The fused momentum-SGD pass (ResNet-50's optimizer) equals the bulk-op formula."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    n = 64 * 1024
+    g_ = torch.Generator(device=cuda).manual_seed(15)
+    w = torch.randn(n, device=cuda, generator=g_)
+    g = torch.randn(n, device=cuda, generator=g_)
+    buf = torch.randn(n, device=cuda, generator=g_)
+    decay = (torch.rand(n // 1024, device=cuda, generator=g_) > 0.5).float()
+    lr, mom, wd, sc = 0.1, 0.9, 5e-5, 0.25
+    dec = decay.repeat_interleave(1024)
+    ref_b = mom * buf + (g * sc + wd * dec * w)
+    ref_w = w - lr * ref_b
+    m.sgd_flat(w, g, buf, decay, lr, mom, wd, sc)
+    torch.testing.assert_close(buf, ref_b, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(w, ref_w, rtol=1e-6, atol=1e-6)
+
+
 def _attn_ref(qkv, H):
     B, S, C3 = qkv.shape
     C = C3 // 3
