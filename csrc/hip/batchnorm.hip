@@ -441,6 +441,22 @@ int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, co
   return 0;
 }
 
+// BatchNorm backward whose statistics (Σg, Σg·(x − mean) partials [G][2][C])
+// came with the input gradient that produced dy (conv.hip): finalize + apply
+int bn_bwd_part(const float* part, int G, const bf16* dy, const bf16* y, const bf16* x, const float* mean,
+                const float* invstd, const float* w, const float* b, long long M, int C, int relu, bf16* dx,
+                bf16* dres, float* dw, float* db, int accumulate, float* coef, hipStream_t st) {
+  if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1) return -2;
+  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, G, M, C, w, invstd, dw, db, accumulate, coef);
+  const long long n8 = M * C / 8;
+  const unsigned g = apply_grid(n8);
+  if (256 % (C / 8) == 0)
+    bn_bwd_apply_kernel<true><<<g, 256, 0, st>>>(dy, y, x, mean, invstd, w, b, coef, n8, C, relu, dx, dres);
+  else
+    bn_bwd_apply_kernel<false><<<g, 256, 0, st>>>(dy, y, x, mean, invstd, w, b, coef, n8, C, relu, dx, dres);
+  return 0;
+}
+
 int bn_bwd_scratch_floats(long long M, int C) {
   int gx, gy;
   long long rpg;

@@ -334,6 +334,18 @@ at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c
   return c;
 }
 
+// c = a·bᵀ + r (r: [M, N] contiguous bf16), one pass
+at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r) {
+  nt_check(a, b);
+  CHECK_IN(r); CHECK_BF16(r);
+  const int M = a.size(0), N = b.size(0), K = a.size(1);
+  TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N, "gemm_nt_add: r must be [M, N]");
+  auto c = at::empty({M, N}, a.options());
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, 4, nullptr, bp(r), N, nullptr, cur_stream()),
+           "gemm_nt_add");
+  return c;
+}
+
 // (pre, y): pre = a·bᵀ, y = gelu(pre + bias)
 std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias) {
   nt_check(a, b);
@@ -415,9 +427,11 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> res, 
   return {y, mean, invstd};
 }
 
-std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor mean,
-                                   at::Tensor invstd, at::Tensor w, at::Tensor b, bool relu, bool want_dres,
-                                   c10::optional<at::Tensor> dw_into, c10::optional<at::Tensor> db_into) {
+// part: (Σg, Σg·(x − mean)) partials [G, 2, C] that came with dy (conv_dgrad_bn); else a stats pass
+static std::vector<at::Tensor> bn_act_bwd_impl(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x,
+                                               at::Tensor mean, at::Tensor invstd, at::Tensor w, at::Tensor b,
+                                               bool relu, bool want_dres, c10::optional<at::Tensor> dw_into,
+                                               c10::optional<at::Tensor> db_into, const at::Tensor* part) {
   CHECK_BF16(dy); CHECK_BF16(x); CHECK_F32(w); CHECK_F32(b);
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "bn_act_bwd: channels_last x");
   auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -444,12 +458,36 @@ std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, a
     dw = at::empty({C}, w.options());
     db = at::empty({C}, w.options());
   }
-  auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_floats(M, C)}, w.options());
-  CHECK_RC(pdo::bn_bwd(bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M, (int)C, relu ? 1 : 0, bp(dx),
-                       want_dres ? bp(dres) : nullptr, fp(dw), fp(db), into ? 1 : 0, fp(scratch), cur_stream()),
-           "bn_bwd");
+  if (part) {
+    CHECK_F32((*part));
+    TORCH_CHECK(part->dim() == 3 && part->size(1) == 2 && part->size(2) == C && part->is_contiguous(),
+                "bn_act_bwd_part: partials [G, 2, C]");
+    auto coef = at::empty({3 * C}, w.options());
+    CHECK_RC(pdo::bn_bwd_part(fp(*part), (int)part->size(0), bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M,
+                              (int)C, relu ? 1 : 0, bp(dx), want_dres ? bp(dres) : nullptr, fp(dw), fp(db),
+                              into ? 1 : 0, fp(coef), cur_stream()),
+             "bn_bwd_part");
+  } else {
+    auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_floats(M, C)}, w.options());
+    CHECK_RC(pdo::bn_bwd(bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M, (int)C, relu ? 1 : 0, bp(dx),
+                         want_dres ? bp(dres) : nullptr, fp(dw), fp(db), into ? 1 : 0, fp(scratch), cur_stream()),
+             "bn_bwd");
+  }
   if (into) return {dx, dres, at::Tensor(), at::Tensor()};
   return {dx, dres, dw, db};
+}
+
+std::vector<at::Tensor> bn_act_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor mean,
+                                   at::Tensor invstd, at::Tensor w, at::Tensor b, bool relu, bool want_dres,
+                                   c10::optional<at::Tensor> dw_into, c10::optional<at::Tensor> db_into) {
+  return bn_act_bwd_impl(dy, y, x, mean, invstd, w, b, relu, want_dres, dw_into, db_into, nullptr);
+}
+
+std::vector<at::Tensor> bn_act_bwd_part(at::Tensor part, at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x,
+                                        at::Tensor mean, at::Tensor invstd, at::Tensor w, at::Tensor b, bool relu,
+                                        bool want_dres, c10::optional<at::Tensor> dw_into,
+                                        c10::optional<at::Tensor> db_into) {
+  return bn_act_bwd_impl(dy, y, x, mean, invstd, w, b, relu, want_dres, dw_into, db_into, &part);
 }
 
 // ---------------------------------------------------------------- NHWC implicit-GEMM convolutions (conv.hip)
@@ -490,17 +528,51 @@ at::Tensor conv_weight_t(at::Tensor w) {
 }
 
 // dx [N, C, H, W] (channels_last) of y = conv(x, w) from dy and wt = conv_weight_t(w)
+// add: a same-shape channels_last bf16 gradient summed in the epilogue (dx = dgrad + add)
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor wt, int64_t C, int64_t R, int64_t S, int64_t H, int64_t W,
-                      int64_t stride, int64_t pad) {
+                      int64_t stride, int64_t pad, c10::optional<at::Tensor> add) {
   CHECK_BF16(dy); CHECK_BF16(wt);
   TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv_dgrad: channels_last bf16 dy");
   const int N = (int)dy.size(0), K = (int)dy.size(1);
   TORCH_CHECK(wt.is_contiguous() && wt.size(0) == C && wt.size(1) == R * S * K, "conv_dgrad: wt [C, R*S*K]");
   auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  const bf16* ap = nullptr;
+  if (add && add->defined()) {
+    CHECK_BF16((*add));
+    TORCH_CHECK(add->sizes() == dx.sizes() && add->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_dgrad: add must match dx (channels_last)");
+    ap = bp(*add);
+  }
   CHECK_RC(pdo::conv_dgrad_nhwc(bp(dy), N, (int)H, (int)W, (int)C, bp(wt), K, (int)R, (int)S, (int)stride, (int)pad,
-                                bp(dx), cur_stream()), "conv_dgrad_nhwc");
+                                bp(dx), cur_stream(), nullptr, ap), "conv_dgrad_nhwc");
   return dx;
+}
+
+// conv_dgrad whose input x was the output of a BatchNorm (input bx, batch mean /
+// invstd, affine w / b, ReLU): also that BatchNorm's backward partials
+// [tiles, 2, C] (Σg, Σg·(bx − mean), g = dx·relu'), for bn_act_bwd_part
+std::vector<at::Tensor> conv_dgrad_bn(at::Tensor dy, at::Tensor wt, int64_t R, int64_t S, int64_t stride,
+                                      int64_t pad, at::Tensor bx, at::Tensor mean, at::Tensor invstd, at::Tensor w,
+                                      at::Tensor b, bool relu) {
+  CHECK_BF16(dy); CHECK_BF16(wt); CHECK_BF16(bx);
+  CHECK_F32(mean); CHECK_F32(invstd); CHECK_F32(w); CHECK_F32(b);
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_bn: channels_last bf16 dy");
+  TORCH_CHECK(bx.dim() == 4 && bx.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_dgrad_bn: channels_last bx");
+  const int N = (int)dy.size(0), K = (int)dy.size(1);
+  const int C = (int)bx.size(1), H = (int)bx.size(2), W = (int)bx.size(3);
+  TORCH_CHECK(bx.size(0) == N, "conv_dgrad_bn: batch");
+  TORCH_CHECK(wt.is_contiguous() && wt.size(0) == C && wt.size(1) == R * S * K, "conv_dgrad_bn: wt [C, R*S*K]");
+  for (const at::Tensor* t : {&mean, &invstd, &w, &b})
+    TORCH_CHECK(t->numel() == C && t->is_contiguous(), "conv_dgrad_bn: per-channel BatchNorm tensors");
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  auto part = at::empty({pdo::conv_dgrad_tiles(N, H, W, C, (int)R, (int)stride, (int)pad), 2, C},
+                        dy.options().dtype(at::kFloat));
+  pdo::ConvBnBwd bn{bp(bx), fp(mean), fp(invstd), fp(w), fp(b), fp(part), relu ? 1 : 0};
+  CHECK_RC(pdo::conv_dgrad_nhwc(bp(dy), N, H, W, C, bp(wt), K, (int)R, (int)S, (int)stride, (int)pad, bp(dx),
+                                cur_stream(), &bn), "conv_dgrad_nhwc(bn)");
+  return {dx, part};
 }
 
 // dw (fp32 [K, C, R, S] channels_last, e.g. the flat arena's slice) (+)= the weight
@@ -826,7 +898,11 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("with_stats") = false);
   m.def("conv_tile_rows", &conv_tile_rows);
   m.def("conv_weight_t", &conv_weight_t);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("C"), py::arg("R"), py::arg("S"),
+        py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("add") = py::none());
+  m.def("gemm_nt_add", &gemm_nt_add);
+  m.def("conv_dgrad_bn", &conv_dgrad_bn);
+  m.def("bn_act_bwd_part", &bn_act_bwd_part);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_act_bwd", &bn_act_bwd);

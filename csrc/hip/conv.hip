@@ -78,6 +78,14 @@ struct ConvArgs {
   int ist, ipad;         // base pixel (a·ist − ipad, b·ist − ipad)
   int OH, OW, ost, oph, opw;  // output pixel (a·ost + oph, b·ost + opw)
   int ident;             // output row = token (forward)
+  // input gradient with the backward statistics of the BatchNorm that produced
+  // x (its input bx, batch mean / invstd, affine w / b, ReLU): per M-tile Σg and
+  // Σg·(bx − mean), g = dy·[bx·sc + sh > 0], into bpart[tile_off + tile][2][Kout]
+  const bf16* bx;
+  const bf16* add;  // y = conv + add (same layout as y): a branch gradient joining this one
+  const float *bmean, *binv, *bw, *bb;
+  float* bpart;
+  int brelu, tile_off;
   unsigned xbytes;
   int ntaps;
   int dh[9], dw[9], bcol[9];
@@ -226,6 +234,15 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
   const int g4 = lane >> 4;
   const int col = n0 + wn * 64 + 4 * (lane & 15);
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 bsc, bsh, bmu;
+  const bool bnb = a.bx != nullptr;
+  if (bnb) {
+    bmu = *reinterpret_cast<const f32x4*>(a.bmean + col);
+    const f32x4 inv = *reinterpret_cast<const f32x4*>(a.binv + col);
+    bsc = *reinterpret_cast<const f32x4*>(a.bw + col) * inv;
+    bsh = *reinterpret_cast<const f32x4*>(a.bb + col) - bmu * bsc;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -242,13 +259,28 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
         divmod(q, a.TA, a.inv_TA, n, aa);
         row = ((long long)n * a.OH + aa * a.ost + a.oph) * a.OW + bb * a.ost + a.opw;
       }
-      const bf16x4 v = {(bf16)acc[i][0][e], (bf16)acc[i][1][e], (bf16)acc[i][2][e], (bf16)acc[i][3][e]};
+      f32x4 o = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
+      if (a.add) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.add + row * a.Kout + col);
+        o += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+      }
+      const bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
       *reinterpret_cast<bf16x4*>(a.y + row * a.Kout + col) = v;
 #pragma unroll
       for (int j = 0; j < 4; ++j) cs[j] += (float)v[j];
+      if (bnb) {
+        const bf16x4 xb = *reinterpret_cast<const bf16x4*>(a.bx + row * a.Kout + col);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xv = (float)xb[j];
+          // the forward's pre-activation through the same fp32 ops (bit-identical mask)
+          const float g = (!a.brelu || xv * bsc[j] + bsh[j] > 0.f) ? (float)v[j] : 0.f;
+          s1[j] += g;
+          s2[j] += g * (xv - bmu[j]);
+        }
+      }
     }
-  if (!a.stats) return;
-  // ---- BatchNorm partials of this M-tile: Σv and Σ(v − mean_tile)² per channel
+  if (!a.stats && !bnb) return;
   const int rows = (int)(a.M - m0 < BM ? a.M - m0 : BM);
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN] (the last k-step's barrier freed the stages)
   auto tile_sum = [&](float (&v)[4]) {
@@ -271,6 +303,18 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
     }
     __syncthreads();
   };
+  if (bnb) {
+    // ---- BatchNorm backward partials of this M-tile: Σg, Σg·(x − mean) per channel
+    tile_sum(s1);
+    tile_sum(s2);
+    if (wm == 0 && lane < 16) {
+      float* p = a.bpart + (size_t)(a.tile_off + tm) * 2 * a.Kout + col;
+      *reinterpret_cast<f32x4*>(p) = f32x4{s1[0], s1[1], s1[2], s1[3]};
+      *reinterpret_cast<f32x4*>(p + a.Kout) = f32x4{s2[0], s2[1], s2[2], s2[3]};
+    }
+    return;
+  }
+  // ---- BatchNorm forward partials of this M-tile: Σv and Σ(v − mean_tile)² per channel
   tile_sum(cs);
   float mean[4], cq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -549,10 +593,28 @@ int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t s
   return 0;
 }
 
+// tiles the input gradient writes BatchNorm-backward partials for (conv_dgrad_nhwc with bn)
+int conv_dgrad_tiles(int N, int H, int W, int C, int R, int stride, int pad) {
+  const int bm = C == 64 ? 256 : 128;
+  if (stride == 1) return (int)(((long long)N * H * W + bm - 1) / bm);
+  long long t = 0;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      int n = 0;
+      for (int r = 0; r < R; ++r)
+        for (int s = 0; s < R; ++s)
+          if (((ph + pad - r) & 1) == 0 && ((pw + pad - s) & 1) == 0) ++n;
+      const long long ta = (H - ph + 1) / 2, tb = (W - pw + 1) / 2;
+      if (n && ta > 0 && tb > 0) t += ((long long)N * ta * tb + bm - 1) / bm;
+    }
+  return (int)t;
+}
+
 // dx [N][H][W][C] from dy [N][Ho][Wo][Kout] and wt = Wᵀ [C][R·S][Kout]; every
-// element of dx is written (parity classes without taps get zeros by a memset)
+// element of dx is written (parity classes without taps get zeros by a memset,
+// which also contribute nothing to the BatchNorm partials)
 int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
-                    int pad, bf16* dx, hipStream_t st) {
+                    int pad, bf16* dx, hipStream_t st, const ConvBnBwd* bn, const bf16* add) {
   if (!conv_supported(N, H, W, C, Kout, R, S, stride, pad)) return -2;
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   if ((long long)N * Ho * Wo * Kout * 2 >= (1ll << 31)) return -2;
@@ -570,6 +632,16 @@ int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, 
   a.OH = H;
   a.OW = W;
   a.xbytes = (unsigned)((long long)N * Ho * Wo * Kout * 2);
+  a.add = add;
+  if (bn) {
+    a.bx = bn->x;
+    a.bmean = bn->mean;
+    a.binv = bn->invstd;
+    a.bw = bn->w;
+    a.bb = bn->b;
+    a.bpart = bn->part;
+    a.brelu = bn->relu;
+  }
   if (!shape_ok(Kout, C, R, S, 1, pad)) return -2;  // the roles of C and Kout swap here
   if (stride == 1) {
     a.M = (long long)N * H * W;
@@ -597,7 +669,12 @@ int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, 
           if (((ph + pad - r) & 1) == 0 && ((pw + pad - s) & 1) == 0) ++n;
       if (n == 0) zero_needed = true;
     }
-  if (zero_needed && hipMemsetAsync(dx, 0, (size_t)N * H * W * C * 2, st) != hipSuccess) return -5;
+  // rows no class writes: zeros (or the addend itself)
+  if (zero_needed) {
+    const hipError_t e = add ? hipMemcpyAsync(dx, add, (size_t)N * H * W * C * 2, hipMemcpyDeviceToDevice, st)
+                             : hipMemsetAsync(dx, 0, (size_t)N * H * W * C * 2, st);
+    if (e != hipSuccess) return -5;
+  }
   for (int ph = 0; ph < 2; ++ph)
     for (int pw = 0; pw < 2; ++pw) {
       ConvArgs c = a;
@@ -619,14 +696,16 @@ int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, 
           ++c.ntaps;
         }
       if (c.ntaps == 0) continue;
-      const int rc = run_igemm(c, st, nullptr);
+      int rows = 0;
+      const int rc = run_igemm(c, st, &rows);
       if (rc) return rc;
+      a.tile_off += (int)((c.M + rows - 1) / rows);  // the next class's BatchNorm partial rows
     }
   return 0;
 }
 
 // split count of conv_wgrad: ≈ 2 workgroups per CU over the output tiles, ≥ 8
-// 64-token k-steps per slice
+// 64-token k-steps per slice, ≤ 256 slices (the fold reads splits × outputs fp32)
 static void wgrad_cfg(int Kout, int C, int T, long long M, int* bmw, int* bnw, int* splits) {
   *bmw = Kout % 128 == 0 ? 128 : 64;
   *bnw = C % 128 == 0 ? 128 : 64;
@@ -634,7 +713,7 @@ static void wgrad_cfg(int Kout, int C, int T, long long M, int* bmw, int* bnw, i
   const long long ks = (M + 63) / 64;
   long long sp = (512 + tiles - 1) / tiles;
   if (sp > ks / 8) sp = ks / 8;
-  if (sp > 64) sp = 64;
+  if (sp > 256) sp = 256;  // one or two output tiles (64-channel 1×1 at 56×56): still ≥ 256 workgroups
   if (sp < 1) sp = 1;
   *splits = (int)sp;
 }

@@ -25,6 +25,8 @@
 //              through Y), and fp32 column partial sums of C for the bias
 //              gradient (one row per (M-tile, wave)) — the fc2 input-gradient
 //              GEMM with the bias-GELU backward pass fused
+//   EPI_ADD    C = A·Bᵀ + Y — an input gradient that joins another branch's
+//              (ResNet's block input: conv1 dX + the identity / downsample dX)
 // Rounding matches the unfused path bit for bit: the GEMM result is rounded to
 // bf16 before the activation math, as when it made an HBM round trip.
 #include <stdlib.h>
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
   const int c = tid & 31, r0 = tid >> 5;
   const int n = n0 + 8 * c;
   f32x8 bv8;
-  if constexpr (EPI >= 2) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
+  if constexpr (EPI == 2 || EPI == 3) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
   f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
   for (int it = 0; it < 16; ++it) {
@@ -203,6 +205,10 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
       *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
+    } else if constexpr (EPI == 4) {
+      // the addend joins after the bf16 staging: two roundings (the 4-wave path has one)
+      const f32x8 r = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n));
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(to_f32(v) + r);
     } else {
       const f32x8 x = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n)) + bv8;
       const f32x8 dy = to_f32(v);
@@ -252,8 +258,8 @@ int gemm_nt_get_impl() { return g_impl; }
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
   if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
-  if (epi != 0 && !bias) return -3;
-  if ((epi == 2 || epi == 3) && (!Y || ldy % 4 || ldy < N)) return -3;
+  if (epi >= 1 && epi <= 3 && !bias) return -3;
+  if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
   if (nt4_path(K))
     return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, g_impl == 2 ? 1 : 0);
@@ -265,6 +271,7 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
     case 1: gemm_nt_kernel<1><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 2: gemm_nt_kernel<2><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 3: gemm_nt_kernel<3><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 4: gemm_nt_kernel<4><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     default: return -4;
   }
   return 0;

@@ -47,8 +47,20 @@ int conv_fwd_tile_rows(int Kout);
 int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int Kout, int R, int S, int stride, int pad,
                   bf16* y, float* tile_stats, hipStream_t st);
 int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t st);
+// BatchNorm whose output the convolution consumed: its backward statistics ride
+// on the input gradient's epilogue (part: [conv_dgrad_tiles][2][C])
+struct ConvBnBwd {
+  const bf16* x;
+  const float *mean, *invstd, *w, *b;
+  float* part;
+  int relu;
+};
+int conv_dgrad_tiles(int N, int H, int W, int C, int R, int stride, int pad);
 int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
-                    int pad, bf16* dx, hipStream_t st);
+                    int pad, bf16* dx, hipStream_t st, const ConvBnBwd* bn = nullptr, const bf16* add = nullptr);
+int bn_bwd_part(const float* part, int G, const bf16* dy, const bf16* y, const bf16* x, const float* mean,
+                const float* invstd, const float* w, const float* b, long long M, int C, int relu, bf16* dx,
+                bf16* dres, float* dw, float* db, int accumulate, float* coef, hipStream_t st);
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad);
 int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st);

@@ -2,10 +2,13 @@
 elastic ResNet-50) — written out here because torchvision is not part of the
 image.  Standard v1.5 bottleneck architecture (stride on the 3×3 conv).
 
-MI355X choices: channels_last bf16 activations; the 3×3 and strided 1×1
-convolutions on the hand-written NHWC implicit GEMM (csrc/hip/conv.hip, BatchNorm
-statistics from its epilogue), the 1×1 stride-1 ones as token-major GEMMs
-(gemm_nt4 / gemm_dw4), only the 7×7 stem (3 input channels) on MIOpen;
+MI355X choices: channels_last bf16 activations; every convolution but the 7×7
+stem (3 input channels, MIOpen) on hand-written kernels — the NHWC implicit GEMM
+(csrc/hip/conv.hip: BatchNorm forward statistics from its epilogue, the previous
+BatchNorm's backward statistics from its input-gradient epilogue) or, per
+product where measured faster, the token-major GEMMs (gemm_nt4 / gemm_dw4) for
+the wide 1×1 stride-1 products; the residual branch's gradient summed inside
+conv1's input-gradient epilogue;
 BatchNorm (fp32 statistics and affine params) fused with ReLU and the residual
 add into HIP kernels (ops.bn_act); parameters live in a flat fp32 arena
 (parallel.flat) so the gradient all-reduce buckets are slices.
@@ -34,17 +37,18 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        # BN + ReLU (+ residual add) fused into one HIP pass each (ops.bn_act)
-        # 1×1 stride-1 convolutions as token-major GEMMs (ops.conv1x1: gemm_nt4 /
-        # gemm_dw4 / MIOpen per product, whichever measured faster at the shape)
-        # 3×3 and strided 1×1 convolutions on the NHWC implicit GEMM with the
-        # BatchNorm statistics in its epilogue (ops.conv_bn_act, csrc/hip/conv.hip)
-        idt = x
-        out = ops.bn_act(self.bn1, ops.conv1x1(self.conv1, x))
+        # every convolution + BatchNorm (+ ReLU, + residual add) through
+        # ops.conv_bn_act: hand-written kernels per product (NHWC implicit GEMM
+        # with the BatchNorm statistics in its epilogue, or the token-major GEMMs
+        # for the wide 1×1 products), BN apply fused with ReLU / residual.
+        # conv1 forks x for the identity / downsample branch: that branch's
+        # gradient joins conv1's dX in the dX kernel's epilogue.
+        out, xa = ops.conv_bn_act(self.conv1, self.bn1, x, fork=True)
         out = ops.conv_bn_act(self.conv2, self.bn2, out)
+        idt = xa
         if self.downsample is not None:
-            idt = ops.conv_bn_act(self.downsample[0], self.downsample[1], x, relu=False)
-        return ops.bn_act(self.bn3, ops.conv1x1(self.conv3, out), relu=True, residual=idt)
+            idt = ops.conv_bn_act(self.downsample[0], self.downsample[1], xa, relu=False)
+        return ops.conv_bn_act(self.conv3, self.bn3, out, relu=True, residual=idt)
 
 
 class ResNet(nn.Module):

@@ -848,10 +848,14 @@ class _BNActFn(torch.autograd.Function):
     Without a residual the backward recomputes the ReLU mask from x, so only
     x (the conv output autograd keeps anyway) and two [C] vectors are saved.
     ``stats``: the producing convolution's per-tile partials (conv.hip), so the
-    forward skips its statistics pass over x."""
+    forward skips its statistics pass over x.  ``link``: a _BNLink through which
+    the consuming implicit-GEMM convolution hands back the backward statistics
+    it took in its input-gradient epilogue, so the backward skips its
+    statistics pass over dy and x too."""
 
     @staticmethod
-    def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu, stats=None, tile_rows=0):
+    def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu, stats=None, tile_rows=0,
+                link=None):
         m = _native.require_hip()
         if stats is not None:
             y, mean, invstd = m.bn_act_fwd_tiles(x, stats, tile_rows, residual, w, b, running_mean, running_var, eps,
@@ -863,6 +867,9 @@ class _BNActFn(torch.autograd.Function):
         keep_y = relu and ctx.has_res
         ctx.save_for_backward(x, y if keep_y else None, mean, invstd, w, b)
         ctx.params = (w, b)
+        ctx.link = link
+        if link is not None:
+            link.bn = (x, mean, invstd, w, b, relu)
         return y
 
     @staticmethod
@@ -872,16 +879,55 @@ class _BNActFn(torch.autograd.Function):
         pw, pb = ctx.params
         # gamma/beta gradients straight into the flat arena when allowed
         direct = _direct_ok(pw) and _direct_ok(pb) and pw.grad.dtype == torch.float32
-        dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, ctx.relu, ctx.has_res,
-                                        pw.grad if direct else None, pb.grad if direct else None)
+        dwi, dbi = (pw.grad, pb.grad) if direct else (None, None)
+        part = ctx.link.take(dy) if ctx.link is not None else None
+        if part is not None:
+            dx, dres, dw, db = m.bn_act_bwd_part(part, dy, y, x, mean, invstd, w, b, ctx.relu, ctx.has_res, dwi, dbi)
+        else:
+            dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, ctx.relu, ctx.has_res, dwi, dbi)
+        ctx.link = None
         if direct:
             pw._pdo_ready(pw)
             pb._pdo_ready(pb)
             dw = db = None
-        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None
+        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None
+
+
+class _BNLink:
+    """Hand-off between a BatchNorm(+ReLU) output and the implicit-GEMM
+    convolution that consumes it (ResNet's bn1 → conv2).  Forward: the
+    BatchNorm leaves (x, mean, invstd, w, b, relu) here; backward: the
+    convolution's input gradient computes, in its epilogue, that BatchNorm's
+    Σg and Σg·(x − mean) per tile (conv_dgrad_bn) and parks them with the
+    gradient tensor they belong to.  The BatchNorm uses them only when the dy
+    it receives IS that tensor, unmodified (same storage and version — another
+    consumer's gradient added to it would show as a new tensor or a version
+    bump; the reference held here stops autograd from accumulating in place)."""
+
+    __slots__ = ("bn", "dx", "ver", "part")
+
+    def __init__(self):
+        self.bn = self.dx = self.part = None
+        self.ver = -1
+
+    def give(self, dx, part):
+        self.dx, self.ver, self.part = dx, dx._version, part
+
+    def take(self, dy):
+        dx, part, ver = self.dx, self.part, self.ver
+        self.bn = self.dx = self.part = None
+        if (part is None or dy.data_ptr() != dx.data_ptr() or dy._version != ver or dy.shape != dx.shape
+                or not dy.is_contiguous(memory_format=torch.channels_last)):
+            return None
+        _BN_LINK_USED[0] += 1
+        return part
+
+
+_BN_LINK_USED = [0]  # backward passes that took their statistics from a convolution epilogue (tests)
 
 
 _BN_FUSED = [os.environ.get("PDO_BN_FUSED", "1") != "0"]
+_BN_LINK = [os.environ.get("PDO_BN_LINK", "1") != "0"]
 
 
 def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
@@ -896,127 +942,120 @@ def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
                                        and residual.is_contiguous(memory_format=torch.channels_last))))
     if fused:
         mom = bn.momentum if bn.momentum is not None else 0.1
-        return _BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu)
+        link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
+        y = _BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu,
+                           None, 0, link)
+        if link is not None:
+            y._pdo_bn = link  # read by _ConvFn when y feeds an implicit-GEMM convolution
+        return y
     y = bn(x)
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
 
 
-class _Conv1x1Fn(torch.autograd.Function):
-    """1×1 stride-1 convolution on a channels_last bf16 activation as token-major
-    GEMMs over its [N·H·W, C] view — per product, the kernel that measured
-    faster at ResNet-50's shapes (tools/conv1x1_probe.py, profiles/r3_resnet_conv1x1.md):
-
-    * forward y = x·Wᵀ and input gradient dX = dY·W on gemm_nt4 where its
-      contract holds (output width % 128, reduction ≥ 256), else MIOpen;
-    * weight gradient dW = dYᵀ·X on gemm_dw4 where it has ≥ 8 output tiles,
-      else hipBLASLt over 64 token slices + an fp32 fold (no MIOpen zero-fill /
-      cast passes), else (64 × 64) MIOpen."""
-
-    @staticmethod
-    def forward(ctx, x, w):
-        m = _native.require_hip()
-        N, C, H, W_ = x.shape
-        Co = w.shape[0]
-        wb = w.detach().to(torch.bfloat16).view(Co, C) if w.dtype != torch.bfloat16 else w.view(Co, C)
-        T = N * H * W_
-        x2 = x.permute(0, 2, 3, 1).reshape(T, C)
-        if m.gemm_nt_supported(T, Co, C):
-            y = m.gemm_nt(x2, wb).view(N, H, W_, Co).permute(0, 3, 1, 2)
-        else:
-            y = F.conv2d(x, wb.view(Co, C, 1, 1))
-        ctx.save_for_backward(x, wb)
-        ctx.wdtype = w.dtype
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        m = _native.require_hip()
-        x, wb = ctx.saved_tensors
-        N, C, H, W_ = x.shape
-        Co = wb.shape[0]
-        T = N * H * W_
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        dy2 = dy.permute(0, 2, 3, 1).reshape(T, Co)
-        x2 = x.permute(0, 2, 3, 1).reshape(T, C)
-        cb = torch.ops.aten.convolution_backward
-        w4 = wb.view(Co, C, 1, 1)
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            if m.gemm_nt_supported(T, C, Co):
-                dx = m.gemm_nt(dy2, transpose(wb)).view(N, H, W_, C).permute(0, 3, 1, 2)
-            else:
-                dx = cb(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])[0]
-        if ctx.needs_input_grad[1]:
-            tiles = ((Co + 255) // 256) * (C // 256)
-            g = torch.empty(Co, C, device=x.device, dtype=torch.bfloat16)
-            if tiles >= 8 and m.gemm_dw(dy2, x2, g, False):
-                pass
-            elif Co * C >= 64 * 256 and T % 64 == 0:
-                s = 64
-                part = torch.bmm(dy2.view(s, T // s, Co).transpose(1, 2), x2.view(s, T // s, C))
-                g = part.sum(0, dtype=torch.float32)
-            else:
-                g = cb(dy, x, w4, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])[1]
-            dw = g.view(Co, C, 1, 1).to(ctx.wdtype)
-        return dx, dw
+def _gemm_fwd_1x1(m, T, C, K) -> bool:
+    """1×1 stride-1 forward on the token-major GEMM (gemm_nt) rather than the
+    implicit GEMM: measured faster for every ResNet-50 shape with K > 128 output
+    channels; at K ≤ 128 the implicit GEMM is as fast or faster and its epilogue
+    also yields the BatchNorm statistics (profiles/r4d_conv_probe.jsonl)."""
+    return K > 128 and bool(m.gemm_nt_supported(T, K, C))
 
 
-_CONV1X1 = [os.environ.get("PDO_CONV1X1", "1") != "0"]
+def _gemm_dgrad_1x1(m, T, C, K) -> bool:
+    """1×1 stride-1 input gradient on gemm_nt: faster at C > 128 input channels
+    (profiles/r4d_conv_probe.jsonl)."""
+    return C > 128 and bool(m.gemm_nt_supported(T, C, K))
 
 
-def conv1x1(conv: torch.nn.Conv2d, x):
-    """``conv(x)`` for a 1×1, stride-1, bias-free convolution; the GEMM path
-    (_Conv1x1Fn) for channels_last bf16 activations on the HIP path."""
-    if (_CONV1X1[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 4
-            and x.is_contiguous(memory_format=torch.channels_last) and conv.kernel_size == (1, 1)
-            and conv.stride == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None
-            and x.shape[1] % 64 == 0 and conv.out_channels % 64 == 0
-            and (x.shape[0] * x.shape[2] * x.shape[3]) % 256 == 0):
-        return _Conv1x1Fn.apply(x, conv.weight)
-    return conv(x)
+def _gemm_wgrad_1x1(C, K) -> bool:
+    """1×1 stride-1 weight gradient on gemm_dw4 where it has ≥ 8 output tiles
+    (1024/2048-channel shapes); conv_wgrad elsewhere."""
+    return ((K + 255) // 256) * (C // 256) >= 8
 
 
 class _ConvFn(torch.autograd.Function):
-    """y = conv2d(x, w) for a channels_last bf16 activation on the hand-written
-    NHWC implicit GEMM (csrc/hip/conv.hip): 3×3 stride 1 / 2 and strided 1×1,
-    forward (+ BatchNorm tile statistics, a second non-differentiable output),
-    input gradient (Wᵀ built per backward, stride-2 parity classes) and weight
-    gradient (split-K, fp32 — straight into the flat fp32 arena when the
-    parameter allows it).  Replaces MIOpen's igemm fwd / bwd / wrw solvers and
-    their zero-fill / cast passes on ResNet-50 (profiles/r3t_resnet50_kernels.md)."""
+    """y = conv2d(x, w) for a channels_last bf16 activation on hand-written
+    kernels: the NHWC implicit GEMM (csrc/hip/conv.hip) for 3×3 stride 1 / 2 and
+    1×1 stride 1 / 2 — forward (+ BatchNorm tile statistics, a second
+    non-differentiable output), input gradient (Wᵀ built per backward, stride-2
+    parity classes), weight gradient (split-K, fp32, straight into the flat fp32
+    arena when the parameter allows it) — and, per product where measured
+    faster, the token-major GEMMs for 1×1 stride 1 (gemm_nt / gemm_dw4).
+
+    ``fork``: also return x itself (an autograd alias) for a second consumer —
+    ResNet's identity / downsample branch — so that branch's gradient reaches
+    this backward and joins dX in the dX kernel's epilogue (no separate add of
+    two activation-sized gradients).  Replaces MIOpen's igemm fwd / bwd / wrw
+    solvers, their zero-fill / cast passes and the hipBLASLt small-shape weight
+    gradients on ResNet-50 (profiles/r3t_resnet50_kernels.md)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pad, want_stats):
+    def forward(ctx, x, w, stride, pad, want_stats, fork=False):
         m = _native.require_hip()
         wb = w.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        y, st = m.conv_fwd(x, wb, stride, pad, want_stats)
+        K, C, R, _ = wb.shape
+        N, _, H, W_ = x.shape
+        ctx.one = R == 1 and stride == 1
+        st = None
+        if ctx.one and _gemm_fwd_1x1(m, N * H * W_, C, K):
+            y = m.gemm_nt(x.permute(0, 2, 3, 1).reshape(-1, C), wb.view(K, C)).view(N, H, W_, K).permute(0, 3, 1, 2)
+        else:
+            y, st = m.conv_fwd(x, wb, stride, pad, want_stats)
         ctx.save_for_backward(x, wb)
         ctx.stride, ctx.pad = stride, pad
         ctx.wparam = w
+        link = getattr(x, "_pdo_bn", None)
+        ctx.link = link if link is not None and link.bn is not None else None
+        ctx.set_materialize_grads(False)
         if st is not None:
             ctx.mark_non_differentiable(st)
-        return y, st
+        return y, st, (x if fork else None)
 
     @staticmethod
-    def backward(ctx, dy, _dstats):
+    def backward(ctx, dy, _dstats, dalias):
         m = _native.require_hip()
         x, wb = ctx.saved_tensors
         K, C, R, S = wb.shape
+        N, _, H, W_ = x.shape
+        T = N * H * W_
+        link, ctx.link = ctx.link, None
+        if dy is None:  # y unused: only the alias carried a gradient
+            return dalias, None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
+        if dalias is not None:
+            dalias = dalias.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = m.conv_dgrad(dy, m.conv_weight_t(wb), C, R, S, x.shape[2], x.shape[3], ctx.stride, ctx.pad)
+            if link is None and ctx.one and _gemm_dgrad_1x1(m, T, C, K):
+                dy2 = dy.permute(0, 2, 3, 1).reshape(T, K)
+                wt2 = transpose(wb.view(K, C))
+                dx = (m.gemm_nt_add(dy2, wt2, dalias.permute(0, 2, 3, 1).reshape(T, C)) if dalias is not None
+                      else m.gemm_nt(dy2, wt2))
+                dx = dx.view(N, H, W_, C).permute(0, 3, 1, 2)
+            elif link is not None and link.bn is not None:
+                # the producing BatchNorm's backward statistics from this epilogue
+                bx, mean, invstd, bw, bb, relu = link.bn
+                dx, part = m.conv_dgrad_bn(dy, m.conv_weight_t(wb), R, S, ctx.stride, ctx.pad, bx, mean, invstd,
+                                           bw, bb, relu)
+                link.give(dx, part)
+                if dalias is not None:  # (not a ResNet pattern: a BatchNorm output is not forked)
+                    dx = dx + dalias
+            else:
+                dx = m.conv_dgrad(dy, m.conv_weight_t(wb), C, R, S, H, W_, ctx.stride, ctx.pad, dalias)
         if ctx.needs_input_grad[1]:
             p = ctx.wparam
-            if (_direct_ok(p) and p.grad.dtype == torch.float32
+            if ctx.one and _gemm_wgrad_1x1(C, K):
+                g = torch.empty(K, C, device=x.device, dtype=torch.bfloat16)
+                m.gemm_dw(dy.permute(0, 2, 3, 1).reshape(T, K), x.permute(0, 2, 3, 1).reshape(T, C), g, False)
+                dw = g.view(K, C, 1, 1).to(p.dtype)
+            elif (_direct_ok(p) and p.grad.dtype == torch.float32
                     and p.grad.is_contiguous(memory_format=torch.channels_last)):
                 m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad, out=p.grad)
                 p._pdo_ready(p)
             else:
                 dw = m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad).to(p.dtype)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 _HIP_CONV = [os.environ.get("PDO_HIP_CONV", "1") != "0"]
@@ -1029,31 +1068,47 @@ def _hip_conv_ok(conv: torch.nn.Conv2d, x) -> bool:
             and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]):
         return False
     R, st, pad = conv.kernel_size[0], conv.stride[0], conv.padding[0]
-    if R == 1 and st == 1:
-        return False  # 1×1 stride 1: the token-major GEMM path (conv1x1)
     N, C, H, W = x.shape
     return bool(_native.require_hip().conv_ok(N, H, W, C, conv.out_channels, R, R, st, pad))
 
 
-def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
-    """act(BN(conv(x)) [+ residual]) — on the HIP implicit-GEMM convolution with
-    the BatchNorm statistics taken in its epilogue where the shapes allow;
-    otherwise the 1×1 GEMM path / the framework convolution + ops.bn_act."""
-    if _hip_conv_ok(conv, x) and bn.training and _BN_FUSED[0] and bn.weight is not None and \
-            bn.weight.dtype == torch.float32 and (residual is None or (
-                residual.dtype == torch.bfloat16 and residual.is_contiguous(memory_format=torch.channels_last))):
-        y, st = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True)
-        mom = bn.momentum if bn.momentum is not None else 0.1
-        rows = _native.require_hip().conv_tile_rows(conv.out_channels)
-        return _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu,
-                              st, rows)
-    if conv.kernel_size == (1, 1) and conv.stride == (1, 1):
-        y = conv1x1(conv, x)
-    elif _hip_conv_ok(conv, x):
-        y = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], False)[0]
-    else:
-        y = conv(x)
-    return bn_act(bn, y, relu=relu, residual=residual)
+def conv1x1(conv: torch.nn.Conv2d, x):
+    """``conv(x)`` for a 1×1 bias-free convolution: the hand-written kernels
+    (_ConvFn: implicit GEMM or token-major GEMM per product) for channels_last
+    bf16 activations on the HIP path, else the framework convolution."""
+    if _hip_conv_ok(conv, x):
+        return _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], False)[0]
+    return conv(x)
+
+
+def _bn_fused_ok(bn: torch.nn.BatchNorm2d, residual) -> bool:
+    return (bn.training and _BN_FUSED[0] and bn.weight is not None and bn.weight.dtype == torch.float32
+            and (residual is None or (residual.dtype == torch.bfloat16
+                                      and residual.is_contiguous(memory_format=torch.channels_last))))
+
+
+def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None,
+                fork: bool = False):
+    """act(BN(conv(x)) [+ residual]) — on the hand-written convolutions with the
+    BatchNorm statistics taken in the implicit GEMM's epilogue where that kernel
+    runs the forward; otherwise the framework convolution + ops.bn_act.
+    ``fork``: returns (out, x_alias) — x for a second consumer whose gradient
+    then joins this convolution's dX in its epilogue (_ConvFn)."""
+    if _hip_conv_ok(conv, x) and _bn_fused_ok(bn, residual):
+        y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork)
+        if st is None:
+            out = bn_act(bn, y, relu=relu, residual=residual)
+        else:
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            rows = _native.require_hip().conv_tile_rows(conv.out_channels)
+            link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
+            out = _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom,
+                                 relu, st, rows, link)
+            if link is not None:
+                out._pdo_bn = link
+        return (out, xa) if fork else out
+    out = bn_act(bn, conv(x), relu=relu, residual=residual)
+    return (out, x) if fork else out
 
 
 class _MaxPool3s2Fn(torch.autograd.Function):

@@ -68,6 +68,22 @@ def test_conv_dgrad(hip, N, C, H, K, R, stride):
     dx = hip.conv_dgrad(dy, wt, C, R, R, H, H, stride, pad)
     assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
     assert _rel(dx, xf.grad) < 1e-2
+    # a joining branch gradient summed in the epilogue (1×1 stride 2: the untouched
+    # parity classes take the addend as is)
+    add = torch.randn(x.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    dxa = hip.conv_dgrad(dy, wt, C, R, R, H, H, stride, pad, add)
+    assert _rel(dxa, xf.grad + add.float()) < 1e-2
+
+
+@pytest.mark.parametrize("T,N,K", [(1024, 256, 512), (2048, 512, 128), (512, 256, 64)])
+def test_gemm_nt_add(hip, T, N, K):
+    """c = a·bᵀ + r on both mainloops (K ≥ 256: the 4-wave kernel; K = 64 / 128: the 8-wave one)."""
+    g = torch.Generator(device="cuda").manual_seed(T + K)
+    a = torch.randn(T, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    r = torch.randn(T, N, device="cuda", generator=g).bfloat16()
+    c = hip.gemm_nt_add(a, b, r)
+    assert _rel(c, a.float() @ b.float().t() + r.float()) < 1e-2
 
 
 def test_bn_from_tile_stats_matches_stats_pass(hip):
@@ -142,3 +158,62 @@ def test_bottleneck_hip_conv_path_matches_framework_conv():
     assert _rel(outs[0][1], outs[1][1]) < 3e-2
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert _rel(pa.grad, pb.grad) < 3e-2, n
+
+
+@pytest.mark.parametrize("N,C,H,K,stride", [(2, 64, 16, 64, 1), (3, 128, 7, 128, 2), (2, 128, 16, 128, 2)])
+def test_conv_dgrad_bn_partials(hip, N, C, H, K, stride):
+    """The input gradient's epilogue BatchNorm partials, folded by
+    bn_act_bwd_part, give the same dx / dgamma / dbeta as the stats-pass
+    BatchNorm backward on the same (dy, x)."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    bx = torch.randn(N, C, H, H, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    gamma = torch.rand(C, device="cuda", generator=g) + 0.5
+    beta = torch.randn(C, device="cuda", generator=g) * 0.2
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    y, mean, invstd = hip.bn_act_fwd(bx, None, gamma, beta, rm, rv, 1e-5, 0.1, True)
+    w = (torch.randn(K, C, 3, 3, device="cuda", generator=g) / (9 * C) ** 0.5).bfloat16()
+    w = w.contiguous(memory_format=torch.channels_last)
+    Ho = (H + 2 - 3) // stride + 1
+    dy = torch.randn(N, K, Ho, Ho, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    wt = hip.conv_weight_t(w)
+    dx_plain = hip.conv_dgrad(dy, wt, C, 3, 3, H, H, stride, 1)
+    dx, part = hip.conv_dgrad_bn(dy, wt, 3, 3, stride, 1, bx, mean, invstd, gamma, beta, True)
+    assert torch.equal(dx, dx_plain)
+    a = hip.bn_act_bwd(dx, None, bx, mean, invstd, gamma, beta, True, False, None, None)
+    b = hip.bn_act_bwd_part(part, dx, None, bx, mean, invstd, gamma, beta, True, False, None, None)
+    for u, v in ((a[0], b[0]), (a[2], b[2]), (a[3], b[3])):
+        assert _rel(v, u) < 2e-3
+
+
+def test_bottleneck_bn_link_matches_unlinked():
+    """ResNet bottleneck with bn1's backward statistics from conv2's input-gradient
+    epilogue (ops._BNLink) vs the stats-pass backward: same gradients, and the
+    link was actually taken."""
+    import copy
+
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(1)
+    a = Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last)
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 256, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for mod, link in ((a, True), (b, False)):
+        prev, used = ops._BN_LINK[0], ops._BN_LINK_USED[0]
+        ops._BN_LINK[0] = link
+        try:
+            xx = x.clone().requires_grad_()
+            y = mod(xx)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        finally:
+            ops._BN_LINK[0] = prev
+        # bn1 → conv2 and bn2 → conv3 (both implicit-GEMM input gradients)
+        assert (ops._BN_LINK_USED[0] - used) == (2 if link else 0)
+        outs.append(xx.grad)
+    assert _rel(outs[0], outs[1]) < 1e-2
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert _rel(pa.grad, pb.grad) < 1e-2, n

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """ResNet-50 convolutions at batch 256: the hand-written NHWC implicit GEMM
 (csrc/hip/conv.hip) against MIOpen (F.conv2d / aten.convolution_backward,
-bf16 channels_last), forward and input gradient; interleaved rounds in one
-process, median µs per call and TFLOP/s.
+bf16 channels_last) — forward, input gradient, weight gradient — and, for the
+1×1 stride-1 shapes, against the token-major GEMMs ops.conv1x1 uses (gemm_nt /
+gemm_dw); interleaved rounds in one process, median µs per call and TFLOP/s.
 
     python tools/conv_probe.py [--batch 256] [--iters 20] [--rounds 3]
 """
@@ -18,6 +19,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SHAPES = [(64, 56, 64, 3, 1), (128, 56, 128, 3, 2), (128, 28, 128, 3, 1), (256, 28, 256, 3, 2),
           (256, 14, 256, 3, 1), (512, 14, 512, 3, 2), (512, 7, 512, 3, 1),
           (256, 56, 512, 1, 2), (512, 28, 1024, 1, 2), (1024, 14, 2048, 1, 2)]
+# every distinct 1×1 stride-1 (conv1 / conv3 / layer1 downsample)
+SHAPES_1X1 = [(64, 56, 64, 1, 1), (64, 56, 256, 1, 1), (256, 56, 64, 1, 1), (256, 56, 128, 1, 1),
+              (128, 28, 512, 1, 1), (512, 28, 128, 1, 1), (512, 28, 256, 1, 1), (256, 14, 1024, 1, 1),
+              (1024, 14, 256, 1, 1), (1024, 14, 512, 1, 1), (512, 7, 2048, 1, 1), (2048, 7, 512, 1, 1)]
 
 
 def main():
@@ -25,6 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only-1x1", action="store_true")
     a = ap.parse_args()
     import torch
     import torch.nn.functional as F
@@ -46,7 +52,7 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / a.iters * 1e3
 
-    for C, H, K, R, st in SHAPES:
+    for C, H, K, R, st in ([] if a.only_1x1 else SHAPES) + SHAPES_1X1:
         N, pad = a.batch, (R - 1) // 2
         x = torch.randn(N, C, H, H, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
         w = (torch.randn(K, C, R, R, device=dev) / (C * R * R) ** 0.5).bfloat16().contiguous(
@@ -61,7 +67,21 @@ def main():
             "hip_dgrad": lambda: m.conv_dgrad(dy, wt, C, R, R, H, H, st, pad),
             "miopen_dgrad": lambda: cb(dy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
                                        [True, False, False]),
+            "hip_wgrad": lambda: m.conv_wgrad(dy, x, R, R, st, pad),
+            "miopen_wgrad": lambda: cb(dy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+                                       [False, True, False]),
         }
+        if R == 1 and st == 1:
+            T = N * H * H
+            x2, dy2, w2 = x.permute(0, 2, 3, 1).reshape(T, C), dy.permute(0, 2, 3, 1).reshape(T, K), w.view(K, C)
+            w2t = w2.t().contiguous()
+            gw = torch.empty(K, C, device=dev, dtype=torch.bfloat16)
+            if m.gemm_nt_supported(T, K, C):
+                cand["gemm_fwd"] = lambda: m.gemm_nt(x2, w2)
+            if m.gemm_nt_supported(T, C, K):
+                cand["gemm_dgrad"] = lambda: m.gemm_nt(dy2, w2t)
+            if ((K + 255) // 256) * (C // 256) >= 8:
+                cand["gemm_wgrad"] = lambda: m.gemm_dw(dy2, x2, gw, False)
         times = {k: [] for k in cand}
         for _ in range(a.rounds):
             for k, fn in cand.items():
