@@ -318,8 +318,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
 
 // forward finalize from the convolution epilogue's per-M-tile partials
 // ([G][2][C]: Σv and Σ(v − mean_tile)² over the tile's rows, conv.hip): a
-// block per 8 channels, 32 tile lanes × 8 channels.  Two plain reductions
-// (no sequential merge): mean = Σ sum_i / M, then M2 = Σ (M2_i + n_i·(mean_i − mean)²)
+// block per 8 channels, 256 tile lanes each reading the 8 channels as one
+// 32-B vector (G = 3 136 tiles at ResNet's 56 × 56 × 64: 13 per lane).  Two
+// plain reductions (no sequential merge): mean = Σ sum_i / M, then
+// M2 = Σ (M2_i + n_i·(mean_i − mean)²); both through an in-order LDS tree.
+__device__ __forceinline__ f32x8 tree_sum256(f32x8 v, f32x8* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  const f32x8 t = red[0];
+  __syncthreads();
+  return t;
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __restrict__ part, int G, int tile_rows,
                                                                 long long M, int C, const float* __restrict__ w,
                                                                 const float* __restrict__ b, float eps,
@@ -328,45 +343,39 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __r
                                                                 float* __restrict__ mean_out,
                                                                 float* __restrict__ invstd_out,
                                                                 float* __restrict__ ss) {
-  const int ch = threadIdx.x & 7, tl = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + ch;
-  __shared__ float red[32][8];
-  __shared__ float bc[8];
-  float s = 0.f;
-  for (int i = tl; i < G; i += 32) s += part[(size_t)i * 2 * C + c];
-  red[tl][ch] = s;
-  __syncthreads();
-  if (tl == 0) {
-    float t = 0.f;
-    for (int k = 0; k < 32; ++k) t += red[k][ch];
-    bc[ch] = t / (float)M;
-  }
-  __syncthreads();
-  const float mean = bc[ch];
-  float q = 0.f;
-  for (int i = tl; i < G; i += 32) {
+  const int c = blockIdx.x * 8;
+  __shared__ f32x8 red[256];
+  f32x8 s = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < G; i += 256) s += *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + c);
+  const f32x8 mean = tree_sum256(s, red) * (1.f / (float)M);
+  f32x8 q = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < G; i += 256) {
     const long long r0 = (long long)i * tile_rows;
     const float n = (float)(M - r0 < tile_rows ? M - r0 : tile_rows);
-    const float d = part[(size_t)i * 2 * C + c] / n - mean;
-    q += part[(size_t)i * 2 * C + C + c] + n * d * d;
+    const f32x8 d = *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + c) * (1.f / n) - mean;
+    q += *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + C + c) + n * d * d;
   }
-  __syncthreads();
-  red[tl][ch] = q;
-  __syncthreads();
-  if (tl != 0) return;
-  float t = 0.f;
-  for (int k = 0; k < 32; ++k) t += red[k][ch];
-  const float var = fmaxf(t / (float)M, 0.f);
-  const float inv = rsqrtf(var + eps);
-  mean_out[c] = mean;
-  invstd_out[c] = inv;
-  const float sc = w[c] * inv;
-  ss[c] = sc;
-  ss[C + c] = b[c] - mean * sc;
+  q = tree_sum256(q, red);
+  if (threadIdx.x != 0) return;
+  f32x8 var, inv;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    var[j] = fmaxf(q[j] / (float)M, 0.f);
+    inv[j] = rsqrtf(var[j] + eps);
+  }
+  *reinterpret_cast<f32x8*>(mean_out + c) = mean;
+  *reinterpret_cast<f32x8*>(invstd_out + c) = inv;
+  const Affine a = affine8(mean, inv, w + c, b + c);
+  *reinterpret_cast<f32x8*>(ss + c) = a.sc;
+  *reinterpret_cast<f32x8*>(ss + C + c) = a.sh;
   if (running_mean) {
     const float unb = M > 1 ? (float)M / (float)(M - 1) : 1.f;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + (momentum * unb) * var;
+    f32x8 rm = *reinterpret_cast<const f32x8*>(running_mean + c);
+    f32x8 rv = *reinterpret_cast<const f32x8*>(running_var + c);
+    rm = (1.f - momentum) * rm + momentum * mean;
+    rv = (1.f - momentum) * rv + (momentum * unb) * var;
+    *reinterpret_cast<f32x8*>(running_mean + c) = rm;
+    *reinterpret_cast<f32x8*>(running_var + c) = rv;
   }
 }
 

@@ -393,7 +393,11 @@ __global__ __launch_bounds__(CNT, 2) void conv_wgrad_kernel(const WgradArgs a) {
   constexpr int NA = PA / 4, NB = PB / 4;            // per wave
   constexpr int SA = 64 * RA, STAGE = 64 * (RA + RB);
   constexpr int MI = BMW / 32, NJ = BNW / 32;        // 16×16 blocks per wave (wave tile BMW/2 × BNW/2)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // ring depth: the small tiles do little MFMA work per k-step, so the stream
+  // needs more 64-token steps in flight (2 workgroups per CU: ≤ 80 KiB each)
+  constexpr int NS = STAGE <= 16384 ? 4 : STAGE <= 24576 ? 3 : 2;
+  constexpr int PER = NA + NB;                       // DMA pieces per wave per k-step
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -463,16 +467,21 @@ __global__ __launch_bounds__(CNT, 2) void conv_wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) issue(k0, 0);
+  // prologue: k-steps 0 .. NS-2 in flight; step k refills the stage step k-1 used
+  // (every wave's reads of it retired at the barrier that closed step k-1)
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < nk) issue(k0 + j, j);
   for (int k = 0; k < nk; ++k) {
-    if (k + 1 < nk) {
-      issue(k0 + k + 1, (k + 1) & 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (k + NS - 1 < nk) issue(k0 + k + NS - 1, (k + NS - 1) % NS);
+    // steps issued after k (in flight behind it): min(NS - 1, nk - 1 - k)
+    const int after = nk - 1 - k < NS - 1 ? nk - 1 - k : NS - 1;
+    if (after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+    else if (after == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const char* TA_ = smem + (k & 1) * STAGE;
+    const char* TA_ = smem + (k % NS) * STAGE;
     const char* TB_ = TA_ + SA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -503,14 +512,31 @@ __global__ __launch_bounds__(CNT, 2) void conv_wgrad_kernel(const WgradArgs a) {
     }
 }
 
-// out[i] (+)= Σ_s part[s][i], s in order (fp32, 4 per lane)
+// out[i] (+)= Σ_s part[s][i] (fp32, 4 per lane).  A block owns 256 / G
+// consecutive f32x4 outputs; lane group g sums splits g, g + G, … in order and
+// the G group sums join in order through LDS — deterministic, and G-way
+// parallel over the splits (a 64 × 64 1×1 weight has 1 024 f32x4 outputs but
+// up to 256 splits: one lane per output would walk all of them serially).
+template <int G>
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int splits,
                                                                 long long n4, float* __restrict__ out,
                                                                 int accumulate) {
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    f32x4 v = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < splits; ++k) v += reinterpret_cast<const f32x4*>(part)[(long long)k * n4 + i];
-    reinterpret_cast<f32x4*>(out)[i] = v;
+  constexpr int OB = 256 / G;
+  __shared__ f32x4 red[G][OB];
+  const int o = threadIdx.x % OB, g = threadIdx.x / OB;
+  const long long i = (long long)blockIdx.x * OB + o;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+#pragma unroll 4
+    for (int k = g; k < splits; k += G) v += reinterpret_cast<const f32x4*>(part)[(long long)k * n4 + i];
+  }
+  red[g][o] = v;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    f32x4 t = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < G; ++k) t += red[k][o];
+    reinterpret_cast<f32x4*>(out)[i] = t;
   }
 }
 
@@ -759,7 +785,13 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
   else if (bn == 128) conv_wgrad_kernel<64, 128><<<(unsigned)grid, CNT, 0, st>>>(a);
   else conv_wgrad_kernel<64, 64><<<(unsigned)grid, CNT, 0, st>>>(a);
   const long long n4 = (long long)Kout * a.T * C / 4;
-  conv_wgrad_reduce_kernel<<<stream_grid(n4, 256), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
+  // split-group width: ≥ 1 024 blocks where the outputs allow, ≤ the split count
+  if (a.splits >= 16 && n4 < 1024LL * 64)
+    conv_wgrad_reduce_kernel<16><<<(unsigned)((n4 + 15) / 16), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
+  else if (a.splits >= 4)
+    conv_wgrad_reduce_kernel<4><<<(unsigned)((n4 + 63) / 64), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
+  else
+    conv_wgrad_reduce_kernel<1><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
   return 0;
 }
 

@@ -1027,7 +1027,9 @@ class _ConvFn(torch.autograd.Function):
             dalias = dalias.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if link is None and ctx.one and _gemm_dgrad_1x1(m, T, C, K):
+            # the GEMM where it is faster, even past a BatchNorm link (that
+            # BatchNorm then takes its own statistics pass)
+            if ctx.one and _gemm_dgrad_1x1(m, T, C, K):
                 dy2 = dy.permute(0, 2, 3, 1).reshape(T, K)
                 wt2 = transpose(wb.view(K, C))
                 dx = (m.gemm_nt_add(dy2, wt2, dalias.permute(0, 2, 3, 1).reshape(T, C)) if dalias is not None
