@@ -115,6 +115,122 @@ __device__ __forceinline__ void glds(unsigned voff, const void* sbase, unsigned 
                : "memory");
 }
 
+// Epilogue shared by the implicit-GEMM mainloops: acc[i][j][e] =
+// C[m = wm·RW + 16i + 4(l >> 4) + e][col n0 + wn·64 + 4(l & 15) + j] (RW = BM / WM
+// rows per wave): bf16 stores (+ a joining gradient), and the BatchNorm
+// forward tile statistics or the consumed BatchNorm's backward partials.
+template <int MI, int BM, int BN, int WM>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI][4], char* smem, int wm, int wn,
+                                              int lane, long long m0, long long tm, int n0) {
+  constexpr int RW = BM / WM;
+  const int g4 = lane >> 4;
+  const int col = n0 + wn * 64 + 4 * (lane & 15);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 bsc, bsh, bmu;
+  const bool bnb = a.bx != nullptr;
+  if (bnb) {
+    bmu = *reinterpret_cast<const f32x4*>(a.bmean + col);
+    const f32x4 inv = *reinterpret_cast<const f32x4*>(a.binv + col);
+    bsc = *reinterpret_cast<const f32x4*>(a.bw + col) * inv;
+    bsh = *reinterpret_cast<const f32x4*>(a.bb + col) - bmu * bsc;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = wm * RW + 16 * i + 4 * g4 + e;
+      const long long t = m0 + m;
+      if (t >= a.M) continue;
+      long long row;
+      if (a.ident) {
+        row = t;
+      } else {
+        int q, bb, n, aa;
+        divmod((int)t, a.TB, a.inv_TB, q, bb);
+        divmod(q, a.TA, a.inv_TA, n, aa);
+        row = ((long long)n * a.OH + aa * a.ost + a.oph) * a.OW + bb * a.ost + a.opw;
+      }
+      f32x4 o = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
+      if (a.add) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.add + row * a.Kout + col);
+        o += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+      }
+      const bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      *reinterpret_cast<bf16x4*>(a.y + row * a.Kout + col) = v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cs[j] += (float)v[j];
+      if (bnb) {
+        const bf16x4 xb = *reinterpret_cast<const bf16x4*>(a.bx + row * a.Kout + col);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xv = (float)xb[j];
+          // the forward's pre-activation through the same fp32 ops (bit-identical mask)
+          const float g = (!a.brelu || xv * bsc[j] + bsh[j] > 0.f) ? (float)v[j] : 0.f;
+          s1[j] += g;
+          s2[j] += g * (xv - bmu[j]);
+        }
+      }
+    }
+  if (!a.stats && !bnb) return;
+  const int rows = (int)(a.M - m0 < BM ? a.M - m0 : BM);
+  float* red = reinterpret_cast<float*>(smem);  // [WM][BN] (the last k-step's barrier freed the stages)
+  auto tile_sum = [&](float (&v)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] += __shfl_xor(v[j], 16, 64);
+      v[j] += __shfl_xor(v[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[wm * BN + wn * 64 + 4 * lane + j] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int u = 0; u < WM; ++u) s += red[u * BN + wn * 64 + 4 * (lane & 15) + j];
+      v[j] = s;
+    }
+    __syncthreads();
+  };
+  if (bnb) {
+    // ---- BatchNorm backward partials of this M-tile: Σg, Σg·(x − mean) per channel
+    tile_sum(s1);
+    tile_sum(s2);
+    if (wm == 0 && lane < 16) {
+      float* p = a.bpart + (size_t)(a.tile_off + tm) * 2 * a.Kout + col;
+      *reinterpret_cast<f32x4*>(p) = f32x4{s1[0], s1[1], s1[2], s1[3]};
+      *reinterpret_cast<f32x4*>(p + a.Kout) = f32x4{s2[0], s2[1], s2[2], s2[3]};
+    }
+    return;
+  }
+  // ---- BatchNorm forward partials of this M-tile: Σv and Σ(v − mean_tile)² per channel
+  tile_sum(cs);
+  float mean[4], cq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) mean[j] = cs[j] / (float)rows;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long t = m0 + wm * RW + 16 * i + 4 * g4 + e;
+      if (t >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = (float)(bf16)acc[i][j][e] - mean[j];
+        cq[j] += d * d;
+      }
+    }
+  tile_sum(cq);
+  if (wm == 0 && lane < 16) {
+    float* p = a.stats + (size_t)tm * 2 * a.Kout + col;
+    *reinterpret_cast<f32x4*>(p) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    *reinterpret_cast<f32x4*>(p + a.Kout) = f32x4{cq[0], cq[1], cq[2], cq[3]};
+  }
+}
+
 template <int BM, int BN>
 __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
   constexpr int WN = BN / 64, WM = BM / 64;
@@ -230,113 +346,122 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
     __builtin_amdgcn_s_barrier();  // every wave's reads of this stage precede its refill (k-step kt + 2)
   }
 
-  // ---- epilogue: acc[i][j][e] = C[m = wm·64 + 16i + 4(l >> 4) + e][col n0 + wn·64 + 4(l & 15) + j]
-  const int g4 = lane >> 4;
-  const int col = n0 + wn * 64 + 4 * (lane & 15);
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  f32x4 bsc, bsh, bmu;
-  const bool bnb = a.bx != nullptr;
-  if (bnb) {
-    bmu = *reinterpret_cast<const f32x4*>(a.bmean + col);
-    const f32x4 inv = *reinterpret_cast<const f32x4*>(a.binv + col);
-    bsc = *reinterpret_cast<const f32x4*>(a.bw + col) * inv;
-    bsh = *reinterpret_cast<const f32x4*>(a.bb + col) - bmu * bsc;
+  conv_epilogue<4, BM, BN, WM>(a, acc, smem, wm, wn, lane, m0, tm, n0);
+}
+
+// ============================================================================
+// Mainloop 2 (PDO_CONV_IMPL=2): gemm_nt2's shape — BM = 256 tokens × BN (128,
+// or 64 for Kout = 64) output channels per workgroup, two workgroups per CU,
+// BK = 32 channels of one tap per k-step, a 3-stage LDS ring filled two steps
+// ahead, one barrier per step.  Against mainloop 1 (128 × 128, BK = 64, two
+// stages, two barriers) it moves 25-33 % fewer operand bytes per MFMA from L2
+// into LDS and keeps two k-steps of loads in flight.  Waves: 2 × 2 of 128 × 64
+// (BN = 128) or 4 × 1 of 64 × 64 (BN = 64).  LDS rows are 64 B, chunk c of row
+// r at c ^ ((r >> 2) & 3); a DMA piece is 16 rows (1 KiB).
+template <int BN>
+__global__ __launch_bounds__(CNT, 2) void conv_igemm2_kernel(const ConvArgs a) {
+  constexpr int BM = 256, BK = 32, NSG = 3;
+  constexpr int WN = BN / 64, WM = 4 / WN, RW = BM / WM, MI = RW / 16;
+  constexpr int SA = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int NA = BM / 16 / 4, NB = BN / 16 / 4, PER = NA + NB;  // pieces per wave per k-step
+  __shared__ __attribute__((aligned(16))) char smem[NSG * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int ntn = a.Kout / BN;
+  const long long ntm = (a.M + BM - 1) / BM;
+  long long id = blockIdx.x;
+  {  // bijective XCD remap (mainloop 1)
+    const long long nwg = ntm * ntn, q = nwg >> 3, r = nwg & 7, x = id & 7, slot = id >> 3;
+    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
   }
+  const int tn = (int)(id % ntn);
+  const long long tm = id / ntn;
+  const long long m0 = tm * BM;
+  const int n0 = tn * BN;
+
+  // ---- A pieces p = w + 4i: rows 16p + (l >> 2), source chunk (l & 3) ^ ((l >> 4) & 3)
+  const int lch = (lane & 3) ^ ((lane >> 4) & 3);
+  int hb[NA], wb[NA], base[NA];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = wm * 64 + 16 * i + 4 * g4 + e;
-      const long long t = m0 + m;
-      if (t >= a.M) continue;
-      long long row;
-      if (a.ident) {
-        row = t;
-      } else {
-        int q, bb, n, aa;
-        divmod((int)t, a.TB, a.inv_TB, q, bb);
-        divmod(q, a.TA, a.inv_TA, n, aa);
-        row = ((long long)n * a.OH + aa * a.ost + a.oph) * a.OW + bb * a.ost + a.opw;
-      }
-      f32x4 o = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
-      if (a.add) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.add + row * a.Kout + col);
-        o += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
-      }
-      const bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-      *reinterpret_cast<bf16x4*>(a.y + row * a.Kout + col) = v;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cs[j] += (float)v[j];
-      if (bnb) {
-        const bf16x4 xb = *reinterpret_cast<const bf16x4*>(a.bx + row * a.Kout + col);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float xv = (float)xb[j];
-          // the forward's pre-activation through the same fp32 ops (bit-identical mask)
-          const float g = (!a.brelu || xv * bsc[j] + bsh[j] > 0.f) ? (float)v[j] : 0.f;
-          s1[j] += g;
-          s2[j] += g * (xv - bmu[j]);
-        }
-      }
+  for (int i = 0; i < NA; ++i) {
+    const long long t = m0 + 16 * (w + 4 * i) + (lane >> 2);
+    if (t < a.M) {
+      int q, bb, n, aa;
+      divmod((int)t, a.TB, a.inv_TB, q, bb);
+      divmod(q, a.TA, a.inv_TA, n, aa);
+      hb[i] = aa * a.ist - a.ipad;
+      wb[i] = bb * a.ist - a.ipad;
+      base[i] = ((n * a.IH + hb[i]) * a.IW + wb[i]) * a.C + lch * 8;
+    } else {
+      hb[i] = -(1 << 20);  // fails every bounds check
+      wb[i] = 0;
+      base[i] = 0;
     }
-  if (!a.stats && !bnb) return;
-  const int rows = (int)(a.M - m0 < BM ? a.M - m0 : BM);
-  float* red = reinterpret_cast<float*>(smem);  // [WM][BN] (the last k-step's barrier freed the stages)
-  auto tile_sum = [&](float (&v)[4]) {
+  }
+  // ---- B pieces p = w + 4i: wave column block i, physical row 16w + t ↔ column 64i + 4t + w
+  unsigned voffB[NB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] += __shfl_xor(v[j], 16, 64);
-      v[j] += __shfl_xor(v[j], 32, 64);
+  for (int i = 0; i < NB; ++i) {
+    const int col = n0 + 64 * i + 4 * (lane >> 2) + w;
+    voffB[i] = (unsigned)((col * a.ldb + lch * 8) * 2);
+  }
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem + (unsigned)(w * 1024);
+  const int CC = a.C / BK;
+  const int nk = a.ntaps * CC;
+
+  auto issue = [&](int kt, int stage) {
+    const int tap = kt / CC, cc = kt - tap * CC;
+    const int dh = a.dh[tap], dw = a.dw[tap];
+    const int coff = (dh * a.IW + dw) * a.C + cc * BK;
+    const unsigned sb = lds0 + (unsigned)(stage * STAGE);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int hi = hb[i] + dh, wi = wb[i] + dw;
+      const bool ok = (unsigned)hi < (unsigned)a.IH && (unsigned)wi < (unsigned)a.IW;
+      bufld(ok ? (unsigned)((base[i] + coff) * 2) : OOB, rsX, sb + (unsigned)(4096 * i));
     }
-    if (lane < 16) {
+    const bf16* bsrc = a.w + a.bcol[tap] + cc * BK;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) red[wm * BN + wn * 64 + 4 * lane + j] = v[j];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int u = 0; u < WM; ++u) s += red[u * BN + wn * 64 + 4 * (lane & 15) + j];
-      v[j] = s;
-    }
-    __syncthreads();
+    for (int i = 0; i < NB; ++i) glds(voffB[i], bsrc, sb + (unsigned)(SA + 4096 * i));
   };
-  if (bnb) {
-    // ---- BatchNorm backward partials of this M-tile: Σg, Σg·(x − mean) per channel
-    tile_sum(s1);
-    tile_sum(s2);
-    if (wm == 0 && lane < 16) {
-      float* p = a.bpart + (size_t)(a.tile_off + tm) * 2 * a.Kout + col;
-      *reinterpret_cast<f32x4*>(p) = f32x4{s1[0], s1[1], s1[2], s1[3]};
-      *reinterpret_cast<f32x4*>(p + a.Kout) = f32x4{s2[0], s2[1], s2[2], s2[3]};
-    }
-    return;
+
+  // ---- fragments: row (l & 15) of a 16-row block, k chunk (l >> 4), swizzled
+  const int pch = (lane >> 4) ^ ((lane >> 2) & 3);
+  const int oA = (wm * RW + (lane & 15)) * 64 + pch * 16;
+  const int oB = SA + (wn * 64 + (lane & 15)) * 64 + pch * 16;
+
+  f32x4 acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int sg = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step kt landed (kt + 1 flies)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... for every wave; every wave's reads of step kt - 1 are done
+    if (kt + 2 < nk) issue(kt + 2, sg == 0 ? 2 : sg - 1);  // into step kt - 1's stage
+    const char* st = smem + sg * STAGE;
+    bf16x8 fa[MI], fb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + oB + j * 1024);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + oA + i * 1024);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    sg = sg == 2 ? 0 : sg + 1;
   }
-  // ---- BatchNorm forward partials of this M-tile: Σv and Σ(v − mean_tile)² per channel
-  tile_sum(cs);
-  float mean[4], cq[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) mean[j] = cs[j] / (float)rows;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const long long t = m0 + wm * 64 + 16 * i + 4 * g4 + e;
-      if (t >= a.M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = (float)(bf16)acc[i][j][e] - mean[j];
-        cq[j] += d * d;
-      }
-    }
-  tile_sum(cq);
-  if (wm == 0 && lane < 16) {
-    float* p = a.stats + (size_t)tm * 2 * a.Kout + col;
-    *reinterpret_cast<f32x4*>(p) = f32x4{cs[0], cs[1], cs[2], cs[3]};
-    *reinterpret_cast<f32x4*>(p + a.Kout) = f32x4{cq[0], cq[1], cq[2], cq[3]};
-  }
+  // the epilogue reuses the LDS for its tile sums: every wave's last reads first
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  conv_epilogue<MI, BM, BN, WM>(a, acc, smem, wm, wn, lane, m0, tm, n0);
 }
 
 // Wᵀ for the input gradient: w [K][T][C] → wt [C][T][K] (T = R·S taps), bf16
@@ -548,9 +673,23 @@ int launch_igemm(const ConvArgs& a, hipStream_t st) {
   return 0;
 }
 
+// PDO_CONV_IMPL: 1 = mainloop 1 (128 × 128 / 256 × 64, BK 64), 2 = mainloop 2
+int g_conv_impl = [] {
+  const char* e = getenv("PDO_CONV_IMPL");
+  return e && *e ? atoi(e) : 1;
+}();
+
 int run_igemm(ConvArgs& a, hipStream_t st, int* tile_rows) {
   a.inv_TA = 1.f / (float)a.TA;
   a.inv_TB = 1.f / (float)a.TB;
+  if (g_conv_impl == 2) {
+    if (tile_rows) *tile_rows = 256;
+    const long long tiles = ((a.M + 255) / 256) * (a.Kout / (a.Kout == 64 ? 64 : 128));
+    if (tiles > 0x7fffffffLL) return -2;
+    if (a.Kout == 64) conv_igemm2_kernel<64><<<(unsigned)tiles, CNT, 0, st>>>(a);
+    else conv_igemm2_kernel<128><<<(unsigned)tiles, CNT, 0, st>>>(a);
+    return 0;
+  }
   if (a.Kout == 64) {
     if (tile_rows) *tile_rows = 256;
     return launch_igemm<256, 64>(a, st);
@@ -576,8 +715,16 @@ int conv_supported(int N, int H, int W, int C, int Kout, int R, int S, int strid
   return yb < (1ll << 31);
 }
 
-int conv_fwd_tiles(long long M, int Kout) { return (int)((M + (Kout == 64 ? 255 : 127)) / (Kout == 64 ? 256 : 128)); }
-int conv_fwd_tile_rows(int Kout) { return Kout == 64 ? 256 : 128; }
+int conv_fwd_tile_rows(int Kout) { return (g_conv_impl == 2 || Kout == 64) ? 256 : 128; }
+int conv_fwd_tiles(long long M, int Kout) {
+  const int r = conv_fwd_tile_rows(Kout);
+  return (int)((M + r - 1) / r);
+}
+int conv_impl(int impl) {
+  const int prev = g_conv_impl;
+  if (impl == 1 || impl == 2) g_conv_impl = impl;
+  return prev;
+}
 
 int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int Kout, int R, int S, int stride, int pad,
                   bf16* y, float* tile_stats, hipStream_t st) {
@@ -621,7 +768,7 @@ int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t s
 
 // tiles the input gradient writes BatchNorm-backward partials for (conv_dgrad_nhwc with bn)
 int conv_dgrad_tiles(int N, int H, int W, int C, int R, int stride, int pad) {
-  const int bm = C == 64 ? 256 : 128;
+  const int bm = conv_fwd_tile_rows(C);
   if (stride == 1) return (int)(((long long)N * H * W + bm - 1) / bm);
   long long t = 0;
   for (int ph = 0; ph < 2; ++ph)
