@@ -882,7 +882,6 @@ PYBIND11_MODULE(_pdo_hip, m) {
     if (impl >= 0) pdo::gemm_dw_set_impl(impl);
     return prev;
   }, py::arg("impl") = -1, "select gemm_dw's mainloop (0 = 8-wave, 1.. = 4-wave variants); returns the previous");
-  m.def("gemm_nt2_mode", &pdo::gemm_nt2_mode);
   m.def("gemm_nt_impl", [](int impl) {
     const int prev = pdo::gemm_nt_get_impl();
     if (impl >= 0) pdo::gemm_nt_set_impl(impl);

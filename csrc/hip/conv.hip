@@ -135,36 +135,42 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI
     bsc = *reinterpret_cast<const f32x4*>(a.bw + col) * inv;
     bsh = *reinterpret_cast<const f32x4*>(a.bb + col) - bmu * bsc;
   }
+  // per 4-row group: the rows' addresses and their joining-gradient / BatchNorm
+  // input loads first (8 loads in flight), then the math and the stores
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < MI; ++i) {
+    long long rowv[4];
+    bf16x4 adv[4], xbv[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int m = wm * RW + 16 * i + 4 * g4 + e;
-      const long long t = m0 + m;
+      const long long t = m0 + wm * RW + 16 * i + 4 * g4 + e;
+      rowv[e] = -1;
       if (t >= a.M) continue;
-      long long row;
       if (a.ident) {
-        row = t;
+        rowv[e] = t;
       } else {
         int q, bb, n, aa;
         divmod((int)t, a.TB, a.inv_TB, q, bb);
         divmod(q, a.TA, a.inv_TA, n, aa);
-        row = ((long long)n * a.OH + aa * a.ost + a.oph) * a.OW + bb * a.ost + a.opw;
+        rowv[e] = ((long long)n * a.OH + aa * a.ost + a.oph) * a.OW + bb * a.ost + a.opw;
       }
+      if (a.add) adv[e] = *reinterpret_cast<const bf16x4*>(a.add + rowv[e] * a.Kout + col);
+      if (bnb) xbv[e] = *reinterpret_cast<const bf16x4*>(a.bx + rowv[e] * a.Kout + col);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long row = rowv[e];
+      if (row < 0) continue;
       f32x4 o = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
-      if (a.add) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(a.add + row * a.Kout + col);
-        o += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
-      }
+      if (a.add) o += f32x4{(float)adv[e][0], (float)adv[e][1], (float)adv[e][2], (float)adv[e][3]};
       const bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
       *reinterpret_cast<bf16x4*>(a.y + row * a.Kout + col) = v;
 #pragma unroll
       for (int j = 0; j < 4; ++j) cs[j] += (float)v[j];
       if (bnb) {
-        const bf16x4 xb = *reinterpret_cast<const bf16x4*>(a.bx + row * a.Kout + col);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float xv = (float)xb[j];
+          const float xv = (float)xbv[e][j];
           // the forward's pre-activation through the same fp32 ops (bit-identical mask)
           const float g = (!a.brelu || xv * bsc[j] + bsh[j] > 0.f) ? (float)v[j] : 0.f;
           s1[j] += g;
@@ -172,6 +178,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI
         }
       }
     }
+  }
   if (!a.stats && !bnb) return;
   const int rows = (int)(a.M - m0 < BM ? a.M - m0 : BM);
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN] (the last k-step's barrier freed the stages)
@@ -358,11 +365,14 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
 // into LDS and keeps two k-steps of loads in flight.  Waves: 2 × 2 of 128 × 64
 // (BN = 128) or 4 × 1 of 64 × 64 (BN = 64).  LDS rows are 64 B, chunk c of row
 // r at c ^ ((r >> 2) & 3); a DMA piece is 16 rows (1 KiB).
-template <int BN>
+template <int BM, int BN>
 __global__ __launch_bounds__(CNT, 2) void conv_igemm2_kernel(const ConvArgs a) {
-  constexpr int BM = 256, BK = 32, NSG = 3;
+  constexpr int BK = 32;
   constexpr int WN = BN / 64, WM = 4 / WN, RW = BM / WM, MI = RW / 16;
   constexpr int SA = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  // ring depth: as many stages as fit 80 KiB (two workgroups per CU), 2..4
+  constexpr int NSG = 81920 / STAGE > 4 ? 4 : 81920 / STAGE;
+  static_assert(NSG >= 2, "two stages at least");
   constexpr int NA = BM / 16 / 4, NB = BN / 16 / 4, PER = NA + NB;  // pieces per wave per k-step
   __shared__ __attribute__((aligned(16))) char smem[NSG * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -438,14 +448,18 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm2_kernel(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
+#pragma unroll
+  for (int j = 0; j < NSG - 1; ++j)
+    if (j < nk) issue(j, j);
   int sg = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step kt landed (kt + 1 flies)
+    // step kt landed: the steps issued after it (≤ NSG − 2) may still fly
+    const int after = nk - 1 - kt < NSG - 2 ? nk - 1 - kt : NSG - 2;
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // ... for every wave; every wave's reads of step kt - 1 are done
-    if (kt + 2 < nk) issue(kt + 2, sg == 0 ? 2 : sg - 1);  // into step kt - 1's stage
+    if (kt + NSG - 1 < nk) issue(kt + NSG - 1, sg == 0 ? NSG - 1 : sg - 1);  // into step kt - 1's stage
     const char* st = smem + sg * STAGE;
     bf16x8 fa[MI], fb[4];
 #pragma unroll
@@ -456,7 +470,7 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm2_kernel(const ConvArgs a) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    sg = sg == 2 ? 0 : sg + 1;
+    sg = sg == NSG - 1 ? 0 : sg + 1;
   }
   // the epilogue reuses the LDS for its tile sums: every wave's last reads first
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -682,12 +696,15 @@ int g_conv_impl = [] {
 int run_igemm(ConvArgs& a, hipStream_t st, int* tile_rows) {
   a.inv_TA = 1.f / (float)a.TA;
   a.inv_TB = 1.f / (float)a.TB;
-  if (g_conv_impl == 2) {
-    if (tile_rows) *tile_rows = 256;
-    const long long tiles = ((a.M + 255) / 256) * (a.Kout / (a.Kout == 64 ? 64 : 128));
+  if (g_conv_impl >= 2) {
+    // 2: 128 × 128 (4 stages); 3: 256 × 128 (3 stages); Kout = 64: 256 × 64 (4 stages)
+    const int bm = (a.Kout == 64 || g_conv_impl == 3) ? 256 : 128;
+    if (tile_rows) *tile_rows = bm;
+    const long long tiles = ((a.M + bm - 1) / bm) * (a.Kout / (a.Kout == 64 ? 64 : 128));
     if (tiles > 0x7fffffffLL) return -2;
-    if (a.Kout == 64) conv_igemm2_kernel<64><<<(unsigned)tiles, CNT, 0, st>>>(a);
-    else conv_igemm2_kernel<128><<<(unsigned)tiles, CNT, 0, st>>>(a);
+    if (a.Kout == 64) conv_igemm2_kernel<256, 64><<<(unsigned)tiles, CNT, 0, st>>>(a);
+    else if (bm == 256) conv_igemm2_kernel<256, 128><<<(unsigned)tiles, CNT, 0, st>>>(a);
+    else conv_igemm2_kernel<128, 128><<<(unsigned)tiles, CNT, 0, st>>>(a);
     return 0;
   }
   if (a.Kout == 64) {
@@ -715,14 +732,14 @@ int conv_supported(int N, int H, int W, int C, int Kout, int R, int S, int strid
   return yb < (1ll << 31);
 }
 
-int conv_fwd_tile_rows(int Kout) { return (g_conv_impl == 2 || Kout == 64) ? 256 : 128; }
+int conv_fwd_tile_rows(int Kout) { return (g_conv_impl == 3 || Kout == 64) ? 256 : 128; }
 int conv_fwd_tiles(long long M, int Kout) {
   const int r = conv_fwd_tile_rows(Kout);
   return (int)((M + r - 1) / r);
 }
 int conv_impl(int impl) {
   const int prev = g_conv_impl;
-  if (impl == 1 || impl == 2) g_conv_impl = impl;
+  if (impl >= 1 && impl <= 3) g_conv_impl = impl;
   return prev;
 }
 

@@ -242,11 +242,6 @@ static int g_impl = [] {
   return e && *e ? atoi(e) : 1;
 }();
 
-static int g_nt2 = [] {
-  const char* e = getenv("PDO_NT2");
-  return e && *e ? atoi(e) : 0;
-}();
-
 // N % 256 = 128 (the 50304-column LM head) only on the 4-wave mainloop
 static bool nt4_path(int K) { return g_impl >= 1 && K % 128 == 0 && K >= 256; }
 
@@ -258,11 +253,7 @@ int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
 
 int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
 void gemm_nt_set_impl(int impl) { g_impl = impl; }
-int gemm_nt2_mode(int mode) {
-  const int prev = g_nt2;
-  if (mode >= 0) g_nt2 = mode;
-  return prev;
-}
+
 int gemm_nt_get_impl() { return g_impl; }
 
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
@@ -271,10 +262,6 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
   if (epi >= 1 && epi <= 3 && !bias) return -3;
   if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
-  // the fused GELU / GELU′ epilogues on the two-workgroups-per-CU mainloop
-  // (PDO_NT2: 1 = EPI 2 / 3, 2 = every epilogue; 0 = off)
-  if (g_nt2 > 0 && (epi >= 2 || g_nt2 >= 2) && epi <= 3 && gemm_nt2_ok(M, N, K))
-    return gemm_nt2(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st);
   if (nt4_path(K))
     return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, g_impl == 2 ? 1 : 0);
   const long long grid = (long long)(M / BM) * (N / BN);

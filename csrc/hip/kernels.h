@@ -101,10 +101,6 @@ int gemm_nt_dbias_rows(int M);
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);
 // gemm_nt4.hip: the same contract on the 4-wave / 128 × 128-per-wave mainloop
-// two-workgroups-per-CU persistent mainloop (gemm_nt2.hip): M % 256, N % 128, K % 32, K ≥ 96
-int gemm_nt2_ok(int M, int N, int K);
-int gemm_nt2(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
-             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
              const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant = 0);
 // (N % 256 = 128 allowed: half-width last tile column; variant 1 = deferred store drain)
@@ -112,8 +108,6 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
 // (gemm_nt4.hip, default), 2 = 4-wave with the deferred store drain
 void gemm_nt_set_impl(int impl);
 int gemm_nt_get_impl();
-// PDO_NT2 routing (0 off, 1 GELU / GELU′ epilogues, 2 every epilogue); mode < 0 only reads; returns the previous mode
-int gemm_nt2_mode(int mode);
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 

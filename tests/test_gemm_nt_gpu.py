@@ -201,34 +201,3 @@ def test_nt4_fused_epilogues_many_tiles_vs_fp32(hip, impl):
     assert bool(((dx.float() - xp.grad).abs() <= 2e-2 + 1e-2 * xp.grad.abs()).all())
     torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=2e-2, atol=0.5)
 
-
-@pytest.mark.parametrize("M,N,K", [(16384, 4096, 1024), (512, 256, 128), (768, 512, 2048), (3328, 1024, 3072)])
-def test_nt2_two_workgroups_per_cu_vs_fp32(hip, M, N, K):
-    """The two-workgroups-per-CU mainloop (gemm_nt2.hip, PDO_NT2=2: every
-    epilogue) against fp32: plain, bias, GELU (pre-activation + activation) and
-    GELU'+bias-grad; 16384 x 4096 runs 2048 tiles over 512 persistent workgroups
-    (the k-step stream crosses tile boundaries), K = 128 is the 4-step minimum."""
-    g = torch.Generator(device="cuda").manual_seed(M + K)
-    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
-    b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
-    bias = torch.empty(N, device="cuda", dtype=torch.bfloat16).uniform_(-0.1, 0.1, generator=g)
-    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16).uniform_(-2, 2, generator=g)
-    prev = hip.gemm_nt2_mode(2)
-    try:
-        c = hip.gemm_nt(a, b, None)
-        cb = hip.gemm_nt(a, b, bias)
-        p, y = hip.gemm_nt_gelu(a, b, bias)
-        dx, db = hip.gemm_nt_dgelu(a, b, pre, bias)
-    finally:
-        hip.gemm_nt2_mode(prev)
-    ref = a.float() @ b.float().t()
-    tol = 1e-2 + 8e-3 * ref.abs()
-    assert bool(((c.float() - ref).abs() <= tol).all())
-    assert bool(((cb.float() - ref - bias.float()).abs() <= tol).all())
-    assert bool(((p.float() - ref).abs() <= tol).all())
-    gl = torch.nn.functional.gelu(ref + bias.float(), approximate="tanh")
-    assert bool(((y.float() - gl).abs() <= 1e-2 + 8e-3 * gl.abs()).all())
-    xp = (pre.float() + bias.float()).requires_grad_(True)
-    torch.nn.functional.gelu(xp, approximate="tanh").backward(ref.to(torch.bfloat16).float())
-    assert bool(((dx.float() - xp.grad).abs() <= 2e-2 + 1e-2 * xp.grad.abs()).all())
-    torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=2e-2, atol=0.5)

@@ -35,19 +35,6 @@ def main():
         "dw_qkv": lambda: m.gemm_dw(dq, x, gq, False),
         "dw_fc1": lambda: m.gemm_dw(h4, x, g1, False),
     }
-    if hasattr(m, "gemm_nt2_mode") and os.environ.get("AB_NT2"):
-        # the two-workgroups-per-CU mainloop on the same shapes (this build only)
-        def nt2(fn):
-            def run():
-                prev = m.gemm_nt2_mode(2)
-                try:
-                    return fn()
-                finally:
-                    m.gemm_nt2_mode(prev)
-            return run
-        for k in list(cases):
-            if not k.startswith("dw") and not k.startswith("lm"):
-                cases[k + "_nt2"] = nt2(cases[k])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = {}
     for name, fn in cases.items():
