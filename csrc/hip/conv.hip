@@ -356,128 +356,6 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
   conv_epilogue<4, BM, BN, WM>(a, acc, smem, wm, wn, lane, m0, tm, n0);
 }
 
-// ============================================================================
-// Mainloop 2 (PDO_CONV_IMPL=2): gemm_nt2's shape — BM = 256 tokens × BN (128,
-// or 64 for Kout = 64) output channels per workgroup, two workgroups per CU,
-// BK = 32 channels of one tap per k-step, a 3-stage LDS ring filled two steps
-// ahead, one barrier per step.  Against mainloop 1 (128 × 128, BK = 64, two
-// stages, two barriers) it moves 25-33 % fewer operand bytes per MFMA from L2
-// into LDS and keeps two k-steps of loads in flight.  Waves: 2 × 2 of 128 × 64
-// (BN = 128) or 4 × 1 of 64 × 64 (BN = 64).  LDS rows are 64 B, chunk c of row
-// r at c ^ ((r >> 2) & 3); a DMA piece is 16 rows (1 KiB).
-template <int BM, int BN>
-__global__ __launch_bounds__(CNT, 2) void conv_igemm2_kernel(const ConvArgs a) {
-  constexpr int BK = 32;
-  constexpr int WN = BN / 64, WM = 4 / WN, RW = BM / WM, MI = RW / 16;
-  constexpr int SA = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
-  // ring depth: as many stages as fit 80 KiB (two workgroups per CU), 2..4
-  constexpr int NSG = 81920 / STAGE > 4 ? 4 : 81920 / STAGE;
-  static_assert(NSG >= 2, "two stages at least");
-  constexpr int NA = BM / 16 / 4, NB = BN / 16 / 4, PER = NA + NB;  // pieces per wave per k-step
-  __shared__ __attribute__((aligned(16))) char smem[NSG * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WN, wn = w % WN;
-  const int ntn = a.Kout / BN;
-  const long long ntm = (a.M + BM - 1) / BM;
-  long long id = blockIdx.x;
-  {  // bijective XCD remap (mainloop 1)
-    const long long nwg = ntm * ntn, q = nwg >> 3, r = nwg & 7, x = id & 7, slot = id >> 3;
-    id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
-  }
-  const int tn = (int)(id % ntn);
-  const long long tm = id / ntn;
-  const long long m0 = tm * BM;
-  const int n0 = tn * BN;
-
-  // ---- A pieces p = w + 4i: rows 16p + (l >> 2), source chunk (l & 3) ^ ((l >> 4) & 3)
-  const int lch = (lane & 3) ^ ((lane >> 4) & 3);
-  int hb[NA], wb[NA], base[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const long long t = m0 + 16 * (w + 4 * i) + (lane >> 2);
-    if (t < a.M) {
-      int q, bb, n, aa;
-      divmod((int)t, a.TB, a.inv_TB, q, bb);
-      divmod(q, a.TA, a.inv_TA, n, aa);
-      hb[i] = aa * a.ist - a.ipad;
-      wb[i] = bb * a.ist - a.ipad;
-      base[i] = ((n * a.IH + hb[i]) * a.IW + wb[i]) * a.C + lch * 8;
-    } else {
-      hb[i] = -(1 << 20);  // fails every bounds check
-      wb[i] = 0;
-      base[i] = 0;
-    }
-  }
-  // ---- B pieces p = w + 4i: wave column block i, physical row 16w + t ↔ column 64i + 4t + w
-  unsigned voffB[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int col = n0 + 64 * i + 4 * (lane >> 2) + w;
-    voffB[i] = (unsigned)((col * a.ldb + lch * 8) * 2);
-  }
-  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
-  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem + (unsigned)(w * 1024);
-  const int CC = a.C / BK;
-  const int nk = a.ntaps * CC;
-
-  auto issue = [&](int kt, int stage) {
-    const int tap = kt / CC, cc = kt - tap * CC;
-    const int dh = a.dh[tap], dw = a.dw[tap];
-    const int coff = (dh * a.IW + dw) * a.C + cc * BK;
-    const unsigned sb = lds0 + (unsigned)(stage * STAGE);
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int hi = hb[i] + dh, wi = wb[i] + dw;
-      const bool ok = (unsigned)hi < (unsigned)a.IH && (unsigned)wi < (unsigned)a.IW;
-      bufld(ok ? (unsigned)((base[i] + coff) * 2) : OOB, rsX, sb + (unsigned)(4096 * i));
-    }
-    const bf16* bsrc = a.w + a.bcol[tap] + cc * BK;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) glds(voffB[i], bsrc, sb + (unsigned)(SA + 4096 * i));
-  };
-
-  // ---- fragments: row (l & 15) of a 16-row block, k chunk (l >> 4), swizzled
-  const int pch = (lane >> 4) ^ ((lane >> 2) & 3);
-  const int oA = (wm * RW + (lane & 15)) * 64 + pch * 16;
-  const int oB = SA + (wn * 64 + (lane & 15)) * 64 + pch * 16;
-
-  f32x4 acc[MI][4];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int j = 0; j < NSG - 1; ++j)
-    if (j < nk) issue(j, j);
-  int sg = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    // step kt landed: the steps issued after it (≤ NSG − 2) may still fly
-    const int after = nk - 1 - kt < NSG - 2 ? nk - 1 - kt : NSG - 2;
-    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // ... for every wave; every wave's reads of step kt - 1 are done
-    if (kt + NSG - 1 < nk) issue(kt + NSG - 1, sg == 0 ? NSG - 1 : sg - 1);  // into step kt - 1's stage
-    const char* st = smem + sg * STAGE;
-    bf16x8 fa[MI], fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + oB + j * 1024);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + oA + i * 1024);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    sg = sg == NSG - 1 ? 0 : sg + 1;
-  }
-  // the epilogue reuses the LDS for its tile sums: every wave's last reads first
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  conv_epilogue<MI, BM, BN, WM>(a, acc, smem, wm, wn, lane, m0, tm, n0);
-}
-
 // Wᵀ for the input gradient: w [K][T][C] → wt [C][T][K] (T = R·S taps), bf16
 __global__ __launch_bounds__(256) void conv_wt_kernel(const bf16* __restrict__ w, bf16* __restrict__ wt, int K, int T,
                                                       int C) {
@@ -687,26 +565,9 @@ int launch_igemm(const ConvArgs& a, hipStream_t st) {
   return 0;
 }
 
-// PDO_CONV_IMPL: 1 = mainloop 1 (128 × 128 / 256 × 64, BK 64), 2 = mainloop 2
-int g_conv_impl = [] {
-  const char* e = getenv("PDO_CONV_IMPL");
-  return e && *e ? atoi(e) : 1;
-}();
-
 int run_igemm(ConvArgs& a, hipStream_t st, int* tile_rows) {
   a.inv_TA = 1.f / (float)a.TA;
   a.inv_TB = 1.f / (float)a.TB;
-  if (g_conv_impl >= 2) {
-    // 2: 128 × 128 (4 stages); 3: 256 × 128 (3 stages); Kout = 64: 256 × 64 (4 stages)
-    const int bm = (a.Kout == 64 || g_conv_impl == 3) ? 256 : 128;
-    if (tile_rows) *tile_rows = bm;
-    const long long tiles = ((a.M + bm - 1) / bm) * (a.Kout / (a.Kout == 64 ? 64 : 128));
-    if (tiles > 0x7fffffffLL) return -2;
-    if (a.Kout == 64) conv_igemm2_kernel<256, 64><<<(unsigned)tiles, CNT, 0, st>>>(a);
-    else if (bm == 256) conv_igemm2_kernel<256, 128><<<(unsigned)tiles, CNT, 0, st>>>(a);
-    else conv_igemm2_kernel<128, 128><<<(unsigned)tiles, CNT, 0, st>>>(a);
-    return 0;
-  }
   if (a.Kout == 64) {
     if (tile_rows) *tile_rows = 256;
     return launch_igemm<256, 64>(a, st);
@@ -732,15 +593,10 @@ int conv_supported(int N, int H, int W, int C, int Kout, int R, int S, int strid
   return yb < (1ll << 31);
 }
 
-int conv_fwd_tile_rows(int Kout) { return (g_conv_impl == 3 || Kout == 64) ? 256 : 128; }
+int conv_fwd_tile_rows(int Kout) { return Kout == 64 ? 256 : 128; }
 int conv_fwd_tiles(long long M, int Kout) {
   const int r = conv_fwd_tile_rows(Kout);
   return (int)((M + r - 1) / r);
-}
-int conv_impl(int impl) {
-  const int prev = g_conv_impl;
-  if (impl >= 1 && impl <= 3) g_conv_impl = impl;
-  return prev;
 }
 
 int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int Kout, int R, int S, int stride, int pad,

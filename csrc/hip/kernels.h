@@ -55,8 +55,6 @@ struct ConvBnBwd {
   float* part;
   int relu;
 };
-// implicit-GEMM mainloop selection (1 or 2; anything else only reads); returns the previous one
-int conv_impl(int impl);
 int conv_dgrad_tiles(int N, int H, int W, int C, int R, int stride, int pad);
 int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
                     int pad, bf16* dx, hipStream_t st, const ConvBnBwd* bn = nullptr, const bf16* add = nullptr);

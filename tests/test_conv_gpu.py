@@ -16,17 +16,6 @@ def hip():
     return _native.require_hip()
 
 
-@pytest.fixture(params=[1, 2, 3], autouse=True)
-def conv_mainloop(request):
-    """Every test on each implicit-GEMM mainloop (conv.hip: 1 = 128 × 128 / BK 64 /
-    2 stages, 2 = 128 × 128 / BK 32 / 4 stages, 3 = 256 × 128 / BK 32 / 3 stages)."""
-    from paddle_operator_amd import _native
-    m = _native.require_hip()
-    prev = m.conv_impl(request.param)
-    yield request.param
-    m.conv_impl(prev)
-
-
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 

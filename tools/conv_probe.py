@@ -71,18 +71,6 @@ def main():
             "miopen_wgrad": lambda: cb(dy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
                                        [False, True, False]),
         }
-        if hasattr(m, "conv_impl"):  # mainloop 2 (256-row tiles, 3-stage ring)
-            def on(impl, fn):
-                def run():
-                    prev = m.conv_impl(impl)
-                    try:
-                        return fn()
-                    finally:
-                        m.conv_impl(prev)
-                return run
-            for impl in (2, 3):
-                cand[f"hip{impl}_fwd"] = on(impl, cand["hip_fwd"])
-                cand[f"hip{impl}_dgrad"] = on(impl, cand["hip_dgrad"])
         if R == 1 and st == 1:
             T = N * H * H
             x2, dy2, w2 = x.permute(0, 2, 3, 1).reshape(T, C), dy.permute(0, 2, 3, 1).reshape(T, K), w.view(K, C)
