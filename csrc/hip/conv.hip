@@ -764,8 +764,31 @@ static void wgrad_cfg(int Kout, int C, int T, long long M, int* bmw, int* bnw, i
   *splits = (int)sp;
 }
 
+// the weight gradient on gemm_dw4's 256 × 256 mainloop (B gathered per tap) where
+// its contract holds: ≥ 128 output channels, R·S·C % 256 = 0 (PDO_WGRAD_DW4=0: off)
+static int g_wgrad_dw4 = [] {
+  const char* e = getenv("PDO_WGRAD_DW4");
+  return e && *e ? atoi(e) : 1;
+}();
+static int wgrad_dw4_splits(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
+  if (!g_wgrad_dw4 || Kout % 128 || (R * S * C) % 256 || C % 8) return 0;
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const long long M = (long long)N * Ho * Wo;
+  if (M % 128 || M >= (1LL << 31) || (long long)N * H * W * C * 2 >= (1LL << 31)) return 0;
+  const int sp = conv_wgrad_dw4_splits(Kout, R * S * C, M);
+  return (M / 128) / sp >= 2 ? sp : 0;
+}
+
+int conv_wgrad_mode(int mode) {
+  const int prev = g_wgrad_dw4;
+  if (mode >= 0) g_wgrad_dw4 = mode;
+  return prev;
+}
+
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const int sp4 = wgrad_dw4_splits(N, H, W, C, Kout, R, S, stride, pad);
+  if (sp4) return (long long)sp4 * Kout * R * S * C;
   int bm, bn, sp;
   wgrad_cfg(Kout, C, R * S, (long long)N * Ho * Wo, &bm, &bn, &sp);
   return (long long)sp * Kout * R * S * C;
@@ -775,6 +798,19 @@ long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R,
 int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st) {
   if (!conv_supported(N, H, W, C, Kout, R, S, stride, pad)) return -2;
+  const int sp4 = wgrad_dw4_splits(N, H, W, C, Kout, R, S, stride, pad);
+  if (sp4) {
+    const int rc = conv_wgrad_dw4(dy, x, N, H, W, C, Kout, R, S, stride, pad, scratch, sp4, st);
+    if (rc) return rc;
+    const long long n4 = (long long)Kout * R * S * C / 4;
+    if (sp4 >= 16 && n4 < 1024LL * 64)
+      conv_wgrad_reduce_kernel<16><<<(unsigned)((n4 + 15) / 16), 256, 0, st>>>(scratch, sp4, n4, dw, accumulate);
+    else if (sp4 >= 4)
+      conv_wgrad_reduce_kernel<4><<<(unsigned)((n4 + 63) / 64), 256, 0, st>>>(scratch, sp4, n4, dw, accumulate);
+    else
+      conv_wgrad_reduce_kernel<1><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(scratch, sp4, n4, dw, accumulate);
+    return 0;
+  }
   WgradArgs a{};
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   a.dy = dy;

@@ -296,10 +296,44 @@ __device__ __forceinline__ bf16x8 frag16(const bf16* T) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// GATHER (the convolution weight gradient, conv.hip's conv_wgrad): B is not a
+// token-major matrix but the NHWC activation gathered per tap — column
+// tap·C + ci of token t is x[pixel(t, tap)][ci], zero for a padding pixel (a
+// buffer_load … lds whose offset is pushed past the buffer) — and the output
+// is fp32 partials [split][M][N] (folded by conv_wgrad_reduce in split order).
+struct DwGather {
+  const bf16* x;
+  unsigned xbytes;
+  int C, S, IH, IW, TA, TB;  // forward output grid: token t = (n·TA + ho)·TB + wo
+  float inv_TA, inv_TB;
+  int st, pad;
+  float* part;
+};
+
+__device__ __forceinline__ void bufld_lds(unsigned voff, __amdgpu_buffer_rsrc_t rs, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "s"(lds_byte)
+               : "memory");
+}
+
+__device__ __forceinline__ void divmodf(int x, int d, float inv, int& q, int& r) {
+  q = (int)((float)x * inv);
+  r = x - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  } else if (r >= d) {
+    ++q;
+    r -= d;
+  }
+}
+
+template <bool GATHER>
 __global__ __launch_bounds__(NTHR, 1) void gemm_dw4m16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                               int lda, int ldb, int M, int N, int ksteps_total,
                                                               int splits, bf16* __restrict__ C, int ldc,
-                                                              long long split_stride, int accumulate) {
+                                                              long long split_stride, int accumulate,
+                                                              const DwGather gx) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TILE];  // [buf][A|B][BK][256]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -332,7 +366,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4m16_kernel(const bf16* __rest
     voffB[par] = (unsigned)((rl * ldb + cs * 8) * 2);
   }
   const bf16* baseA = A + ((size_t)k0 * BK + 2 * w) * lda + m0;
-  const bf16* baseB = B + ((size_t)k0 * BK + 2 * w) * ldb + n0;
+  const bf16* baseB = GATHER ? A : B + ((size_t)k0 * BK + 2 * w) * ldb + n0;
   const unsigned stepAb = (unsigned)(16 * lda), stepBb = (unsigned)(16 * ldb);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) bf16*)smem + (unsigned)(w * 1024);
   auto glds = [](unsigned voff, const bf16* sbase, unsigned lds_byte) {
@@ -341,22 +375,51 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4m16_kernel(const bf16* __rest
                  : "v"(voff), "s"(sbase), "s"(lds_byte)
                  : "memory");
   };
+  // GATHER: per parity, the lane's column chunk → (tap row / column offset, channel)
+  int gdh[2] = {0, 0}, gdw[2] = {0, 0}, gci[2] = {0, 0};
+  const __amdgpu_buffer_rsrc_t rsX =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(GATHER ? gx.x : A), 0, GATHER ? (int)gx.xbytes : 0, 0x00020000);
+  if constexpr (GATHER) {
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int col = n0 + (((lane & 31) ^ swz16(8 * par + rw)) << 3);
+      const int tap = col / gx.C, r = tap / gx.S;
+      gci[par] = col - tap * gx.C;
+      gdh[par] = r - gx.pad;
+      gdw[par] = tap - r * gx.S - gx.pad;
+    }
+  }
   struct Src {
     const char* a;
     const char* b;
     unsigned sa, sb;
+    int kt;
   };
   auto srcs = [&](int kt) {
     Src r{reinterpret_cast<const char*>(baseA + (size_t)kt * BK * lda),
-          reinterpret_cast<const char*>(baseB + (size_t)kt * BK * ldb), stepAb, stepBb};
+          reinterpret_cast<const char*>(baseB + (GATHER ? 0 : (size_t)kt * BK * ldb)), stepAb, stepBb, kt};
     asm volatile("" : "+s"(r.a), "+s"(r.b), "+s"(r.sa), "+s"(r.sb));
     return r;
   };
   auto dma = [&](const Src& sr, auto buf_tag, int p) {  // p < 8: A piece p, else B piece p - 8
     constexpr int BUF = decltype(buf_tag)::value;
     const unsigned base = lds0 + (unsigned)(BUF * 2 * OPB);
-    if (p < 8) glds(voffA[p & 1], reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
-    else glds(voffB[p & 1], reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+    if (p < 8) {
+      glds(voffA[p & 1], reinterpret_cast<const bf16*>(sr.a + p * sr.sa), base + (unsigned)(4096 * p));
+    } else if constexpr (GATHER) {
+      // B piece p - 8: token rows 8(p - 8) + 2w + rl of k-tile k0 + kt
+      const int t = (k0 + sr.kt) * BK + 8 * (p - 8) + rw;
+      int q, wo, n, ho;
+      divmodf(t, gx.TB, gx.inv_TB, q, wo);
+      divmodf(q, gx.TA, gx.inv_TA, n, ho);
+      const int hi = ho * gx.st + gdh[p & 1], wi = wo * gx.st + gdw[p & 1];
+      const unsigned off = ((unsigned)hi < (unsigned)gx.IH && (unsigned)wi < (unsigned)gx.IW)
+                               ? (unsigned)((((n * gx.IH + hi) * gx.IW + wi) * gx.C + gci[p & 1]) * 2)
+                               : 0x80000000u;
+      bufld_lds(off, rsX, base + OPB + (unsigned)(4096 * (p - 8)));
+    } else {
+      glds(voffB[p & 1], reinterpret_cast<const bf16*>(sr.b + (p - 8) * sr.sb), base + OPB + (unsigned)(4096 * (p - 8)));
+    }
   };
 
   // fragment slot q (0..15) of block h (tokens 32h .. 32h+31): q < 8 → A rows
@@ -465,6 +528,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4m16_kernel(const bf16* __rest
   bf16* Cb = C + (size_t)split * split_stride;
   const int g4 = lane >> 4, li = lane & 15;
   if (m0 + wm * 128 >= M) return;  // edge tile: wm = 1 holds rows m0 + 128 .. (wave-uniform)
+  if constexpr (GATHER) {
+    // fp32 partials of this split (ldc = N)
+    float* P = gx.part + (size_t)split * split_stride;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[r]) : "a"(acc[mb][nb][r]));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 128 + 16 * mb + 4 * g4 + r;
+          P[(size_t)m * ldc + n0 + wn * 128 + 16 * nb + li] = v[r];
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int mb = 0; mb < 8; ++mb)
 #pragma unroll
@@ -510,8 +591,46 @@ int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, i
   if (variant == 1)  // the same schedule on 32x32x16 MFMAs (A/B alternative)
     gemm_dw4_kernel<<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
   else
-    gemm_dw4m16_kernel<<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc);
+    gemm_dw4m16_kernel<false><<<grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, (int)ks, splits, out, ldo, stride, acc,
+                                                     DwGather{});
   if (splits > 1) return splitk_add(ws, splits, (long long)M * N, C, accumulate, st);
+  return 0;
+}
+
+// Convolution weight gradient on the gathered mainloop: dW [Kout][R·S·C] fp32
+// partials per token slice into part ([splits][Kout][R·S·C]); the caller folds
+// them.  Contract: Kout % 128 = 0, (R·S·C) % 256 = 0, C % 8 = 0, tokens % 128 = 0
+// with ≥ 4 64-token k-tiles per slice (pairs dealt out).
+int conv_wgrad_dw4_splits(int Kout, int TC, long long M) {
+  const long long tiles = (long long)((Kout + 255) / 256) * (TC / 256);
+  const long long pairs = M / 128;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  // one workgroup per CU (128 KiB of LDS each) and no second round: ⌊CUs / tiles⌋
+  long long sp = ncu / tiles;
+  if (sp > pairs / 2) sp = pairs / 2;
+  if (sp > 256) sp = 256;
+  return sp < 1 ? 1 : (int)sp;
+}
+
+int conv_wgrad_dw4(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
+                   int pad, float* part, int splits, hipStream_t st) {
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  const long long M = (long long)N * Ho * Wo;
+  const int TC = R * S * C;
+  if (Kout % (BM / 2) || TC % BN || C % 8 || M % (2 * BK) || M >= (1LL << 31)) return -2;
+  const long long ks = M / BK;
+  if (splits < 1 || (ks / 2) / splits < 2) return -2;
+  if ((long long)N * H * W * C * 2 >= (1LL << 31)) return -2;
+  DwGather g{x, (unsigned)((long long)N * H * W * C * 2), C, S, H, W, Ho, Wo, 1.f / (float)Ho, 1.f / (float)Wo,
+             stride, pad, part};
+  const int grid = ((Kout + BM - 1) / BM) * (TC / BN) * splits;
+  gemm_dw4m16_kernel<true><<<grid, NTHR, 0, st>>>(dy, nullptr, Kout, 0, Kout, TC, (int)ks, splits, nullptr, TC,
+                                                  (long long)Kout * TC, 0, g);
   return 0;
 }
 

@@ -55,6 +55,12 @@ struct ConvBnBwd {
   float* part;
   int relu;
 };
+// convolution weight gradient on gemm_dw4's mainloop with the activation gathered per tap (gemm_dw4.hip)
+int conv_wgrad_dw4_splits(int Kout, int TC, long long M);
+// PDO_WGRAD_DW4 routing (1 on, 0 off; < 0 only reads); returns the previous mode
+int conv_wgrad_mode(int mode);
+int conv_wgrad_dw4(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
+                   int pad, float* part, int splits, hipStream_t st);
 int conv_dgrad_tiles(int N, int H, int W, int C, int R, int stride, int pad);
 int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
                     int pad, bf16* dx, hipStream_t st, const ConvBnBwd* bn = nullptr, const bf16* add = nullptr);

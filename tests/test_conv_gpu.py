@@ -217,3 +217,29 @@ def test_bottleneck_bn_link_matches_unlinked():
     assert _rel(outs[0], outs[1]) < 1e-2
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert _rel(pa.grad, pb.grad) < 1e-2, n
+
+
+@pytest.mark.parametrize("N,C,H,K,R,stride", [(4, 256, 16, 256, 3, 1), (8, 256, 16, 512, 3, 2), (4, 512, 8, 512, 3, 1),
+                                              (8, 256, 16, 128, 1, 1), (16, 256, 8, 512, 1, 2), (4, 1024, 8, 256, 1, 1)])
+def test_conv_wgrad_dw4_gathered(hip, N, C, H, K, R, stride):
+    """The weight gradient on gemm_dw4's 256 × 256 mainloop with the activation
+    gathered per tap (zero padding through out-of-range buffer offsets; Kout = 128:
+    half-height tiles) against fp32 autograd and against the 128 × 128 kernel."""
+    x, w = _mk(N, C, H, K, R, 9)
+    pad = (R - 1) // 2
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, stride=stride, padding=pad)
+    g = torch.Generator(device="cuda").manual_seed(10)
+    dy = torch.randn(ref.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    ref.backward(dy.float())
+    assert (dy.numel() // K) % 128 == 0  # the shapes take the gathered path
+    prev = hip.conv_wgrad_mode(1)
+    try:
+        dw4 = hip.conv_wgrad(dy, x, R, R, stride, pad)
+        hip.conv_wgrad_mode(0)
+        dw1 = hip.conv_wgrad(dy, x, R, R, stride, pad)
+    finally:
+        hip.conv_wgrad_mode(prev)
+    assert dw4.shape == w.shape and dw4.dtype == torch.float32
+    assert _rel(dw4, wf.grad) < 5e-3
+    assert _rel(dw4, dw1) < 1e-4

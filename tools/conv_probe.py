@@ -71,6 +71,14 @@ def main():
             "miopen_wgrad": lambda: cb(dy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
                                        [False, True, False]),
         }
+        if hasattr(m, "conv_wgrad_mode"):  # the 128 × 128 wgrad kernel where the gathered dw4 path would run
+            def wg1():
+                prev = m.conv_wgrad_mode(0)
+                try:
+                    return m.conv_wgrad(dy, x, R, R, st, pad)
+                finally:
+                    m.conv_wgrad_mode(prev)
+            cand["hip1_wgrad"] = wg1
         if R == 1 and st == 1:
             T = N * H * H
             x2, dy2, w2 = x.permute(0, 2, 3, 1).reshape(T, C), dy.permute(0, 2, 3, 1).reshape(T, K), w.view(K, C)
