@@ -534,18 +534,21 @@ __global__ __launch_bounds__(CNT, 2) void conv_wgrad_kernel(const WgradArgs a) {
 // the G group sums join in order through LDS — deterministic, and G-way
 // parallel over the splits (a 64 × 64 1×1 weight has 1 024 f32x4 outputs but
 // up to 256 splits: one lane per output would walk all of them serially).
+// part rows may be padded: output f32x4 i = row i / cols4, column i % cols4 reads
+// part f32x4 (i / cols4)·ldp4 + i % cols4 of each split (pn4 f32x4 per split)
 template <int G>
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, int splits,
                                                                 long long n4, float* __restrict__ out,
-                                                                int accumulate) {
+                                                                int accumulate, int cols4, int ldp4, long long pn4) {
   constexpr int OB = 256 / G;
   __shared__ f32x4 red[G][OB];
   const int o = threadIdx.x % OB, g = threadIdx.x / OB;
   const long long i = (long long)blockIdx.x * OB + o;
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (i < n4) {
+    const long long row = i / cols4, src = row * ldp4 + (i - row * cols4);
 #pragma unroll 4
-    for (int k = g; k < splits; k += G) v += reinterpret_cast<const f32x4*>(part)[(long long)k * n4 + i];
+    for (int k = g; k < splits; k += G) v += reinterpret_cast<const f32x4*>(part)[(long long)k * pn4 + src];
   }
   red[g][o] = v;
   __syncthreads();
@@ -764,6 +767,19 @@ static void wgrad_cfg(int Kout, int C, int T, long long M, int* bmw, int* bnw, i
   *splits = (int)sp;
 }
 
+// split fold of the weight-gradient partials ([splits][rows][ldp] fp32, rows × cols outputs)
+static void wgrad_fold(const float* part, int splits, int rows, int cols, int ldp, float* dw, int accumulate,
+                       hipStream_t st) {
+  const long long n4 = (long long)rows * cols / 4, pn4 = (long long)rows * ldp / 4;
+  const int c4 = cols / 4, l4 = ldp / 4;
+  if (splits >= 16 && n4 < 1024LL * 64)
+    conv_wgrad_reduce_kernel<16><<<(unsigned)((n4 + 15) / 16), 256, 0, st>>>(part, splits, n4, dw, accumulate, c4, l4, pn4);
+  else if (splits >= 4)
+    conv_wgrad_reduce_kernel<4><<<(unsigned)((n4 + 63) / 64), 256, 0, st>>>(part, splits, n4, dw, accumulate, c4, l4, pn4);
+  else
+    conv_wgrad_reduce_kernel<1><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(part, splits, n4, dw, accumulate, c4, l4, pn4);
+}
+
 // the weight gradient on gemm_dw4's 256 × 256 mainloop (B gathered per tap) where
 // its contract holds: ≥ 128 output channels, R·S·C % 256 = 0 (PDO_WGRAD_DW4=0: off)
 static int g_wgrad_dw4 = [] {
@@ -771,7 +787,8 @@ static int g_wgrad_dw4 = [] {
   return e && *e ? atoi(e) : 1;
 }();
 static int wgrad_dw4_splits(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
-  if (!g_wgrad_dw4 || Kout % 128 || (R * S * C) % 256 || C % 8) return 0;
+  // (R·S·C) % 128: at most half of the last 256-column tile is padding
+  if (!g_wgrad_dw4 || Kout % 128 || (R * S * C) % 128 || C % 8) return 0;
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const long long M = (long long)N * Ho * Wo;
   if (M % 128 || M >= (1LL << 31) || (long long)N * H * W * C * 2 >= (1LL << 31)) return 0;
@@ -788,7 +805,7 @@ int conv_wgrad_mode(int mode) {
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const int sp4 = wgrad_dw4_splits(N, H, W, C, Kout, R, S, stride, pad);
-  if (sp4) return (long long)sp4 * Kout * R * S * C;
+  if (sp4) return (long long)sp4 * Kout * ((R * S * C + 255) / 256 * 256);
   int bm, bn, sp;
   wgrad_cfg(Kout, C, R * S, (long long)N * Ho * Wo, &bm, &bn, &sp);
   return (long long)sp * Kout * R * S * C;
@@ -802,13 +819,8 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
   if (sp4) {
     const int rc = conv_wgrad_dw4(dy, x, N, H, W, C, Kout, R, S, stride, pad, scratch, sp4, st);
     if (rc) return rc;
-    const long long n4 = (long long)Kout * R * S * C / 4;
-    if (sp4 >= 16 && n4 < 1024LL * 64)
-      conv_wgrad_reduce_kernel<16><<<(unsigned)((n4 + 15) / 16), 256, 0, st>>>(scratch, sp4, n4, dw, accumulate);
-    else if (sp4 >= 4)
-      conv_wgrad_reduce_kernel<4><<<(unsigned)((n4 + 63) / 64), 256, 0, st>>>(scratch, sp4, n4, dw, accumulate);
-    else
-      conv_wgrad_reduce_kernel<1><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(scratch, sp4, n4, dw, accumulate);
+    const int TC = R * S * C;
+    wgrad_fold(scratch, sp4, Kout, TC, (TC + 255) / 256 * 256, dw, accumulate, st);
     return 0;
   }
   WgradArgs a{};
@@ -840,14 +852,7 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
   else if (bm == 128) conv_wgrad_kernel<128, 64><<<(unsigned)grid, CNT, 0, st>>>(a);
   else if (bn == 128) conv_wgrad_kernel<64, 128><<<(unsigned)grid, CNT, 0, st>>>(a);
   else conv_wgrad_kernel<64, 64><<<(unsigned)grid, CNT, 0, st>>>(a);
-  const long long n4 = (long long)Kout * a.T * C / 4;
-  // split-group width: ≥ 1 024 blocks where the outputs allow, ≤ the split count
-  if (a.splits >= 16 && n4 < 1024LL * 64)
-    conv_wgrad_reduce_kernel<16><<<(unsigned)((n4 + 15) / 16), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
-  else if (a.splits >= 4)
-    conv_wgrad_reduce_kernel<4><<<(unsigned)((n4 + 63) / 64), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
-  else
-    conv_wgrad_reduce_kernel<1><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(scratch, a.splits, n4, dw, accumulate);
+  wgrad_fold(scratch, a.splits, Kout, a.T * C, a.T * C, dw, accumulate, st);
   return 0;
 }
 

@@ -305,6 +305,7 @@ struct DwGather {
   const bf16* x;
   unsigned xbytes;
   int C, S, IH, IW, TA, TB;  // forward output grid: token t = (n·TA + ho)·TB + wo
+  int TC;                    // R·S·C: columns past it (padding to the 256-column tile) read zeros
   float inv_TA, inv_TB;
   int st, pad;
   float* part;
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_dw4m16_kernel(const bf16* __rest
       const int col = n0 + (((lane & 31) ^ swz16(8 * par + rw)) << 3);
       const int tap = col / gx.C, r = tap / gx.S;
       gci[par] = col - tap * gx.C;
-      gdh[par] = r - gx.pad;
+      gdh[par] = col < gx.TC ? r - gx.pad : -(1 << 20);  // a padding column fails every bounds check
       gdw[par] = tap - r * gx.S - gx.pad;
     }
   }
@@ -598,11 +599,11 @@ int gemm_dw4(const bf16* A, const bf16* B, long long T, int M, int N, int lda, i
 }
 
 // Convolution weight gradient on the gathered mainloop: dW [Kout][R·S·C] fp32
-// partials per token slice into part ([splits][Kout][R·S·C]); the caller folds
-// them.  Contract: Kout % 128 = 0, (R·S·C) % 256 = 0, C % 8 = 0, tokens % 128 = 0
-// with ≥ 4 64-token k-tiles per slice (pairs dealt out).
+// partials per token slice into part ([splits][Kout][TCp], TCp = R·S·C rounded up
+// to 256 columns); the caller folds them.  Contract: Kout % 128 = 0, C % 8 = 0,
+// tokens % 128 = 0 with ≥ 4 64-token k-tiles per slice (pairs dealt out).
 int conv_wgrad_dw4_splits(int Kout, int TC, long long M) {
-  const long long tiles = (long long)((Kout + 255) / 256) * (TC / 256);
+  const long long tiles = (long long)((Kout + 255) / 256) * ((TC + 255) / 256);
   const long long pairs = M / 128;
   static const int ncu = [] {
     int dev = 0, n = 0;
@@ -621,16 +622,16 @@ int conv_wgrad_dw4(const bf16* dy, const bf16* x, int N, int H, int W, int C, in
                    int pad, float* part, int splits, hipStream_t st) {
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const long long M = (long long)N * Ho * Wo;
-  const int TC = R * S * C;
-  if (Kout % (BM / 2) || TC % BN || C % 8 || M % (2 * BK) || M >= (1LL << 31)) return -2;
+  const int TC = R * S * C, TCp = (TC + BN - 1) / BN * BN;
+  if (Kout % (BM / 2) || C % 8 || M % (2 * BK) || M >= (1LL << 31)) return -2;
   const long long ks = M / BK;
   if (splits < 1 || (ks / 2) / splits < 2) return -2;
   if ((long long)N * H * W * C * 2 >= (1LL << 31)) return -2;
-  DwGather g{x, (unsigned)((long long)N * H * W * C * 2), C, S, H, W, Ho, Wo, 1.f / (float)Ho, 1.f / (float)Wo,
+  DwGather g{x, (unsigned)((long long)N * H * W * C * 2), C, S, H, W, Ho, Wo, TC, 1.f / (float)Ho, 1.f / (float)Wo,
              stride, pad, part};
-  const int grid = ((Kout + BM - 1) / BM) * (TC / BN) * splits;
-  gemm_dw4m16_kernel<true><<<grid, NTHR, 0, st>>>(dy, nullptr, Kout, 0, Kout, TC, (int)ks, splits, nullptr, TC,
-                                                  (long long)Kout * TC, 0, g);
+  const int grid = ((Kout + BM - 1) / BM) * (TCp / BN) * splits;
+  gemm_dw4m16_kernel<true><<<grid, NTHR, 0, st>>>(dy, nullptr, Kout, 0, Kout, TCp, (int)ks, splits, nullptr, TCp,
+                                                  (long long)Kout * TCp, 0, g);
   return 0;
 }
 

@@ -220,11 +220,13 @@ def test_bottleneck_bn_link_matches_unlinked():
 
 
 @pytest.mark.parametrize("N,C,H,K,R,stride", [(4, 256, 16, 256, 3, 1), (8, 256, 16, 512, 3, 2), (4, 512, 8, 512, 3, 1),
-                                              (8, 256, 16, 128, 1, 1), (16, 256, 8, 512, 1, 2), (4, 1024, 8, 256, 1, 1)])
+                                              (8, 256, 16, 128, 1, 1), (16, 256, 8, 512, 1, 2), (4, 1024, 8, 256, 1, 1),
+                                              (8, 128, 16, 128, 3, 1), (8, 128, 16, 512, 1, 1)])
 def test_conv_wgrad_dw4_gathered(hip, N, C, H, K, R, stride):
     """The weight gradient on gemm_dw4's 256 × 256 mainloop with the activation
     gathered per tap (zero padding through out-of-range buffer offsets; Kout = 128:
-    half-height tiles) against fp32 autograd and against the 128 × 128 kernel."""
+    half-height tiles; R·S·C = 1152 / 128: a zero-padded last 256-column tile)
+    against fp32 autograd and against the 128 × 128 kernel."""
     x, w = _mk(N, C, H, K, R, 9)
     pad = (R - 1) // 2
     wf = w.float().requires_grad_()
