@@ -787,8 +787,11 @@ static int g_wgrad_dw4 = [] {
   return e && *e ? atoi(e) : 1;
 }();
 static int wgrad_dw4_splits(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
-  // (R·S·C) % 128: at most half of the last 256-column tile is padding
+  // (R·S·C) % 128: at most half of the last 256-column tile is padding.  A 1×1
+  // stride-1 product with half-height or half-padded tiles stays on the 128 × 128
+  // kernel (measured faster there: profiles/r4i_conv_probe.jsonl)
   if (!g_wgrad_dw4 || Kout % 128 || (R * S * C) % 128 || C % 8) return 0;
+  if (R == 1 && stride == 1 && (Kout % 256 || C % 256)) return 0;
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const long long M = (long long)N * Ho * Wo;
   if (M % 128 || M >= (1LL << 31) || (long long)N * H * W * C * 2 >= (1LL << 31)) return 0;
