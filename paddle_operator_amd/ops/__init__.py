@@ -993,7 +993,12 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad, want_stats, fork=False):
         m = _native.require_hip()
-        wb = w.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        sh = getattr(w, "_pdo_shadow", None)  # the arena's bf16 copy, cast once per step (FlatParams.shadow_scope)
+        if sh is not None and sh[0].shadow_live and sh[1].dtype == torch.bfloat16 \
+                and sh[1].is_contiguous(memory_format=torch.channels_last):
+            wb = sh[1]
+        else:
+            wb = w.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         K, C, R, _ = wb.shape
         N, _, H, W_ = x.shape
         ctx.one = R == 1 and stride == 1

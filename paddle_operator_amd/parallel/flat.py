@@ -149,6 +149,32 @@ class FlatParams:
         self.decay_chunks = wd.to(device)
         self.buckets = self._make_buckets(bucket_bytes)
 
+    def enable_shadow(self, dtype=torch.bfloat16):
+        """A low-precision copy of the whole arena for the compute kernels (fp32
+        master weights, bf16 operands): refreshed by ONE cast of the arena per
+        forward (shadow_scope) instead of a cast per weight per forward.  Each
+        parameter gets ``_pdo_shadow = (arena, view)``; consumers use the view only
+        while ``arena.shadow_live`` (inside shadow_scope), so a weight changed
+        outside the trainer's step is never read stale."""
+        self.shadow = torch.empty(self.numel, dtype=dtype, device=self.device)
+        self.shadow_live = False
+        for s in self.slots:
+            s.param._pdo_shadow = (self, self._view(self.shadow, s))
+
+    def shadow_scope(self):
+        flat = self
+
+        class _Scope:
+            def __enter__(self):
+                if getattr(flat, "shadow", None) is not None:
+                    flat.shadow.copy_(flat.params)
+                    flat.shadow_live = True
+
+            def __exit__(self, *exc):
+                flat.shadow_live = False
+
+        return _Scope()
+
     def _view(self, buf, s):
         seg = buf[s.offset:s.offset + s.numel]
         st = self._strides.get(s.name)

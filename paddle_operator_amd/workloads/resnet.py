@@ -11,6 +11,8 @@ for the shipped shapes.
 """
 from __future__ import annotations
 
+import os
+
 from ..utils.tuning import use_shipped_miopen_db
 
 use_shipped_miopen_db()
@@ -69,6 +71,8 @@ class ResNetTrainer:
             model = model.to(memory_format=torch.channels_last)
         self.model = model
         self.flat = FlatParams(model, dtype=torch.float32, device=self.device, bucket_bytes=bucket_mb << 20)
+        if self.device.type == "cuda" and os.environ.get("PDO_WEIGHT_SHADOW", "1") != "0":
+            self.flat.enable_shadow(torch.bfloat16)
         self.ddp = BucketedDDP(self.flat)
         self.opt = FlatSGD(self.flat)
         self.res = 32 if tiny else 224
@@ -91,7 +95,9 @@ class ResNetTrainer:
         x, y = self.batch()
         self.flat.zero_grad()
         self.ddp.prepare()
-        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.device.type == "cuda"):
+        # bf16 copies of the fp32 master weights: one cast of the arena per step
+        with self.flat.shadow_scope(), torch.autocast(self.device.type, dtype=torch.bfloat16,
+                                                      enabled=self.device.type == "cuda"):
             out = self.model(x)
         loss = F.cross_entropy(out.float(), y)
         loss.backward()
