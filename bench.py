@@ -108,6 +108,9 @@ def parse_args(argv=None):
                          "one-pod = 1 pod × N amd.com/gpu running --nproc-per-pod N local ranks (the Kubernetes "
                          "xGMI layout: under a device plugin only GPUs of one pod see each other)")
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
+    ap.add_argument("--secondary-resnet", type=int, default=int(os.environ.get("PDO_BENCH_RESNET", "1")),
+                    help="after the GPT-2 job (GPUs only): a ResNet-50 job (configs 2/3, batch 256 per GPU, 20 timed "
+                         "steps) on the same ranks, reported under 'secondary' (0: skip)")
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
     ap.add_argument("--ready-only", action="store_true", help="only the ready trials (prints their record)")
@@ -367,6 +370,18 @@ def orchestrate(a):
             L.finish(name)
             out["bench"] = rs
             out["bench_ready_s"] = max(r["t_ready"] for r in rs) - t0
+            if a.workload == "gpt2" and a.secondary_resnet and gpus and a.ops == "hip":
+                # the reference's own example workload (deploy/examples/resnet.yaml) in the same
+                # driver run; a failure here never costs the headline record
+                try:
+                    wl2 = ["--workload", "resnet50", "--batch", "256", "--steps", "20", "--warmup", "5", "--bench",
+                           "--timeout", "600"]
+                    L.launch("resnet50-bench", N, wl2, a.ops)
+                    out["resnet"] = L.wait_records("resnet50-bench", "bench", N, a.timeout)
+                    L.finish("resnet50-bench")
+                except Exception as e:  # noqa: BLE001
+                    out["resnet_error"] = f"{type(e).__name__}: {e}"
+                    log(f"secondary ResNet-50 job failed: {out['resnet_error']}")
         finally:
             L.stop()
         if a.compat_trials:
@@ -428,6 +443,20 @@ def orchestrate(a):
                "gpt2_job_ready_s": extra["job_ready_s"],
                "model_tflops_per_gpu": round(flops_gpu / 1e12, 1),
                "mfu_vs_2.5PF_dense": round(flops_gpu / 2.5e15, 4)}
+        if out.get("resnet"):
+            r2 = out["resnet"]
+            dt2 = max(r["seconds"] for r in r2)
+            rate2 = sum(r["tokens_per_step_rank"] for r in r2) * 20 / dt2
+            rec["secondary"] = {
+                "metric": "launched images/sec (ResNet-50 PaddleJob through the pdo operator, collective DP over RCCL)",
+                "value": round(rate2, 1), "unit": "images/s", "n_gpus": N, "steps": 20, "warmup": 5,
+                "ms_per_step": round(dt2 / 20 * 1e3, 3), "dtype": "bf16",
+                "data": "synthetic (on-device random 224x224 images and labels), random-init weights",
+                "config": {"model": "resnet50", "global_batch": 256 * N, "micro_batch_per_gpu": 256, "resolution": 224,
+                           "parallelism": f"dp{N}", "pod_layout": f"{pods}x{N // pods}"},
+                "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in r2)}
+        elif out.get("resnet_error"):
+            rec["secondary"] = {"error": out["resnet_error"]}
     else:
         rec = {"metric": "launched images/sec (ResNet-50 PaddleJob through the pdo operator, collective DP over RCCL)",
                "value": round(rate, 1), "unit": "images/s", **common,
