@@ -161,10 +161,12 @@ __global__ __launch_bounds__(FIN_THREADS) void bn_finalize_kernel(const float* _
 
 // forward apply: y = act(x·scale + shift [+ res]).  HOIST: 256 % (C/8) == 0, so
 // a lane's channel chunk never changes along the grid-stride loop.
+// mask (optional): bit j of byte i = [y[8i + j] > 0], the ReLU mask the backward
+// reads instead of y (1/16 of the bytes; relu = 2 there)
 template <bool HOIST>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                        const float* __restrict__ ss, long long n8, int C, int relu,
-                                                       bf16* __restrict__ y) {
+                                                       bf16* __restrict__ y, unsigned char* __restrict__ mask) {
   const int C8 = C / 8;
   const long long i0 = blockIdx.x * 256LL + threadIdx.x;
   const long long stride = (long long)gridDim.x * 256;
@@ -186,7 +188,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
-    reinterpret_cast<bf16x8*>(y)[i] = to_bf16(v);
+    const bf16x8 yb = to_bf16(v);
+    reinterpret_cast<bf16x8*>(y)[i] = yb;
+    if (mask) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= ((float)yb[j] > 0.f ? 1u : 0u) << j;
+      mask[i] = (unsigned char)bits;
+    }
   }
 }
 
@@ -195,7 +204,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 __device__ __forceinline__ f32x8 relu_grad(const bf16* dy, const bf16* y, const f32x8& xv, const Affine& a,
                                            long long i, int relu) {
   f32x8 g = to_f32(reinterpret_cast<const bf16x8*>(dy)[i]);
-  if (relu) {
+  if (relu == 2) {  // y is the forward's ReLU bitmask (bn_apply_kernel)
+    const unsigned bits = reinterpret_cast<const unsigned char*>(y)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = (bits >> j) & 1u ? g[j] : 0.f;
+  } else if (relu) {
     if (y) {
       const f32x8 yv = to_f32(reinterpret_cast<const bf16x8*>(y)[i]);
 #pragma unroll
@@ -414,7 +427,7 @@ int bn_fwd_scratch_floats(long long M, int C) {
 
 int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float* running_mean, float* running_var,
            long long M, int C, float eps, float momentum, int relu, bf16* y, float* mean, float* invstd,
-           float* scratch, hipStream_t st) {
+           float* scratch, hipStream_t st, unsigned char* mask) {
   if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32)) return -2;
   const int TX = pick_tx(C);
   int gx, gy;
@@ -430,8 +443,8 @@ int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float
                                              invstd, ss);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
-  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);
-  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);
+  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
+  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
   return 0;
 }
 
@@ -439,14 +452,15 @@ int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float
 // (conv.hip tile partials): finalize + apply, no statistics pass over x
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
-                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st) {
+                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st,
+                 unsigned char* mask) {
   if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1) return -2;
   bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
                                                   running_var, mean, invstd, ss);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
-  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);
-  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y);
+  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
+  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
   return 0;
 }
 

@@ -422,9 +422,13 @@ std::vector<at::Tensor> bn_act_fwd(at::Tensor x, c10::optional<at::Tensor> res, 
   }
   float* rmp = rm && rm->defined() ? fp(*rm) : nullptr;
   float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
+  // ReLU after a residual add: also the 1-bit mask the backward reads instead of y
+  at::Tensor mask;
+  if (relu && rp) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   CHECK_RC(pdo::bn_fwd(bp(x), rp, fp(w), fp(b), rmp, rvp, M, (int)C, (float)eps, (float)momentum, relu ? 1 : 0,
-                       bp(y), fp(mean), fp(invstd), fp(scratch), cur_stream()), "bn_fwd");
-  return {y, mean, invstd};
+                       bp(y), fp(mean), fp(invstd), fp(scratch), cur_stream(),
+                       mask.defined() ? mask.data_ptr<uint8_t>() : nullptr), "bn_fwd");
+  return {y, mean, invstd, mask};
 }
 
 // part: (Σg, Σg·(x − mean)) partials [G, 2, C] that came with dy (conv_dgrad_bn); else a stats pass
@@ -436,13 +440,20 @@ static std::vector<at::Tensor> bn_act_bwd_impl(at::Tensor dy, c10::optional<at::
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "bn_act_bwd: channels_last x");
   auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
   const bf16* yp = nullptr;
-  if (y && y->defined()) {
-    CHECK_BF16((*y));
-    TORCH_CHECK(y->sizes() == x.sizes() && y->is_contiguous(at::MemoryFormat::ChannelsLast));
-    yp = bp(*y);
-  }
-  TORCH_CHECK(!(relu && want_dres && !yp), "bn_act_bwd: residual + ReLU needs the saved output");
+  int rmode = relu ? 1 : 0;
   const long long C = x.size(1), M = x.numel() / C;
+  if (y && y->defined()) {
+    if (y->scalar_type() == at::kByte) {  // the forward's ReLU bitmask
+      TORCH_CHECK(relu && y->numel() == M * C / 8 && y->is_contiguous(), "bn_act_bwd: mask [M·C/8] uint8");
+      yp = reinterpret_cast<const bf16*>(y->data_ptr<uint8_t>());
+      rmode = 2;
+    } else {
+      CHECK_BF16((*y));
+      TORCH_CHECK(y->sizes() == x.sizes() && y->is_contiguous(at::MemoryFormat::ChannelsLast));
+      yp = bp(*y);
+    }
+  }
+  TORCH_CHECK(!(relu && want_dres && !yp), "bn_act_bwd: residual + ReLU needs the saved output or its mask");
   auto dx = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
@@ -464,12 +475,12 @@ static std::vector<at::Tensor> bn_act_bwd_impl(at::Tensor dy, c10::optional<at::
                 "bn_act_bwd_part: partials [G, 2, C]");
     auto coef = at::empty({3 * C}, w.options());
     CHECK_RC(pdo::bn_bwd_part(fp(*part), (int)part->size(0), bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M,
-                              (int)C, relu ? 1 : 0, bp(dx), want_dres ? bp(dres) : nullptr, fp(dw), fp(db),
+                              (int)C, rmode, bp(dx), want_dres ? bp(dres) : nullptr, fp(dw), fp(db),
                               into ? 1 : 0, fp(coef), cur_stream()),
              "bn_bwd_part");
   } else {
     auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_floats(M, C)}, w.options());
-    CHECK_RC(pdo::bn_bwd(bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M, (int)C, relu ? 1 : 0, bp(dx),
+    CHECK_RC(pdo::bn_bwd(bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M, (int)C, rmode, bp(dx),
                          want_dres ? bp(dres) : nullptr, fp(dw), fp(db), into ? 1 : 0, fp(scratch), cur_stream()),
              "bn_bwd");
   }
@@ -622,10 +633,12 @@ std::vector<at::Tensor> bn_act_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t
   }
   float* rmp = rm && rm->defined() ? fp(*rm) : nullptr;
   float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
+  at::Tensor mask;
+  if (relu && rp) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   CHECK_RC(pdo::bn_fwd_tiles(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), rp, fp(w), fp(b), rmp, rvp, M,
                              (int)C, (float)eps, (float)momentum, relu ? 1 : 0, bp(y), fp(mean), fp(invstd), fp(ss),
-                             cur_stream()), "bn_fwd_tiles");
-  return {y, mean, invstd};
+                             cur_stream(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr), "bn_fwd_tiles");
+  return {y, mean, invstd, mask};
 }
 
 // ---------------------------------------------------------------- NHWC max-pool 3×3/2

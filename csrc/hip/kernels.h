@@ -72,11 +72,11 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st);
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
-                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st);
+                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st, unsigned char* mask = nullptr);
 int bn_fwd_scratch_floats(long long M, int C);
 int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float* running_mean, float* running_var,
            long long M, int C, float eps, float momentum, int relu, bf16* y, float* mean, float* invstd,
-           float* scratch, hipStream_t st);
+           float* scratch, hipStream_t st, unsigned char* mask = nullptr);
 int bn_bwd_scratch_floats(long long M, int C);
 // y may be null: the ReLU mask is then recomputed from x (only valid without a residual)
 int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, const float* invstd, const float* w,

@@ -857,15 +857,16 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu, stats=None, tile_rows=0,
                 link=None):
         m = _native.require_hip()
+        # mask: with a residual under the ReLU, the 1-bit ReLU mask the backward reads
+        # instead of the bf16 output (1/16 of the bytes, both backward passes)
         if stats is not None:
-            y, mean, invstd = m.bn_act_fwd_tiles(x, stats, tile_rows, residual, w, b, running_mean, running_var, eps,
-                                                 momentum, relu)
+            y, mean, invstd, mask = m.bn_act_fwd_tiles(x, stats, tile_rows, residual, w, b, running_mean,
+                                                       running_var, eps, momentum, relu)
         else:
-            y, mean, invstd = m.bn_act_fwd(x, residual, w, b, running_mean, running_var, eps, momentum, relu)
+            y, mean, invstd, mask = m.bn_act_fwd(x, residual, w, b, running_mean, running_var, eps, momentum, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        keep_y = relu and ctx.has_res
-        ctx.save_for_backward(x, y if keep_y else None, mean, invstd, w, b)
+        ctx.save_for_backward(x, mask if (relu and ctx.has_res) else None, mean, invstd, w, b)
         ctx.params = (w, b)
         ctx.link = link
         if link is not None:

@@ -96,8 +96,8 @@ def test_bn_from_tile_stats_matches_stats_pass(hip):
     beta = torch.randn(64, device="cuda", generator=g) * 0.1
     rm1, rv1 = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
     rm2, rv2 = rm1.clone(), rv1.clone()
-    a, m_a, i_a = hip.bn_act_fwd(y, None, gamma, beta, rm1, rv1, 1e-5, 0.1, True)
-    b, m_b, i_b = hip.bn_act_fwd_tiles(y, st, hip.conv_tile_rows(64), None, gamma, beta, rm2, rv2, 1e-5, 0.1, True)
+    a, m_a, i_a, _ = hip.bn_act_fwd(y, None, gamma, beta, rm1, rv1, 1e-5, 0.1, True)
+    b, m_b, i_b, _ = hip.bn_act_fwd_tiles(y, st, hip.conv_tile_rows(64), None, gamma, beta, rm2, rv2, 1e-5, 0.1, True)
     torch.testing.assert_close(m_b, m_a, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(i_b, i_a, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(rv2, rv1, rtol=1e-3, atol=1e-5)
@@ -170,7 +170,7 @@ def test_conv_dgrad_bn_partials(hip, N, C, H, K, stride):
     gamma = torch.rand(C, device="cuda", generator=g) + 0.5
     beta = torch.randn(C, device="cuda", generator=g) * 0.2
     rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
-    y, mean, invstd = hip.bn_act_fwd(bx, None, gamma, beta, rm, rv, 1e-5, 0.1, True)
+    y, mean, invstd, _ = hip.bn_act_fwd(bx, None, gamma, beta, rm, rv, 1e-5, 0.1, True)
     w = (torch.randn(K, C, 3, 3, device="cuda", generator=g) / (9 * C) ** 0.5).bfloat16()
     w = w.contiguous(memory_format=torch.channels_last)
     Ho = (H + 2 - 3) // stride + 1
@@ -245,3 +245,23 @@ def test_conv_wgrad_dw4_gathered(hip, N, C, H, K, R, stride):
     assert dw4.shape == w.shape and dw4.dtype == torch.float32
     assert _rel(dw4, wf.grad) < 5e-3
     assert _rel(dw4, dw1) < 1e-4
+
+
+def test_bn_residual_relu_mask_matches_saved_output(hip):
+    """BatchNorm + residual + ReLU: the backward from the forward's 1-bit ReLU mask
+    equals the backward from the saved bf16 output, bit for bit."""
+    g = torch.Generator(device="cuda").manual_seed(12)
+    x = torch.randn(4, 256, 14, 14, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    res = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
+    gamma = torch.rand(256, device="cuda", generator=g) + 0.5
+    beta = torch.randn(256, device="cuda", generator=g) * 0.2
+    y, mean, invstd, mask = hip.bn_act_fwd(x, res, gamma, beta, None, None, 1e-5, 0.1, True)
+    assert mask.dtype == torch.uint8 and mask.numel() == x.numel() // 8
+    yl = y.permute(0, 2, 3, 1).reshape(-1)
+    bits = ((mask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).reshape(-1)
+    assert torch.equal(bits.bool(), yl.float() > 0)
+    dy = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
+    a = hip.bn_act_bwd(dy, y, x, mean, invstd, gamma, beta, True, True, None, None)
+    b = hip.bn_act_bwd(dy, mask, x, mean, invstd, gamma, beta, True, True, None, None)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
