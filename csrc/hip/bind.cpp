@@ -538,6 +538,16 @@ at::Tensor conv_weight_t(at::Tensor w) {
   return wt;
 }
 
+// dst[segment] = Wᵀ of src[segment] for every (offset, K, T, C) row of table (int32, device)
+void conv_weight_t_batched(at::Tensor src, at::Tensor dst, at::Tensor table, int64_t max_tiles) {
+  CHECK_BF16(src); CHECK_BF16(dst);
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.numel() == dst.numel() && table.is_cuda() &&
+              table.scalar_type() == at::kInt && table.dim() == 2 && table.size(1) == 4 && table.is_contiguous(),
+              "conv_weight_t_batched: bf16 arenas and an int32 [n, 4] device table");
+  CHECK_RC(pdo::conv_weight_t_batched(bp(src), bp(dst), table.data_ptr<int>(), (int)table.size(0), max_tiles,
+                                      cur_stream()), "conv_weight_t_batched");
+}
+
 // dx [N, C, H, W] (channels_last) of y = conv(x, w) from dy and wt = conv_weight_t(w)
 // add: a same-shape channels_last bf16 gradient summed in the epilogue (dx = dgrad + add)
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor wt, int64_t C, int64_t R, int64_t S, int64_t H, int64_t W,
@@ -911,6 +921,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("with_stats") = false);
   m.def("conv_tile_rows", &conv_tile_rows);
   m.def("conv_weight_t", &conv_weight_t);
+  m.def("conv_weight_t_batched", &conv_weight_t_batched);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("C"), py::arg("R"), py::arg("S"),
         py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("add") = py::none());
   m.def("gemm_nt_add", &gemm_nt_add);

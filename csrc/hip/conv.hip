@@ -637,6 +637,40 @@ int conv_fwd_nhwc(const bf16* x, int N, int H, int W, int C, const bf16* w, int 
   return run_igemm(a, st, nullptr);
 }
 
+// Wᵀ of many convolution weights in one launch: segment j (blockIdx.y) =
+// table[j] = (element offset, K, T, C) in both arenas (bf16 shadow → its Wᵀ
+// image).  Per tap t the segment is a K × C → C × K transpose; a block moves one
+// 64 × 64 tile through LDS (reads along C, writes along K, both coalesced);
+// blockIdx.x enumerates (t, k-tile, c-tile), blocks past a segment's tiles exit.
+__global__ __launch_bounds__(256) void conv_wt_batched_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                              const int* __restrict__ table) {
+  __shared__ bf16 tile[64][65];
+  const int* e = table + 4 * blockIdx.y;
+  const long long off = e[0];
+  const int K = e[1], T = e[2], C = e[3];
+  const int kt = (K + 63) / 64, ct = (C + 63) / 64;
+  const int b = blockIdx.x;
+  if (b >= T * kt * ct) return;
+  const int t = b / (kt * ct), r = b - t * kt * ct, k0 = (r / ct) * 64, c0 = (r % ct) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {  // src [K][T][C]: row k0 + i, columns c0 + tx
+    const int k = k0 + i, c = c0 + tx;
+    if (k < K && c < C) tile[i][tx] = src[off + ((long long)k * T + t) * C + c];
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {  // dst [C][T][K]: row c0 + i, columns k0 + tx
+    const int c = c0 + i, k = k0 + tx;
+    if (k < K && c < C) dst[off + ((long long)c * T + t) * K + k] = tile[tx][i];
+  }
+}
+
+int conv_weight_t_batched(const bf16* src, bf16* dst, const int* table, int n, long long max_tiles,
+                          hipStream_t st) {
+  if (n < 1 || n > 65535 || max_tiles < 1 || max_tiles > 0x7fffffffLL) return -2;
+  conv_wt_batched_kernel<<<dim3((unsigned)max_tiles, (unsigned)n), 256, 0, st>>>(src, dst, table);
+  return 0;
+}
+
 int conv_weight_t(const bf16* w, bf16* wt, int Kout, int T, int C, hipStream_t st) {
   conv_wt_kernel<<<stream_grid((long long)Kout * T * C, 256), 256, 0, st>>>(w, wt, Kout, T, C);
   return 0;

@@ -61,6 +61,9 @@ int conv_wgrad_dw4_splits(int Kout, int TC, long long M);
 int conv_wgrad_mode(int mode);
 int conv_wgrad_dw4(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                    int pad, float* part, int splits, hipStream_t st);
+// Wᵀ [C][T·K] of each [K][T][C] segment (table: n × (offset, K, T, C) int32, device) in one launch;
+// max_tiles = the largest segment's T·⌈K/64⌉·⌈C/64⌉
+int conv_weight_t_batched(const bf16* src, bf16* dst, const int* table, int n, long long max_tiles, hipStream_t st);
 int conv_dgrad_tiles(int N, int H, int W, int C, int R, int stride, int pad);
 int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, int Kout, int R, int S, int stride,
                     int pad, bf16* dx, hipStream_t st, const ConvBnBwd* bn = nullptr, const bf16* add = nullptr);

@@ -995,9 +995,11 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, w, stride, pad, want_stats, fork=False):
         m = _native.require_hip()
         sh = getattr(w, "_pdo_shadow", None)  # the arena's bf16 copy, cast once per step (FlatParams.shadow_scope)
+        ctx.wt = None
         if sh is not None and sh[0].shadow_live and sh[1].dtype == torch.bfloat16 \
                 and sh[1].is_contiguous(memory_format=torch.channels_last):
             wb = sh[1]
+            ctx.wt = getattr(w, "_pdo_shadow_t", None)  # Wᵀ, built with the shadow (one launch per step)
         else:
             wb = w.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         K, C, R, _ = wb.shape
@@ -1041,16 +1043,17 @@ class _ConvFn(torch.autograd.Function):
                 dx = (m.gemm_nt_add(dy2, wt2, dalias.permute(0, 2, 3, 1).reshape(T, C)) if dalias is not None
                       else m.gemm_nt(dy2, wt2))
                 dx = dx.view(N, H, W_, C).permute(0, 3, 1, 2)
-            elif link is not None and link.bn is not None:
-                # the producing BatchNorm's backward statistics from this epilogue
-                bx, mean, invstd, bw, bb, relu = link.bn
-                dx, part = m.conv_dgrad_bn(dy, m.conv_weight_t(wb), R, S, ctx.stride, ctx.pad, bx, mean, invstd,
-                                           bw, bb, relu)
-                link.give(dx, part)
-                if dalias is not None:  # (not a ResNet pattern: a BatchNorm output is not forked)
-                    dx = dx + dalias
             else:
-                dx = m.conv_dgrad(dy, m.conv_weight_t(wb), C, R, S, H, W_, ctx.stride, ctx.pad, dalias)
+                wt = ctx.wt if ctx.wt is not None else m.conv_weight_t(wb)
+                if link is not None and link.bn is not None:
+                    # the producing BatchNorm's backward statistics from this epilogue
+                    bx, mean, invstd, bw, bb, relu = link.bn
+                    dx, part = m.conv_dgrad_bn(dy, wt, R, S, ctx.stride, ctx.pad, bx, mean, invstd, bw, bb, relu)
+                    link.give(dx, part)
+                    if dalias is not None:  # (not a ResNet pattern: a BatchNorm output is not forked)
+                        dx = dx + dalias
+                else:
+                    dx = m.conv_dgrad(dy, wt, C, R, S, H, W_, ctx.stride, ctx.pad, dalias)
         if ctx.needs_input_grad[1]:
             p = ctx.wparam
             if ctx.one and _gemm_wgrad_1x1(C, K):

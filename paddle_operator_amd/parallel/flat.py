@@ -160,6 +160,20 @@ class FlatParams:
         self.shadow_live = False
         for s in self.slots:
             s.param._pdo_shadow = (self, self._view(self.shadow, s))
+        # convolution weights (channels_last [K, C, R, S] = OHWI memory) also get their
+        # input-gradient operand Wᵀ [C, R·S·K], built for all of them in one launch
+        self.shadow_t, self._wt_table, self._wt_max = None, None, 0
+        convs = [s for s in self.slots if len(s.shape) == 4 and s.param.is_contiguous(memory_format=torch.channels_last)
+                 and s.param.shape[1] % 8 == 0]
+        if convs and self.device.type == "cuda":
+            self.shadow_t = torch.empty(self.numel, dtype=dtype, device=self.device)
+            rows = []
+            for s in convs:
+                K, C, R, S = s.shape
+                rows.append((s.offset, K, R * S, C))
+                s.param._pdo_shadow_t = self.shadow_t[s.offset:s.offset + s.numel].view(C, R * S * K)
+                self._wt_max = max(self._wt_max, R * S * ((K + 63) // 64) * ((C + 63) // 64))  # 64 × 64 tiles
+            self._wt_table = torch.tensor(rows, dtype=torch.int32, device=self.device)
 
     def shadow_scope(self):
         flat = self
@@ -168,6 +182,10 @@ class FlatParams:
             def __enter__(self):
                 if getattr(flat, "shadow", None) is not None:
                     flat.shadow.copy_(flat.params)
+                    if flat.shadow_t is not None:
+                        from .. import _native
+                        _native.require_hip().conv_weight_t_batched(flat.shadow, flat.shadow_t, flat._wt_table,
+                                                                     flat._wt_max)
                     flat.shadow_live = True
 
             def __exit__(self, *exc):

@@ -85,9 +85,12 @@ class ResNetTrainer:
             broadcast_buffers(list(self.model.buffers()), 0)
 
     def batch(self):
-        x = torch.randn(self.B, 3, self.res, self.res, device=self.device, generator=self.gen)
-        if self.cl:
-            x = x.to(memory_format=torch.channels_last)
+        if self.cl:  # drawn in NHWC memory order: a channels_last tensor without a layout copy
+            # (bf16: the stem convolution runs in bf16 under autocast anyway — no cast pass)
+            x = torch.randn(self.B, self.res, self.res, 3, device=self.device, generator=self.gen,
+                            dtype=torch.bfloat16).permute(0, 3, 1, 2)
+        else:
+            x = torch.randn(self.B, 3, self.res, self.res, device=self.device, generator=self.gen)
         y = torch.randint(0, self.classes, (self.B,), device=self.device, generator=self.gen)
         return x, y
 
