@@ -110,7 +110,8 @@ def parse_args(argv=None):
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
     ap.add_argument("--secondary-resnet", type=int, default=int(os.environ.get("PDO_BENCH_RESNET", "1")),
                     help="after the GPT-2 job (GPUs only): a ResNet-50 job (configs 2/3, batch 256 per GPU, 20 timed "
-                         "steps) on the same ranks, reported under 'secondary' (0: skip)")
+                         "steps) on the same ranks, reported under 'secondary' — 1: at one GPU only, 2: at every N, "
+                         "0: skip")
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
     ap.add_argument("--ready-only", action="store_true", help="only the ready trials (prints their record)")
@@ -370,14 +371,14 @@ def orchestrate(a):
             L.finish(name)
             out["bench"] = rs
             out["bench_ready_s"] = max(r["t_ready"] for r in rs) - t0
-            if a.workload == "gpt2" and a.secondary_resnet and gpus and a.ops == "hip":
+            if a.workload == "gpt2" and a.secondary_resnet and gpus and a.ops == "hip" and (N == 1 or a.secondary_resnet > 1):
                 # the reference's own example workload (deploy/examples/resnet.yaml) in the same
                 # driver run; a failure here never costs the headline record
                 try:
                     wl2 = ["--workload", "resnet50", "--batch", "256", "--steps", "20", "--warmup", "5", "--bench",
                            "--timeout", "600"]
                     L.launch("resnet50-bench", N, wl2, a.ops)
-                    out["resnet"] = L.wait_records("resnet50-bench", "bench", N, a.timeout)
+                    out["resnet"] = L.wait_records("resnet50-bench", "bench", N, min(a.timeout, 300.0))
                     L.finish("resnet50-bench")
                 except Exception as e:  # noqa: BLE001
                     out["resnet_error"] = f"{type(e).__name__}: {e}"
