@@ -308,3 +308,30 @@ def test_bench_launched_resnet_workload():
     rec = _json_line(r.stdout)
     assert rec["unit"] == "images/s" and rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 8
     assert abs(rec["value"] - 4 * 2 * 2 / (rec["ms_per_step"] * 2 / 1e3)) / rec["value"] < 1e-2
+
+
+def test_flat_shadow_scope_cpu():
+    """FlatParams.enable_shadow: the low-precision copy of the arena is refreshed
+    on entering shadow_scope, readable (shadow_live) only inside it, and each
+    parameter's _pdo_shadow view aliases its slice with the parameter's strides."""
+    import torch
+
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Conv2d(8, 16, 3, bias=False), torch.nn.Linear(16, 4))
+    m = m.to(memory_format=torch.channels_last)
+    flat = FlatParams(m, dtype=torch.float32, device=torch.device("cpu"))
+    flat.enable_shadow(torch.bfloat16)
+    w = m[0].weight
+    arena, view = w._pdo_shadow
+    assert arena is flat and not flat.shadow_live
+    assert view.shape == w.shape and view.stride() == w.stride() and view.dtype == torch.bfloat16
+    with flat.shadow_scope():
+        assert flat.shadow_live
+        assert torch.equal(view, w.detach().to(torch.bfloat16))
+    assert not flat.shadow_live
+    with torch.no_grad():
+        w.add_(1.0)  # a change outside the scope: the next scope refreshes
+    with flat.shadow_scope():
+        assert torch.equal(view, w.detach().to(torch.bfloat16))
