@@ -927,6 +927,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("gemm_nt_add", &gemm_nt_add);
   m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("conv_wgrad_mode", &pdo::conv_wgrad_mode);
+  m.def("conv_wgrad_c64_mode", &pdo::conv_wgrad_c64_mode);
   m.def("bn_act_bwd_part", &bn_act_bwd_part);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none());

@@ -59,6 +59,8 @@ struct ConvBnBwd {
 int conv_wgrad_dw4_splits(int Kout, int TC, long long M);
 // PDO_WGRAD_DW4 routing (1 on, 0 off; < 0 only reads); returns the previous mode
 int conv_wgrad_mode(int mode);
+// PDO_WGRAD_C64 routing (the all-taps 64-channel 3×3 weight gradient); < 0 only reads
+int conv_wgrad_c64_mode(int mode);
 int conv_wgrad_dw4(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                    int pad, float* part, int splits, hipStream_t st);
 // Wᵀ [C][T·K] of each [K][T][C] segment (table: n × (offset, K, T, C) int32, device) in one launch;

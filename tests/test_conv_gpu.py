@@ -265,3 +265,25 @@ def test_bn_residual_relu_mask_matches_saved_output(hip):
     b = hip.bn_act_bwd(dy, mask, x, mean, invstd, gamma, beta, True, True, None, None)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("N,H", [(8, 16), (3, 7), (16, 28)])
+def test_conv_wgrad_c64_all_taps(hip, N, H):
+    """The all-taps 64-channel 3×3 weight gradient (one workgroup stages dY once
+    and the nine gathered X tiles per k-step) against fp32 autograd and the
+    per-tap kernel; token counts with a partial last k-step (3 × 7 × 7)."""
+    x, w = _mk(N, 64, H, 64, 3, 13)
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, padding=1)
+    g = torch.Generator(device="cuda").manual_seed(14)
+    dy = torch.randn(ref.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    ref.backward(dy.float())
+    prev = hip.conv_wgrad_c64_mode(1)
+    try:
+        dw = hip.conv_wgrad(dy, x, 3, 3, 1, 1)
+        hip.conv_wgrad_c64_mode(0)
+        dw1 = hip.conv_wgrad(dy, x, 3, 3, 1, 1)
+    finally:
+        hip.conv_wgrad_c64_mode(prev)
+    assert _rel(dw, wf.grad) < 5e-3
+    assert _rel(dw, dw1) < 1e-4

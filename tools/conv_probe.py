@@ -79,6 +79,14 @@ def main():
                 finally:
                     m.conv_wgrad_mode(prev)
             cand["hip1_wgrad"] = wg1
+        if hasattr(m, "conv_wgrad_c64_mode") and C == 64 and K == 64 and R == 3:
+            def wg64off():
+                prev = m.conv_wgrad_c64_mode(0)
+                try:
+                    return m.conv_wgrad(dy, x, R, R, st, pad)
+                finally:
+                    m.conv_wgrad_c64_mode(prev)
+            cand["hip_pertap_wgrad"] = wg64off
         if R == 1 and st == 1:
             T = N * H * H
             x2, dy2, w2 = x.permute(0, 2, 3, 1).reshape(T, C), dy.permute(0, 2, 3, 1).reshape(T, K), w.view(K, C)
