@@ -530,18 +530,18 @@ __global__ __launch_bounds__(CNT, 2) void conv_wgrad_kernel(const WgradArgs a) {
 }
 
 // ============================================================================
-// weight gradient, 64 → 64 channels, 3×3 (ResNet layer 1): ALL nine taps in one
-// workgroup.  The 128 × 128 kernel re-reads dY once per tap tile (9×) and the
-// gathered X once per tap; here a workgroup owns the whole [64 co][9 taps][64 ci]
-// output for one token slice, so each 64-token k-step stages dY once (8 KiB) and
-// the nine gathered X sub-tiles (9 × 8 KiB; each token row's pixel computed once,
-// the taps as offsets), two stages = 160 KiB, one workgroup per CU.  Wave w owns
-// output columns [144w, 144w + 144) = 64 co × 9 blocks of 16 (144 accumulators);
-// fragments are transposed LDS reads as in conv_wgrad_kernel (128-B rows, wswz<128>).
-struct Wgrad64Args {
+// weight gradient, C = Kout = CH, 3×3 (ResNet layers 1 and 2): NT taps in one
+// workgroup (CH 64: all nine; CH 128: one kernel row of three, grid × 3).  The
+// per-tap kernels re-read dY once per tap tile; here each 64-token k-step stages
+// dY once ([64 tok][CH]) and the NT gathered X sub-tiles (each token row's pixel
+// computed once, the taps as offsets) — 160 KiB (CH 64) / 128 KiB (CH 128) for
+// two stages, one workgroup per CU.  Wave w owns output columns
+// [w·NT·CH/4, (w + 1)·NT·CH/4) of the group's NT·CH, all CH rows; fragments are
+// transposed LDS reads as in conv_wgrad_kernel.
+struct WgradTapsArgs {
   const bf16* dy;
   const bf16* x;
-  float* part;  // [splits][64][576]
+  float* part;  // [splits][CH][9·CH]
   long long M;
   int IH, IW, TA, TB;
   float inv_TA, inv_TB;
@@ -550,32 +550,40 @@ struct Wgrad64Args {
   int splits, ksteps;
 };
 
-__global__ __launch_bounds__(CNT, 1) void conv_wgrad_c64_kernel(const Wgrad64Args a) {
-  constexpr int TS = 64 * 128;       // bytes of one [64 tok][64] bf16 sub-tile
-  constexpr int STAGE = 10 * TS;     // dY + 9 X taps
+template <int CH, int NT>
+__global__ __launch_bounds__(CNT, 1) void conv_wgrad_taps_kernel(const WgradTapsArgs a) {
+  constexpr int RB = CH * 2;                 // LDS row bytes
+  constexpr int TS = 64 * RB;                // bytes of one [64 tok][CH] sub-tile
+  constexpr int STAGE = (1 + NT) * TS;
+  constexpr int RPP = 1024 / RB;             // rows per 1-KiB piece
+  constexpr int LPR = RB / 16;               // lanes per row
+  constexpr int PW = 64 / RPP / 4;           // pieces per wave per sub-tile
+  constexpr int WC = NT * CH / 4;            // output columns per wave
+  constexpr int NJ = WC / 16, MI = CH / 16;  // accumulator blocks
+  constexpr int PER = PW * (1 + NT);         // DMA pieces per wave per k-step
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int split = blockIdx.x;
+  const int split = blockIdx.x % a.splits, grp = blockIdx.x / a.splits;  // tap group: taps NT·grp ..
   const int kq = a.ksteps / a.splits, kr = a.ksteps % a.splits;
   const int k0 = split * kq + min(split, kr), nk = kq + (split < kr ? 1 : 0);
   const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.dy), 0, (int)a.dybytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  // this lane's rows in pieces p = w, w + 4 (8 rows × 128 B each): row 8p + (l >> 3), chunk (l & 7) ^ swz
-  int prow[2], pch[2];
+  // this lane's rows in pieces p = w + 4i: row RPP·p + l / LPR, chunk (l % LPR) ^ swz
+  int prow[PW], pch[PW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    prow[i] = 8 * (w + 4 * i) + (lane >> 3);
-    pch[i] = (lane & 7) ^ wswz<128>(prow[i]);
+  for (int i = 0; i < PW; ++i) {
+    prow[i] = RPP * (w + 4 * i) + lane / LPR;
+    pch[i] = (lane % LPR) ^ wswz<RB>(prow[i]);
   }
   auto issue = [&](int kt, int stage) {
     const unsigned sb = lds0 + (unsigned)(stage * STAGE);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < PW; ++i) {
       const long long t = (long long)kt * 64 + prow[i];
       const unsigned p = (unsigned)((w + 4 * i) * 1024);
-      bufld(t < a.M ? (unsigned)((t * 64 + pch[i] * 8) * 2) : OOB, rsY, sb + p);
+      bufld(t < a.M ? (unsigned)((t * CH + pch[i] * 8) * 2) : OOB, rsY, sb + p);
       int hb = -(1 << 20), wb = 0, base = 0;
       if (t < a.M) {
         int q, wo, n, ho;
@@ -583,13 +591,13 @@ __global__ __launch_bounds__(CNT, 1) void conv_wgrad_c64_kernel(const Wgrad64Arg
         divmod(q, a.TA, a.inv_TA, n, ho);
         hb = ho * a.st - a.pad;
         wb = wo * a.st - a.pad;
-        base = ((n * a.IH + hb) * a.IW + wb) * 64 + pch[i] * 8;
+        base = ((n * a.IH + hb) * a.IW + wb) * CH + pch[i] * 8;
       }
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int dh = tap / 3, dw = tap % 3;
+      for (int u = 0; u < NT; ++u) {
+        const int tap = NT * grp + u, dh = tap / 3, dw = tap - 3 * dh;
         const bool ok = (unsigned)(hb + dh) < (unsigned)a.IH && (unsigned)(wb + dw) < (unsigned)a.IW;
-        bufld(ok ? (unsigned)((base + (dh * a.IW + dw) * 64) * 2) : OOB, rsX, sb + (unsigned)((1 + tap) * TS) + p);
+        bufld(ok ? (unsigned)((base + (dh * a.IW + dw) * CH) * 2) : OOB, rsX, sb + (unsigned)((1 + u) * TS) + p);
       }
     }
   };
@@ -597,24 +605,23 @@ __global__ __launch_bounds__(CNT, 1) void conv_wgrad_c64_kernel(const Wgrad64Arg
   auto frag = [&](const char* T, int cb, int kk) -> bf16x8 {
     const int col = cb + 4 * p4;
     const int r0 = 32 * kk + 4 * g + q4, r1 = r0 + 16;
-    const char* a0 = T + r0 * 128 + (((col >> 3) ^ wswz<128>(r0)) << 4) + (col & 7) * 2;
-    const char* a1 = T + r1 * 128 + (((col >> 3) ^ wswz<128>(r1)) << 4) + (col & 7) * 2;
+    const char* a0 = T + r0 * RB + (((col >> 3) ^ wswz<RB>(r0)) << 4) + (col & 7) * 2;
+    const char* a1 = T + r1 * RB + (((col >> 3) ^ wswz<RB>(r1)) << 4) + (col & 7) * 2;
     const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a0);
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a1);
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   };
-  // wave w's 9 column blocks of 16: global column 144w + 16j = tap (144w + 16j) / 64, ci block
-  f32x4 acc[4][9];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) issue(k0, 0);
   for (int k = 0; k < nk; ++k) {
     if (k + 1 < nk) {
       issue(k0 + k + 1, (k + 1) & 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(20) : "memory");  // step k landed (step k + 1's 20 pieces fly)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step k landed (step k + 1 flies)
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -622,29 +629,29 @@ __global__ __launch_bounds__(CNT, 1) void conv_wgrad_c64_kernel(const Wgrad64Arg
     const char* S0 = smem + (k & 1) * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 fa[4];
+      bf16x8 fa[MI];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag(S0, 16 * i, kk);
+      for (int i = 0; i < MI; ++i) fa[i] = frag(S0, 16 * i, kk);
 #pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const int gc = 144 * w + 16 * j, tap = gc >> 6;
-        const bf16x8 fb = frag(S0 + (1 + tap) * TS, gc & 63, kk);
+      for (int j = 0; j < NJ; ++j) {
+        const int gc = WC * w + 16 * j, u = gc / CH;  // the group's column → sub-tile u, channel gc % CH
+        const bf16x8 fb = frag(S0 + (1 + u) * TS, gc % CH, kk);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MI; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  // acc[i][j][e] = dW[co = 16i + 4g + e][col = 144w + 16j + (l & 15)]
-  float* out = a.part + (size_t)split * 64 * 576;
+  // acc[i][j][e] = dW[co = 16i + 4g + e][9·CH column NT·CH·grp + WC·w + 16j + (l & 15)]
+  float* out = a.part + (size_t)split * CH * 9 * CH + NT * CH * grp;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float* orow = out + (16 * i + 4 * g + e) * 576 + 144 * w + (lane & 15);
+      float* orow = out + (size_t)(16 * i + 4 * g + e) * 9 * CH + WC * w + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < 9; ++j) orow[16 * j] = acc[i][j][e];
+      for (int j = 0; j < NJ; ++j) orow[16 * j] = acc[i][j][e];
     }
 }
 
@@ -958,16 +965,17 @@ int conv_wgrad_mode(int mode) {
   return prev;
 }
 
-// the all-taps 64-channel 3×3 kernel (PDO_WGRAD_C64=0: the 128 × 128 / 64 × 64 kernel)
+// the tap-group 3×3 kernels for 64 / 128 channels (PDO_WGRAD_C64=0: the per-tap / dw4 kernels)
 static int g_wgrad_c64 = [] {
   const char* e = getenv("PDO_WGRAD_C64");
   return e && *e ? atoi(e) : 1;
 }();
+// splits of the tap-group kernel (grid = splits × tap groups ≈ one workgroup per CU); 0: not taken
 static int wgrad_c64_splits(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
-  if (!g_wgrad_c64 || C != 64 || Kout != 64 || R != 3 || S != 3 || pad != 1) return 0;
+  if (!g_wgrad_c64 || C != Kout || (C != 64 && C != 128) || R != 3 || S != 3 || pad != 1) return 0;
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   const long long ks = ((long long)N * Ho * Wo + 63) / 64;
-  long long sp = 256;  // one workgroup per CU
+  long long sp = C == 64 ? 256 : 85;  // 9 / NT tap groups per split
   if (sp > ks / 4) sp = ks / 4;
   return sp < 1 ? 1 : (int)sp;
 }
@@ -980,7 +988,7 @@ int conv_wgrad_c64_mode(int mode) {
 
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
   const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
-  if (const int sp64 = wgrad_c64_splits(N, H, W, C, Kout, R, S, stride, pad)) return (long long)sp64 * 64 * 576;
+  if (const int sp64 = wgrad_c64_splits(N, H, W, C, Kout, R, S, stride, pad)) return (long long)sp64 * C * 9 * C;
   const int sp4 = wgrad_dw4_splits(N, H, W, C, Kout, R, S, stride, pad);
   if (sp4) return (long long)sp4 * Kout * ((R * S * C + 255) / 256 * 256);
   int bm, bn, sp;
@@ -993,7 +1001,7 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st) {
   if (!conv_supported(N, H, W, C, Kout, R, S, stride, pad)) return -2;
   if (const int sp64 = wgrad_c64_splits(N, H, W, C, Kout, R, S, stride, pad)) {
-    Wgrad64Args g{};
+    WgradTapsArgs g{};
     const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
     g.dy = dy;
     g.x = x;
@@ -1007,12 +1015,13 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
     g.inv_TB = 1.f / (float)Wo;
     g.st = stride;
     g.pad = pad;
-    g.xbytes = (unsigned)((long long)N * H * W * 64 * 2);
-    g.dybytes = (unsigned)(g.M * 64 * 2);
+    g.xbytes = (unsigned)((long long)N * H * W * C * 2);
+    g.dybytes = (unsigned)(g.M * C * 2);
     g.splits = sp64;
     g.ksteps = (int)((g.M + 63) / 64);
-    conv_wgrad_c64_kernel<<<(unsigned)sp64, CNT, 0, st>>>(g);
-    wgrad_fold(scratch, sp64, 64, 576, 576, dw, accumulate, st);
+    if (C == 64) conv_wgrad_taps_kernel<64, 9><<<(unsigned)sp64, CNT, 0, st>>>(g);
+    else conv_wgrad_taps_kernel<128, 3><<<(unsigned)(sp64 * 3), CNT, 0, st>>>(g);
+    wgrad_fold(scratch, sp64, C, 9 * C, 9 * C, dw, accumulate, st);
     return 0;
   }
   const int sp4 = wgrad_dw4_splits(N, H, W, C, Kout, R, S, stride, pad);

@@ -267,22 +267,24 @@ def test_bn_residual_relu_mask_matches_saved_output(hip):
         assert torch.equal(u, v)
 
 
-@pytest.mark.parametrize("N,H", [(8, 16), (3, 7), (16, 28)])
-def test_conv_wgrad_c64_all_taps(hip, N, H):
-    """The all-taps 64-channel 3×3 weight gradient (one workgroup stages dY once
-    and the nine gathered X tiles per k-step) against fp32 autograd and the
-    per-tap kernel; token counts with a partial last k-step (3 × 7 × 7)."""
-    x, w = _mk(N, 64, H, 64, 3, 13)
+@pytest.mark.parametrize("N,C,H,stride", [(8, 64, 16, 1), (3, 64, 7, 1), (16, 64, 28, 1), (8, 128, 16, 1),
+                                           (3, 128, 7, 1), (8, 128, 16, 2), (4, 64, 14, 2)])
+def test_conv_wgrad_tap_groups(hip, N, C, H, stride):
+    """The tap-group 3×3 weight gradient (C = Kout = 64: all nine taps per
+    workgroup; 128: one kernel row of three) — dY staged once per k-step for the
+    group's gathered X tiles — against fp32 autograd and the per-tap / dw4
+    kernels; token counts with a partial last k-step (3 × 7 × 7), stride 2."""
+    x, w = _mk(N, C, H, C, 3, 13)
     wf = w.float().requires_grad_()
-    ref = F.conv2d(x.float(), wf, padding=1)
+    ref = F.conv2d(x.float(), wf, stride=stride, padding=1)
     g = torch.Generator(device="cuda").manual_seed(14)
     dy = torch.randn(ref.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
     ref.backward(dy.float())
     prev = hip.conv_wgrad_c64_mode(1)
     try:
-        dw = hip.conv_wgrad(dy, x, 3, 3, 1, 1)
+        dw = hip.conv_wgrad(dy, x, 3, 3, stride, 1)
         hip.conv_wgrad_c64_mode(0)
-        dw1 = hip.conv_wgrad(dy, x, 3, 3, 1, 1)
+        dw1 = hip.conv_wgrad(dy, x, 3, 3, stride, 1)
     finally:
         hip.conv_wgrad_c64_mode(prev)
     assert _rel(dw, wf.grad) < 5e-3

@@ -79,7 +79,7 @@ def main():
                 finally:
                     m.conv_wgrad_mode(prev)
             cand["hip1_wgrad"] = wg1
-        if hasattr(m, "conv_wgrad_c64_mode") and C == 64 and K == 64 and R == 3:
+        if hasattr(m, "conv_wgrad_c64_mode") and C == K and C in (64, 128) and R == 3:
             def wg64off():
                 prev = m.conv_wgrad_c64_mode(0)
                 try:
