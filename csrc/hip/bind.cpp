@@ -335,13 +335,20 @@ at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c
 }
 
 // c = a·bᵀ + r (r: [M, N] contiguous bf16), one pass
-at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r) {
+// c = a·bᵀ (+ bias) + r, one rounding on the 4-wave mainloop
+at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r, c10::optional<at::Tensor> bias) {
   nt_check(a, b);
   CHECK_IN(r); CHECK_BF16(r);
   const int M = a.size(0), N = b.size(0), K = a.size(1);
   TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N, "gemm_nt_add: r must be [M, N]");
+  const bf16* bptr = nullptr;
+  if (bias && bias->defined()) {
+    CHECK_IN((*bias)); CHECK_BF16((*bias));
+    TORCH_CHECK(bias->numel() == N, "gemm_nt_add: bias must have N elements");
+    bptr = bp(*bias);
+  }
   auto c = at::empty({M, N}, a.options());
-  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, 4, nullptr, bp(r), N, nullptr, cur_stream()),
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, bptr ? 5 : 4, bptr, bp(r), N, nullptr, cur_stream()),
            "gemm_nt_add");
   return c;
 }
@@ -618,6 +625,58 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t R, int64_t S, int64_t
                            x.options().dtype(at::kFloat));
   CHECK_RC(pdo::conv_wgrad_nhwc(bp(dy), bp(x), N, H, W, C, K, (int)R, (int)S, (int)stride, (int)pad, fp(dw),
                                 acc ? 1 : 0, fp(scratch), cur_stream()), "conv_wgrad_nhwc");
+  return dw;
+}
+
+// ResNet stem 7×7 / stride 2 / pad 3 (3 → 64 channels) through the space-to-depth
+// 4×4 implicit GEMM: [y, BatchNorm tile statistics (with_stats), z = the 16-channel
+// image the weight gradient reads]
+bool stem_ok(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K) {
+  return pdo::stem_supported((int)N, (int)H, (int)W, (int)C, (int)K) != 0;
+}
+
+std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, bool with_stats) {
+  CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_fwd: channels_last bf16 input");
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+              w.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_fwd: channels_last bf16 weight [K, 3, 7, 7]");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)w.size(0);
+  TORCH_CHECK(pdo::stem_supported(N, H, W, C, K), "stem_fwd: unsupported shape");
+  const int IH = H / 2, IW = W / 2;
+  auto z = at::empty({N, 16, IH, IW}, x.options(), at::MemoryFormat::ChannelsLast);
+  auto w2 = at::empty({K, 256}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  auto y = at::empty({N, K, IH, IW}, x.options(), at::MemoryFormat::ChannelsLast);
+  at::Tensor st;
+  if (with_stats) st = at::empty({pdo::stem_fwd_tiles((long long)N * IH * IW), 2, K}, x.options().dtype(at::kFloat));
+  auto s = cur_stream();
+  CHECK_RC(pdo::stem_s2d(bp(x), N, H, W, bp(z), s), "stem_s2d");
+  CHECK_RC(pdo::stem_weight(bp(w), bp(w2), K, s), "stem_weight");
+  CHECK_RC(pdo::stem_fwd(bp(z), N, IH, IW, bp(w2), K, bp(y), with_stats ? fp(st) : nullptr, s), "stem_fwd");
+  return {y, st, z};
+}
+
+// dw (fp32 [K, 3, 7, 7] channels_last) (+)= the stem's weight gradient from dy and stem_fwd's z
+at::Tensor stem_wgrad(at::Tensor dy, at::Tensor z, c10::optional<at::Tensor> out) {
+  CHECK_BF16(dy); CHECK_BF16(z);
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              z.is_contiguous(at::MemoryFormat::ChannelsLast) && z.size(1) == 16,
+              "stem_wgrad: channels_last bf16 dy, z [N, 16, H/2, W/2]");
+  const int N = (int)z.size(0), IH = (int)z.size(2), IW = (int)z.size(3), K = (int)dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == IH && dy.size(3) == IW, "stem_wgrad: dy / z shapes");
+  at::Tensor dw;
+  const bool acc = out.has_value() && out->defined();
+  if (acc) {
+    dw = *out;
+    CHECK_F32(dw);
+    TORCH_CHECK(dw.numel() == (int64_t)K * 147 && dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_wgrad: out must be a channels_last fp32 [K, 3, 7, 7]");
+  } else {
+    dw = at::empty({K, 3, 7, 7}, z.options().dtype(at::kFloat), at::MemoryFormat::ChannelsLast);
+  }
+  auto scratch = at::empty({pdo::stem_wgrad_scratch_floats(N, IH, IW, K)}, z.options().dtype(at::kFloat));
+  CHECK_RC(pdo::stem_wgrad(bp(dy), bp(z), N, IH, IW, K, fp(dw), acc ? 1 : 0, fp(scratch), cur_stream()),
+           "stem_wgrad");
   return dw;
 }
 
@@ -920,11 +979,15 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("with_stats") = false);
   m.def("conv_tile_rows", &conv_tile_rows);
+  m.def("stem_ok", &stem_ok);
+  m.def("stem_tile_rows", &pdo::stem_tile_rows);
+  m.def("stem_fwd", &stem_fwd, py::arg("x"), py::arg("w"), py::arg("with_stats") = true);
+  m.def("stem_wgrad", &stem_wgrad, py::arg("dy"), py::arg("z"), py::arg("out") = py::none());
   m.def("conv_weight_t", &conv_weight_t);
   m.def("conv_weight_t_batched", &conv_weight_t_batched);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("C"), py::arg("R"), py::arg("S"),
         py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("add") = py::none());
-  m.def("gemm_nt_add", &gemm_nt_add);
+  m.def("gemm_nt_add", &gemm_nt_add, py::arg("a"), py::arg("b"), py::arg("r"), py::arg("bias") = py::none());
   m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("conv_wgrad_mode", &pdo::conv_wgrad_mode);
   m.def("conv_wgrad_c64_mode", &pdo::conv_wgrad_c64_mode);

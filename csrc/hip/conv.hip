@@ -277,6 +277,9 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
       hb[i] = aa * a.ist - a.ipad;
       wb[i] = bb * a.ist - a.ipad;
       base[i] = ((n * a.IH + hb[i]) * a.IW + wb[i]) * a.C + cg * 8;
+      // 16-channel input (the space-to-depth stem): a 128-B row is 4 pixels, the
+      // lane's chunk cg lies in pixel cg / 2 of them (bounds checked per lane)
+      if (a.C == 16) wb[i] += cg >> 1;
     } else {
       hb[i] = -(1 << 20);  // fails every bounds check
       wb[i] = 0;
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(CNT, 2) void conv_igemm_kernel(const ConvArgs a) {
   }
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  const int CC = a.C >> 6;
+  const int CC = a.C >= 64 ? a.C >> 6 : 1;  // C = 16: one k-step per tap (a row of 4 pixels)
   const int nk = a.ntaps * CC;
 
   auto issue = [&](int kt, int stage) {
@@ -550,7 +553,11 @@ struct WgradTapsArgs {
   int splits, ksteps;
 };
 
-template <int CH, int NT>
+// S2D (the space-to-depth stem, CH = 64, NT = 4): X is the 16-channel image
+// [N][IH][IW][16] of stem_s2d; tap u = kernel row u of the 4 × 4 stride-1
+// convolution, a 128-B X row = 4 pixels × 16 channels from the token's pixel
+// (ho − 2 + u, wo − 2), each lane's 16-B chunk bounds-checked on its own pixel.
+template <int CH, int NT, bool S2D>
 __global__ __launch_bounds__(CNT, 1) void conv_wgrad_taps_kernel(const WgradTapsArgs a) {
   constexpr int RB = CH * 2;                 // LDS row bytes
   constexpr int TS = 64 * RB;                // bytes of one [64 tok][CH] sub-tile
@@ -561,6 +568,9 @@ __global__ __launch_bounds__(CNT, 1) void conv_wgrad_taps_kernel(const WgradTaps
   constexpr int WC = NT * CH / 4;            // output columns per wave
   constexpr int NJ = WC / 16, MI = CH / 16;  // accumulator blocks
   constexpr int PER = PW * (1 + NT);         // DMA pieces per wave per k-step
+  constexpr int XC = S2D ? 16 : CH;          // X channels per pixel
+  constexpr int TOT = S2D ? NT * CH : 9 * CH;  // output columns (all tap groups)
+  static_assert(!S2D || (CH == 64 && NT == 4), "stem: 64 channels, 4 kernel rows");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -591,13 +601,14 @@ __global__ __launch_bounds__(CNT, 1) void conv_wgrad_taps_kernel(const WgradTaps
         divmod(q, a.TA, a.inv_TA, n, ho);
         hb = ho * a.st - a.pad;
         wb = wo * a.st - a.pad;
-        base = ((n * a.IH + hb) * a.IW + wb) * CH + pch[i] * 8;
+        base = ((n * a.IH + hb) * a.IW + wb) * XC + pch[i] * 8;
+        if (S2D) wb += pch[i] >> 1;  // this lane's pixel of the 4
       }
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
-        const int tap = NT * grp + u, dh = tap / 3, dw = tap - 3 * dh;
+        const int tap = NT * grp + u, dh = S2D ? u : tap / 3, dw = S2D ? 0 : tap - 3 * dh;
         const bool ok = (unsigned)(hb + dh) < (unsigned)a.IH && (unsigned)(wb + dw) < (unsigned)a.IW;
-        bufld(ok ? (unsigned)((base + (dh * a.IW + dw) * CH) * 2) : OOB, rsX, sb + (unsigned)((1 + u) * TS) + p);
+        bufld(ok ? (unsigned)((base + (dh * a.IW + dw) * XC) * 2) : OOB, rsX, sb + (unsigned)((1 + u) * TS) + p);
       }
     }
   };
@@ -643,13 +654,13 @@ __global__ __launch_bounds__(CNT, 1) void conv_wgrad_taps_kernel(const WgradTaps
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  // acc[i][j][e] = dW[co = 16i + 4g + e][9·CH column NT·CH·grp + WC·w + 16j + (l & 15)]
-  float* out = a.part + (size_t)split * CH * 9 * CH + NT * CH * grp;
+  // acc[i][j][e] = dW[co = 16i + 4g + e][TOT column NT·CH·grp + WC·w + 16j + (l & 15)]
+  float* out = a.part + (size_t)split * CH * TOT + NT * CH * grp;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float* orow = out + (size_t)(16 * i + 4 * g + e) * 9 * CH + WC * w + (lane & 15);
+      float* orow = out + (size_t)(16 * i + 4 * g + e) * TOT + WC * w + (lane & 15);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) orow[16 * j] = acc[i][j][e];
     }
@@ -1019,8 +1030,8 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
     g.dybytes = (unsigned)(g.M * C * 2);
     g.splits = sp64;
     g.ksteps = (int)((g.M + 63) / 64);
-    if (C == 64) conv_wgrad_taps_kernel<64, 9><<<(unsigned)sp64, CNT, 0, st>>>(g);
-    else conv_wgrad_taps_kernel<128, 3><<<(unsigned)(sp64 * 3), CNT, 0, st>>>(g);
+    if (C == 64) conv_wgrad_taps_kernel<64, 9, false><<<(unsigned)sp64, CNT, 0, st>>>(g);
+    else conv_wgrad_taps_kernel<128, 3, false><<<(unsigned)(sp64 * 3), CNT, 0, st>>>(g);
     wgrad_fold(scratch, sp64, C, 9 * C, 9 * C, dw, accumulate, st);
     return 0;
   }
@@ -1062,6 +1073,287 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
   else if (bn == 128) conv_wgrad_kernel<64, 128><<<(unsigned)grid, CNT, 0, st>>>(a);
   else conv_wgrad_kernel<64, 64><<<(unsigned)grid, CNT, 0, st>>>(a);
   wgrad_fold(scratch, a.splits, Kout, a.T * C, a.T * C, dw, accumulate, st);
+  return 0;
+}
+
+// ============================================================================
+// ResNet stem: y = conv7×7/2(x, w), pad 3, C = 3 → 64 channels.  With
+// z[n][i][j][(2p + q)·3 + c] = x[n][2i + p][2j + q][c] (channels 12-15 zero) and
+// the weight padded to 8 × 8 at the top / left (w8[r + 1][s + 1] = w[r][s]),
+//   y[oh][ow] = Σ_{a,b<4} Σ_{p,q,c} z[oh − 2 + a][ow − 2 + b][(2p + q)·3 + c] · w8[2a + p][2b + q][c]
+// — a 4×4 stride-1 convolution over a 16-channel image (pad 2 before, 1 after):
+// K = 4 kernel rows × (4 pixels × 16 channels) = 256, every tap row one 128-B
+// chunk of z, so the implicit GEMM (forward, BatchNorm statistics in the
+// epilogue) and the tap-group weight gradient run it with no 3-channel gathers
+// (MIOpen's igemm fwd / wrw solvers did, at ≈ 360 µs each for batch 256).
+namespace {
+
+// one z pixel (32 B) per thread from the two 12-B pixel pairs of x (4-B aligned: W even)
+__global__ __launch_bounds__(256) void stem_s2d_kernel(const bf16* __restrict__ x, bf16* __restrict__ z, int H, int W,
+                                                      long long npix) {
+  const int IW = W >> 1, IH = H >> 1;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < npix; i += (long long)gridDim.x * 256) {
+    const int j = (int)(i % IW);
+    const long long ni = i / IW;
+    const int ii = (int)(ni % IH);
+    const long long n = ni / IH;
+    const unsigned* r0 = reinterpret_cast<const unsigned*>(x + ((n * H + 2 * ii) * W + 2 * j) * 3);
+    const unsigned* r1 = r0 + (W * 3) / 2;
+    uint4 lo = {r0[0], r0[1], r0[2], r1[0]};
+    uint4 hi = {r1[1], r1[2], 0u, 0u};
+    uint4* o = reinterpret_cast<uint4*>(z + i * 16);
+    o[0] = lo;
+    o[1] = hi;
+  }
+}
+
+// w [Kout][7][7][3] (OHWI) → w2 [Kout][4 a][4 b][16 ch] (bf16)
+__global__ __launch_bounds__(256) void stem_weight_kernel(const bf16* __restrict__ w, bf16* __restrict__ w2, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int co = i >> 8, k = i & 255, aa = k >> 6, b = (k >> 4) & 3, ch = k & 15;
+  bf16 v = (bf16)0.f;
+  if (ch < 12) {
+    const int pq = ch / 3, c = ch - 3 * pq;
+    const int r = 2 * aa + (pq >> 1) - 1, s = 2 * b + (pq & 1) - 1;
+    if (r >= 0 && s >= 0) v = w[((co * 7 + r) * 7 + s) * 3 + c];
+  }
+  w2[i] = v;
+}
+
+// dw [Kout][7][7][3] fp32 (+)= the stem entries of dw2 [Kout][256]
+__global__ __launch_bounds__(256) void stem_dw_kernel(const float* __restrict__ dw2, float* __restrict__ dw, int n,
+                                                     int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = i % 3, rs = (i / 3) % 49, co = i / 147, r = rs / 7, s = rs - 7 * r;
+  const int aa = (r + 1) >> 1, p = (r + 1) & 1, b = (s + 1) >> 1, q = (s + 1) & 1;
+  const float v = dw2[co * 256 + aa * 64 + b * 16 + (2 * p + q) * 3 + c];
+  dw[i] = accumulate ? dw[i] + v : v;
+}
+
+// Persistent stem forward: 128-token × 64-channel tiles, a contiguous range of
+// tiles per workgroup (neighbouring tiles read the same z rows: one XCD's L2).
+// The K = 256 weight (32 KiB) stays in registers as MFMA B fragments for the
+// whole kernel; A (4 k-steps × 128 rows × 128 B = 64 KiB per tile) is double
+// buffered in LDS and the next tile's pieces are issued before this tile's
+// MFMAs, so their latency hides behind this tile's MFMAs and epilogue (the
+// 4-k-step tiles of conv_igemm_kernel waited out one load latency per k-step).
+constexpr int SBM = 128, STILE = 4 * SBM * 128;
+__global__ __launch_bounds__(CNT, 1) void stem_fwd_kernel(const ConvArgs a, int tiles_per_wg) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STILE + 4 * 64 * 4];
+  char* red = smem + 2 * STILE;  // the epilogue's [4][64] reduction rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long ntm = (a.M + SBM - 1) / SBM;
+  const long long t0 = (long long)blockIdx.x * tiles_per_wg;
+  const long long t1 = t0 + tiles_per_wg < ntm ? t0 + tiles_per_wg : ntm;
+  if (t0 >= t1) return;
+  // B fragment (k-step kt, half kk, block j): output channel 4(l & 15) + j (the
+  // epilogue's column order), k 64kt + 32kk + 8(l >> 4) .. +7
+  bf16x8 fb[4][2][4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[kt][kk][j] = *reinterpret_cast<const bf16x8*>(a.w + (4 * (lane & 15) + j) * 256 + 64 * kt + 32 * kk +
+                                                         8 * (lane >> 4));
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // tile tm's A into buffer b: pieces p = w + 4i, rows 8p + (l >> 3), one DMA per k-step (kernel row)
+  auto issue = [&](long long tm, int b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = w + 4 * i;
+      const int row = 8 * p + (lane >> 3);
+      const int cg = (lane & 7) ^ ((row >> 1) & 7);
+      const long long t = tm * SBM + row;
+      int hb = -(1 << 20), wl = 0, base = 0;
+      if (t < a.M) {
+        int q, ow, n, oh;
+        divmod((int)t, a.TB, a.inv_TB, q, ow);
+        divmod(q, a.TA, a.inv_TA, n, oh);
+        hb = oh - a.ipad;
+        base = ((n * a.IH + hb) * a.IW + ow - a.ipad) * 16 + cg * 8;
+        wl = ow - a.ipad + (cg >> 1);
+      }
+      const bool okw = (unsigned)wl < (unsigned)a.IW;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bool ok = okw && (unsigned)(hb + kt) < (unsigned)a.IH;
+        bufld(ok ? (unsigned)((base + kt * a.IW * 16) * 2) : OOB, rsX,
+              lds0 + (unsigned)(b * STILE + kt * SBM * 128 + p * 1024));
+      }
+    }
+  };
+  const int sw = (lane >> 1) & 7;
+  const int ch0 = ((lane >> 4) ^ sw) << 4, ch1 = ((4 + (lane >> 4)) ^ sw) << 4;
+  const int rA = (w * 32 + (lane & 15)) * 128;
+  issue(t0, 0);
+  for (long long tm = t0; tm < t1; ++tm) {
+    const int b = (int)((tm - t0) & 1);
+    if (tm + 1 < t1) {
+      issue(tm + 1, b ^ 1);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile tm landed (tile tm + 1 flies)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* st = smem + b * STILE;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(st + kt * SBM * 128 + rA + i * 2048 + (kk ? ch1 : ch0));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[kt][kk][j], acc[i][j], 0, 0, 0);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // buffer b's reads precede its refill (tile tm + 2, next iteration)
+    conv_epilogue<2, SBM, 64, 4>(a, acc, red, w, 0, lane, tm * SBM, tm, 0);
+  }
+}
+
+int stem_ncu() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      c = 256;
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+
+// PDO_STEM_FWD=0: the stem forward on conv_igemm_kernel (256-row tiles) instead
+int stem_fwd_mode() {
+  static const int m = [] {
+    const char* e = getenv("PDO_STEM_FWD");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return m;
+}
+
+// split count of the stem weight gradient: two workgroups per CU, ≥ 8 k-steps each
+int stem_splits(long long M) {
+  static const int env = [] {
+    const char* e = getenv("PDO_STEM_SPLITS");
+    return e && *e ? atoi(e) : 0;
+  }();
+  const long long ks = (M + 63) / 64;
+  long long sp = env > 0 ? env : 512;
+  if (sp > ks / 8) sp = ks / 8;
+  return sp < 1 ? 1 : (int)sp;
+}
+
+}  // namespace
+
+int stem_supported(int N, int H, int W, int C, int Kout) {
+  if (C != 3 || Kout != 64 || (H & 1) || (W & 1) || H < 8 || W < 8) return 0;
+  const long long M = (long long)N * (H / 2) * (W / 2);
+  return M < (1 << 24) && M * 16 * 2 < (1ll << 31) && M * Kout * 2 < (1ll << 31);
+}
+
+int stem_s2d(const bf16* x, int N, int H, int W, bf16* z, hipStream_t st) {
+  if (!stem_supported(N, H, W, 3, 64)) return -2;
+  const long long npix = (long long)N * (H / 2) * (W / 2);
+  stem_s2d_kernel<<<stream_grid(npix, 256), 256, 0, st>>>(x, z, H, W, npix);
+  return 0;
+}
+
+int stem_weight(const bf16* w, bf16* w2, int Kout, hipStream_t st) {
+  const int n = Kout * 256;
+  stem_weight_kernel<<<(n + 255) / 256, 256, 0, st>>>(w, w2, n);
+  return 0;
+}
+
+int stem_fwd(const bf16* z, int N, int IH, int IW, const bf16* w2, int Kout, bf16* y, float* tile_stats,
+             hipStream_t st) {
+  if (!stem_supported(N, 2 * IH, 2 * IW, 3, Kout)) return -2;
+  ConvArgs a{};
+  a.x = z;
+  a.w = w2;
+  a.y = y;
+  a.stats = tile_stats;
+  a.M = (long long)N * IH * IW;
+  a.C = 16;
+  a.Kout = Kout;
+  a.ldb = 256;
+  a.IH = IH;
+  a.IW = IW;
+  a.TA = IH;
+  a.TB = IW;
+  a.ist = 1;
+  a.ipad = 2;
+  a.OH = IH;
+  a.OW = IW;
+  a.ost = 1;
+  a.ident = 1;
+  a.xbytes = (unsigned)((long long)N * IH * IW * 16 * 2);
+  a.ntaps = 4;
+  for (int t = 0; t < 4; ++t) {
+    a.dh[t] = t;
+    a.dw[t] = 0;
+    a.bcol[t] = t * 64;
+  }
+  if (!stem_fwd_mode() || Kout != 64) return run_igemm(a, st, nullptr);
+  a.inv_TA = 1.f / (float)a.TA;
+  a.inv_TB = 1.f / (float)a.TB;
+  const long long ntm = (a.M + SBM - 1) / SBM;
+  const long long nwg = ntm < stem_ncu() ? ntm : stem_ncu();
+  const int per = (int)((ntm + nwg - 1) / nwg);
+  stem_fwd_kernel<<<(unsigned)((ntm + per - 1) / per), CNT, 0, st>>>(a, per);
+  return 0;
+}
+
+int stem_tile_rows() { return stem_fwd_mode() ? SBM : conv_fwd_tile_rows(64); }
+int stem_fwd_tiles(long long M) {
+  const int r = stem_tile_rows();
+  return (int)((M + r - 1) / r);
+}
+
+long long stem_wgrad_scratch_floats(int N, int IH, int IW, int Kout) {
+  return (long long)(stem_splits((long long)N * IH * IW) + 1) * Kout * 256;
+}
+
+// dw [Kout][7][7][3] fp32 (+)= the stem's weight gradient from dy [N][IH][IW][Kout] and z
+int stem_wgrad(const bf16* dy, const bf16* z, int N, int IH, int IW, int Kout, float* dw, int accumulate,
+               float* scratch, hipStream_t st) {
+  if (!stem_supported(N, 2 * IH, 2 * IW, 3, Kout)) return -2;
+  WgradTapsArgs g{};
+  g.dy = dy;
+  g.x = z;
+  g.part = scratch;
+  g.M = (long long)N * IH * IW;
+  g.IH = IH;
+  g.IW = IW;
+  g.TA = IH;
+  g.TB = IW;
+  g.inv_TA = 1.f / (float)IH;
+  g.inv_TB = 1.f / (float)IW;
+  g.st = 1;
+  g.pad = 2;
+  g.xbytes = (unsigned)(g.M * 16 * 2);
+  g.dybytes = (unsigned)(g.M * Kout * 2);
+  g.splits = stem_splits(g.M);
+  g.ksteps = (int)((g.M + 63) / 64);
+  conv_wgrad_taps_kernel<64, 4, true><<<(unsigned)g.splits, CNT, 0, st>>>(g);
+  float* dw2 = scratch + (size_t)g.splits * Kout * 256;
+  wgrad_fold(scratch, g.splits, Kout, 256, 256, dw2, 0, st);
+  const int n = Kout * 147;
+  stem_dw_kernel<<<(n + 255) / 256, 256, 0, st>>>(dw2, dw, n, accumulate);
   return 0;
 }
 

@@ -25,7 +25,8 @@
 //              through Y), and fp32 column partial sums of C for the bias
 //              gradient (one row per (M-tile, wave)) — the fc2 input-gradient
 //              GEMM with the bias-GELU backward pass fused
-//   EPI_ADD    C = A·Bᵀ + Y — an input gradient that joins another branch's
+//   EPI_ADD    C = A·Bᵀ + Y (EPI 5: + bias too — a projection writing the residual
+//              stream x + proj(a) + b) — or an input gradient that joins another branch's
 //              (ResNet's block input: conv1 dX + the identity / downsample dX)
 // Rounding matches the unfused path bit for bit: the GEMM result is rounded to
 // bf16 before the activation math, as when it made an HBM round trip.
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI == 1) {  // bias before the rounding, as a library bias epilogue
+    if constexpr (EPI == 1 || EPI == 5) {  // bias before the rounding, as a library bias epilogue
       const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * 64 + 16 * j + 4 * (lane >> 4));
       bv = f32x4{(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
     }
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 8; ++e) y[e] = gelu_sig(x[e]);
       *reinterpret_cast<bf16x8*>(Y + m * ldy + n) = to_bf16(y);
-    } else if constexpr (EPI == 4) {
+    } else if constexpr (EPI == 4 || EPI == 5) {
       // the addend joins after the bf16 staging: two roundings (the 4-wave path has one)
       const f32x8 r = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n));
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(to_f32(v) + r);
@@ -259,7 +260,7 @@ int gemm_nt_get_impl() { return g_impl; }
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
   if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
-  if (epi >= 1 && epi <= 3 && !bias) return -3;
+  if (((epi >= 1 && epi <= 3) || epi == 5) && !bias) return -3;
   if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
   if (nt4_path(K))
@@ -273,6 +274,7 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
     case 2: gemm_nt_kernel<2><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 3: gemm_nt_kernel<3><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 4: gemm_nt_kernel<4><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 5: gemm_nt_kernel<5><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     default: return -4;
   }
   return 0;

@@ -228,13 +228,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const int g4 = lane >> 4;
     const int nb = n0 + wn * 128 + 8 * (lane & 15);
     const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
-    bf16x8 pre[EPI >= 3 ? 32 : 1];  // EPI 3: the GELU pre-activation; EPI 4: the addend
+    bf16x8 pre[EPI >= 3 ? 32 : 1];  // EPI 3: the GELU pre-activation; EPI 4 / 5: the addend
     if constexpr (EPI >= 3) {
 #pragma unroll
       for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
     }
     f32x8 bv8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI >= 1 && EPI <= 3) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
+    if constexpr ((EPI >= 1 && EPI <= 3) || EPI == 5) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
     f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     f32x2 m1 = {-1.f, -1.f};
     asm volatile("" : "+v"(m1));
@@ -267,6 +267,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           st16(Y + m * ldy + nb, to_bf16(y));
         } else if constexpr (EPI == 4) {
           st16(crow, to_bf16(v + to_f32(pre[4 * i + e])));  // C = A·Bᵀ + Y, one rounding
+        } else if constexpr (EPI == 5) {
+          st16(crow, to_bf16(v + bv8 + to_f32(pre[4 * i + e])));  // C = A·Bᵀ + bias + Y (residual stream)
         } else {
           const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
           const f32x8& dy = v;  // the fp32 product, not its bf16 rounding
@@ -473,6 +475,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
       case 2: gemm_nt4_kernel<2, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       case 3: gemm_nt4_kernel<3, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       case 4: gemm_nt4_kernel<4, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 5: gemm_nt4_kernel<5, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       default: return -4;
     }
     return 0;

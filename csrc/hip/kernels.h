@@ -75,6 +75,18 @@ int bn_bwd_part(const float* part, int G, const bf16* dy, const bf16* y, const b
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad);
 int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st);
+// ResNet stem (7×7 / stride 2 / pad 3, 3 → Kout = 64 channels) as a space-to-depth
+// 4×4 stride-1 convolution over a 16-channel image on the implicit GEMM (conv.hip)
+int stem_supported(int N, int H, int W, int C, int Kout);
+int stem_s2d(const bf16* x, int N, int H, int W, bf16* z, hipStream_t st);
+int stem_weight(const bf16* w, bf16* w2, int Kout, hipStream_t st);
+int stem_fwd(const bf16* z, int N, int IH, int IW, const bf16* w2, int Kout, bf16* y, float* tile_stats,
+             hipStream_t st);
+long long stem_wgrad_scratch_floats(int N, int IH, int IW, int Kout);
+int stem_tile_rows();              // rows per BatchNorm statistics tile of stem_fwd
+int stem_fwd_tiles(long long M);
+int stem_wgrad(const bf16* dy, const bf16* z, int N, int IH, int IW, int Kout, float* dw, int accumulate,
+               float* scratch, hipStream_t st);
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
                  float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st, unsigned char* mask = nullptr);

@@ -106,18 +106,21 @@ class Block(nn.Module):
         self.fc = Linear(C, 4 * C)
         self.fc_proj = Linear(4 * C, C)
 
-    def forward(self, x, h):
+    def forward(self, x, h, ln_next_w, ln_next_b):
         """x: residual stream, h: LN1(x) already computed by the caller.
 
-        Returns (x_mid, m, fc_proj_bias): the MLP branch output ``m`` WITHOUT
-        its bias — the caller fuses ``x_mid + m + bias`` with the next LayerNorm.
+        Returns (x_out, LN_next(x_out)) — the next block's LN1 (or the final LN)
+        taken here, so each branch output joins the residual stream inside its
+        output projection's GEMM epilogue (bias and residual added there,
+        ops.linear_add_layer_norm / ops.mlp_add_layer_norm) and the following
+        LayerNorm reads the stream once.
         """
         cfg = self.cfg
         a = ops.qkv_attention(h, self.qkv.weight, self.qkv.bias, cfg.n_head)
-        a = self.proj.forward_nobias(a)
-        x, h2 = ops.add_layer_norm(x, a, self.ln2_w, self.ln2_b, cfg.ln_eps, rbias=self.proj.bias)
-        m = ops.mlp(h2, self.fc.weight, self.fc.bias, self.fc_proj.weight)
-        return x, m, self.fc_proj.bias
+        x, h2 = ops.linear_add_layer_norm(a, self.proj.weight, self.proj.bias, x, self.ln2_w, self.ln2_b,
+                                          cfg.ln_eps)
+        return ops.mlp_add_layer_norm(h2, self.fc.weight, self.fc.bias, self.fc_proj.weight, self.fc_proj.bias,
+                                      x, ln_next_w, ln_next_b, cfg.ln_eps)
 
 
 class GPT2(nn.Module):
@@ -160,12 +163,11 @@ class GPT2(nn.Module):
         blk0 = self.blocks[0]
         h = ops.layer_norm(x, blk0.ln1_w, blk0.ln1_b, cfg.ln_eps)
         for i, blk in enumerate(self.blocks):
-            x, m, mb = blk(x, h)
             if i + 1 < len(self.blocks):
                 nb = self.blocks[i + 1]
-                x, h = ops.add_layer_norm(x, m, nb.ln1_w, nb.ln1_b, cfg.ln_eps, rbias=mb)
+                x, h = blk(x, h, nb.ln1_w, nb.ln1_b)
             else:
-                x, h = ops.add_layer_norm(x, m, self.lnf_w, self.lnf_b, cfg.ln_eps, rbias=mb)
+                x, h = blk(x, h, self.lnf_w, self.lnf_b)
         if targets is None:
             return ops.linear(h, self.wte)[..., :cfg.vocab_size]
         return ops.lm_head_xent(h, self.wte, targets, cfg.vocab_size)

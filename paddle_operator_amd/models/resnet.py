@@ -2,8 +2,9 @@
 elastic ResNet-50) — written out here because torchvision is not part of the
 image.  Standard v1.5 bottleneck architecture (stride on the 3×3 conv).
 
-MI355X choices: channels_last bf16 activations; every convolution but the 7×7
-stem (3 input channels, MIOpen) on hand-written kernels — the NHWC implicit GEMM
+MI355X choices: channels_last bf16 activations; every convolution on
+hand-written kernels — the 7×7 stem as a space-to-depth 4×4 convolution over a
+16-channel image (ops._StemFn), the rest on the NHWC implicit GEMM
 (csrc/hip/conv.hip: BatchNorm forward statistics from its epilogue, the previous
 BatchNorm's backward statistics from its input-gradient epilogue) or, per
 product where measured faster, the token-major GEMMs (gemm_nt4 / gemm_dw4) for
@@ -83,7 +84,7 @@ class ResNet(nn.Module):
                 nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x):
-        x = ops.bn_act(self.bn1, self.conv1(x))
+        x = ops.conv_bn_act(self.conv1, self.bn1, x)  # the space-to-depth stem on the HIP path
         x = ops.max_pool_3x3s2(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

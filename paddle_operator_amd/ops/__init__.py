@@ -150,6 +150,92 @@ def add_layer_norm(x, r, w, b, eps=1e-5, rbias=None):
     return h, F.layer_norm(h, (h.shape[-1],), w, b, eps)
 
 
+class _LNResFn(torch.autograd.Function):
+    """(h, LN(h)) for a residual-stream tensor h that the producing GEMM already
+    summed (x + proj(a) + bias in its epilogue, _LinearResFn / _NTMLPFn): the
+    LayerNorm reads h once and writes y — no second input read and no h write
+    (_AddLayerNormFn's x + r pass).  h is returned as an alias so the
+    downstream residual gradient reaches this backward and joins the
+    LayerNorm's in one kernel (layernorm_bwd_add), which also reduces the
+    gradient of the producer's bias (``rbias``: added in the GEMM, its gradient
+    — the column sum of dh — taken here)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, rbias, eps):
+        m = _native.require_hip()
+        h2 = h.reshape(-1, h.shape[-1])
+        y, mean, rstd = m.layernorm_fwd(h2, w, b, eps)
+        ctx.save_for_backward(h2, w, mean, rstd)
+        ctx.shape = h.shape
+        ctx.has_rbias = rbias is not None
+        ctx.params = (w, b, rbias) if rbias is not None else (w, b)
+        return h, y.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        m = _native.require_hip()
+        h2, w, mean, rstd = ctx.saved_tensors
+        gd = _arena_grads(ctx.params)
+        dh2 = dh.reshape(h2.shape).contiguous() if dh is not None else torch.zeros_like(h2)
+        outs = m.layernorm_bwd_add(dy.reshape(h2.shape).contiguous(), h2, w, mean, rstd, dh2, ctx.has_rbias,
+                                   grads=gd)
+        dx = outs[0].view(ctx.shape)
+        if gd is not None:
+            _signal_ready(ctx.params)
+            return dx, None, None, None, None
+        return dx, outs[1], outs[2], (outs[3] if ctx.has_rbias else None), None
+
+
+class _LinearResFn(torch.autograd.Function):
+    """h = a·Wᵀ + b + x on gemm_nt4's EPI 5 (bias and the residual stream x
+    summed in the register epilogue, one rounding).  ``b`` is taken as a
+    constant here: its gradient is reduced by the LayerNorm that consumes h
+    (_LNResFn's rbias).  Backward: dA, dW as _LinearFn; dx = dh."""
+
+    @staticmethod
+    def forward(ctx, a, w, b, x):
+        m = _native.require_hip()
+        a2 = a.reshape(-1, a.shape[-1])
+        h = m.gemm_nt_add(a2, w, x.reshape(-1, x.shape[-1]), bias=b)
+        ctx.save_for_backward(a2, w)
+        ctx.shape = a.shape
+        return h.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dh):
+        a2, w = ctx.saved_tensors
+        dh2 = dh.reshape(-1, dh.shape[-1]).contiguous()
+        da = _input_grad(dh2, w).view(ctx.shape) if ctx.needs_input_grad[0] else None
+        dw = _weight_grad(w, dh2, a2) if ctx.needs_input_grad[1] else None
+        return da, dw, None, dh
+
+
+_RES_EPI = [os.environ.get("PDO_RES_EPI", "1") != "0"]
+
+
+def _res_epi_ok(T, w, x) -> bool:
+    """The residual-stream GEMM epilogue applies to [T, K]·Wᵀ → [T, N] + x: bf16
+    contiguous operands on the 4-wave gemm_nt4 path (K % 128, K ≥ 256) within
+    its shape contract."""
+    N, K = w.shape
+    if not (_RES_EPI[0] and use_hip(x) and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and w.is_contiguous() and x.is_contiguous() and x.numel() == T * N):
+        return False
+    return K % 128 == 0 and K >= 256 and bool(_native.require_hip().gemm_nt_supported(T, N, K))
+
+
+def linear_add_layer_norm(a, w, b, x, ln_w, ln_b, eps=1e-5):
+    """(h, LN(h)) with h = x + a·Wᵀ + b — GPT-2's attention output projection
+    joining the residual stream: the sum in the GEMM epilogue (_LinearResFn)
+    and a one-input LayerNorm (_LNResFn) where the shapes allow, else the GEMM
+    + the fused add+LayerNorm pass."""
+    if (a.is_cuda and a.dtype == torch.bfloat16 and a.is_contiguous()
+            and _res_epi_ok(a.numel() // a.shape[-1], w, x)):
+        hs = _LinearResFn.apply(a, w, b.detach(), x)
+        return _LNResFn.apply(hs, ln_w, ln_b, b, eps)
+    return add_layer_norm(x, linear(a, w), ln_w, ln_b, eps, rbias=b)
+
+
 # ----------------------------------------------------------------------------
 # linear with direct-to-arena weight gradient
 # ----------------------------------------------------------------------------
@@ -441,16 +527,24 @@ class _NTMLPFn(torch.autograd.Function):
     re-read by a separate bias-GELU pass.  Backward = _GeluLinearFn's fused
     dGELU epilogue plus fc1's dW / dX.  Measured at [65536, 1024] → 4096 on
     1×MI355X: 598.7 µs vs 644.5 µs for hipBLASLt + bias_gelu_fwd
-    (tools/nt4_probe.py fc1_fwd, profiles/r2_gemm_nt4.md)."""
+    (tools/nt4_probe.py fc1_fwd, profiles/r2_gemm_nt4.md).
+
+    ``res``/``b2`` (optional): the fc2 GEMM also adds its bias and the residual
+    stream in the epilogue (gemm_nt4 EPI 5), returning x_res + m + b2 for a
+    one-input LayerNorm (_LNResFn, which takes b2's gradient); the residual's
+    gradient is dy itself."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2):
+    def forward(ctx, x, w1, b1, w2, b2=None, res=None):
         m = _native.require_hip()
         x2 = x.reshape(-1, x.shape[-1])
         hp, h = m.gemm_nt_gelu(x2, w1, b1)
         ctx.save_for_backward(x2, w1, hp, h, w2)
         ctx.b1 = b1
         ctx.shape = x.shape
+        ctx.res = res is not None
+        if res is not None:
+            return m.gemm_nt_add(h, w2, res.reshape(-1, res.shape[-1]), bias=b2).view(res.shape)
         return _fwd_gemm(h, w2).view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
@@ -469,7 +563,7 @@ class _NTMLPFn(torch.autograd.Function):
             dhp, db1 = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1)
         dw1 = _weight_grad(w1, dhp, x2) if ctx.needs_input_grad[1] else None  # its bucket can go first
         dx = _input_grad(dhp, w1).view(ctx.shape) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1, dw2
+        return dx, dw1, db1, dw2, None, (dy if ctx.res else None)
 
 
 # fc1 forward with the fused GELU epilogue (gemm_nt): on by default since the
@@ -500,11 +594,25 @@ def mlp(x, w1, b1, w2):
     if (_NT_GELU[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.is_contiguous()
             and _nt_dgelu_ok(x, w2)
             and _native.require_hip().gemm_nt_supported(x.numel() // x.shape[-1], w1.shape[0], w1.shape[1])):
-        return _NTMLPFn.apply(x, w1, b1, w2)
+        return _NTMLPFn.apply(x, w1, b1, w2, None, None)
     hp = linear(x, w1)
     if use_hip(hp) and _nt_dgelu_ok(hp, w2):
         return _GeluLinearFn.apply(hp, b1, w2)
     return linear(bias_gelu(hp, b1), w2)
+
+
+def mlp_add_layer_norm(x, w1, b1, w2, b2, res, ln_w, ln_b, eps=1e-5):
+    """(h, LN(h)) with h = res + mlp(x) + b2 — GPT-2's MLP output joining the
+    residual stream: fc2's GEMM epilogue adds b2 and res (_NTMLPFn with res) and
+    the LayerNorm reads h once (_LNResFn) where the shapes allow, else
+    mlp() + the fused add+LayerNorm pass."""
+    T = x.numel() // x.shape[-1]
+    if (_NT_GELU[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.is_contiguous()
+            and _nt_dgelu_ok(x, w2) and _native.require_hip().gemm_nt_supported(T, w1.shape[0], w1.shape[1])
+            and _res_epi_ok(T, w2, res)):
+        hs = _NTMLPFn.apply(x, w1, b1, w2, b2.detach(), res)
+        return _LNResFn.apply(hs, ln_w, ln_b, b2, eps)
+    return add_layer_norm(res, mlp(x, w1, b1, w2), ln_w, ln_b, eps, rbias=b2)
 
 
 def bias_gelu(x, b):
@@ -1092,6 +1200,59 @@ def conv1x1(conv: torch.nn.Conv2d, x):
     return conv(x)
 
 
+class _StemFn(torch.autograd.Function):
+    """ResNet's 7×7 / stride-2 / pad-3 stem convolution (3 → 64 channels) for a
+    channels_last bf16 image, as a space-to-depth 4×4 stride-1 convolution over a
+    16-channel image (csrc/hip/conv.hip, stem_*): forward on the implicit GEMM
+    with the BatchNorm tile statistics in its epilogue, weight gradient on the
+    tap-group kernel (dY staged once for the four kernel rows).  The image needs
+    no gradient.  Replaces MIOpen's igemm fwd / wrw solvers on 3-channel input
+    (≈ 360 µs each at batch 256, profiles/r4p_resnet50_kernels.md)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        m = _native.require_hip()
+        sh = getattr(w, "_pdo_shadow", None)
+        if sh is not None and sh[0].shadow_live and sh[1].dtype == torch.bfloat16 \
+                and sh[1].is_contiguous(memory_format=torch.channels_last):
+            wb = sh[1]
+        else:
+            wb = w.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y, st, z = m.stem_fwd(x, wb, True)
+        ctx.save_for_backward(z)
+        ctx.wparam = w
+        ctx.mark_non_differentiable(st)
+        return y, st
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        m = _native.require_hip()
+        (z,) = ctx.saved_tensors
+        p = ctx.wparam
+        dw = None
+        if dy is not None and ctx.needs_input_grad[1]:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+            if _direct_ok(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous(memory_format=torch.channels_last):
+                m.stem_wgrad(dy, z, p.grad)
+                p._pdo_ready(p)
+            else:
+                dw = m.stem_wgrad(dy, z).to(p.dtype)
+        return None, dw
+
+
+_HIP_STEM = [os.environ.get("PDO_HIP_STEM", "1") != "0"]
+
+
+def _stem_ok(conv: torch.nn.Conv2d, x) -> bool:
+    if not (_HIP_CONV[0] and _HIP_STEM[0] and use_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 4 and not x.requires_grad
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.groups == 1 and conv.bias is None
+            and conv.dilation == (1, 1) and tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2)
+            and tuple(conv.padding) == (3, 3)):
+        return False
+    N, C, H, W = x.shape
+    return bool(_native.require_hip().stem_ok(N, H, W, C, conv.out_channels))
+
+
 def _bn_fused_ok(bn: torch.nn.BatchNorm2d, residual) -> bool:
     return (bn.training and _BN_FUSED[0] and bn.weight is not None and bn.weight.dtype == torch.float32
             and (residual is None or (residual.dtype == torch.bfloat16
@@ -1105,13 +1266,19 @@ def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool =
     runs the forward; otherwise the framework convolution + ops.bn_act.
     ``fork``: returns (out, x_alias) — x for a second consumer whose gradient
     then joins this convolution's dX in its epilogue (_ConvFn)."""
-    if _hip_conv_ok(conv, x) and _bn_fused_ok(bn, residual):
-        y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork)
+    stem = not fork and _stem_ok(conv, x)
+    if (stem or _hip_conv_ok(conv, x)) and _bn_fused_ok(bn, residual):
+        if stem:
+            y, st = _StemFn.apply(x, conv.weight)
+            xa = None
+        else:
+            y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork)
         if st is None:
             out = bn_act(bn, y, relu=relu, residual=residual)
         else:
             mom = bn.momentum if bn.momentum is not None else 0.1
-            rows = _native.require_hip().conv_tile_rows(conv.out_channels)
+            m = _native.require_hip()
+            rows = m.stem_tile_rows() if stem else m.conv_tile_rows(conv.out_channels)
             link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
             out = _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom,
                                  relu, st, rows, link)

@@ -289,3 +289,76 @@ def test_conv_wgrad_tap_groups(hip, N, C, H, stride):
         hip.conv_wgrad_c64_mode(prev)
     assert _rel(dw, wf.grad) < 5e-3
     assert _rel(dw, dw1) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 30, 30), (2, 64, 48), (1, 8, 14)])
+def test_stem_space_to_depth(hip, N, H, W):
+    """The 7×7 / stride-2 / pad-3 stem as a 4×4 stride-1 convolution over the
+    16-channel space-to-depth image: output and BatchNorm tile statistics vs
+    fp32 F.conv2d, weight gradient (fresh and accumulated) vs fp32 autograd;
+    token counts with a partial last tile / k-step (3 × 15 × 15, 1 × 4 × 7)."""
+    g = torch.Generator(device="cuda").manual_seed(H + W)
+    x = torch.randn(N, 3, H, W, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) / 147 ** 0.5).bfloat16()
+    w = w.contiguous(memory_format=torch.channels_last)
+    assert hip.stem_ok(N, H, W, 3, 64)
+    y, st, z = hip.stem_fwd(x, w, True)
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, stride=2, padding=3)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert z.shape == (N, 16, H // 2, W // 2)
+    assert _rel(y, ref) < 1e-2
+    rows = hip.stem_tile_rows()
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    M = yf.shape[0]
+    assert st.shape == ((M + rows - 1) // rows, 2, 64)
+    mean = st[:, 0].sum(0) / M
+    n = torch.tensor([min(rows, M - i * rows) for i in range(st.shape[0])], device="cuda", dtype=torch.float32)
+    var = (st[:, 1].sum(0) + (n[:, None] * (st[:, 0] / n[:, None] - mean) ** 2).sum(0)) / M
+    torch.testing.assert_close(mean, yf.mean(0), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(var, yf.var(0, unbiased=False), rtol=1e-3, atol=1e-5)
+    dy = torch.randn(ref.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    ref.backward(dy.float())
+    dw = hip.stem_wgrad(dy, z)
+    assert dw.shape == w.shape and dw.dtype == torch.float32
+    assert _rel(dw, wf.grad) < 5e-3
+    base = torch.randn_like(dw).contiguous(memory_format=torch.channels_last)
+    acc = base.clone()
+    hip.stem_wgrad(dy, z, acc)
+    assert _rel(acc - base, wf.grad) < 5e-3
+
+
+def test_resnet_stem_hip_path_matches_framework_conv():
+    """ResNet-50's stem block (conv1 → bn1 → ReLU → max-pool) on the
+    space-to-depth kernels and on the framework convolution (both bf16), each
+    against the same block in fp32: the HIP path's output and conv / BatchNorm
+    parameter gradients are as close to fp32 as the framework's (the conv
+    weight gradient sums a BatchNorm-centred dY over every pixel, so both bf16
+    paths sit a few % off fp32 there)."""
+    import copy
+
+    from paddle_operator_amd import ops
+
+    torch.manual_seed(0)
+    a = torch.nn.ModuleDict({"conv1": torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
+                             "bn1": torch.nn.BatchNorm2d(64)}).cuda().to(memory_format=torch.channels_last)
+    torch.nn.init.uniform_(a["bn1"].weight, 0.5, 1.5)
+    b, c = copy.deepcopy(a), copy.deepcopy(a)
+    x = torch.randn(4, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for mod, hip_conv, xin in ((a, True, x), (b, False, x), (c, False, x.float())):
+        prev = ops._HIP_CONV[0]
+        ops._HIP_CONV[0] = hip_conv
+        try:
+            assert ops._stem_ok(mod["conv1"], xin) == hip_conv
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=xin.dtype == torch.bfloat16):
+                y = ops.max_pool_3x3s2(ops.conv_bn_act(mod["conv1"], mod["bn1"], xin))
+            (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        finally:
+            ops._HIP_CONV[0] = prev
+        outs.append(y)
+    assert _rel(outs[0], outs[2]) < 2e-2 and _rel(outs[1], outs[2]) < 2e-2
+    for (n, pa), (_, pb), (_, pc) in zip(a.named_parameters(), b.named_parameters(), c.named_parameters()):
+        e_hip, e_fw = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
+        assert e_hip < 1.5 * e_fw + 1e-2, (n, e_hip, e_fw)
+    torch.testing.assert_close(a["bn1"].running_mean, c["bn1"].running_mean, rtol=1e-2, atol=1e-3)

@@ -728,3 +728,54 @@ def test_gemm_dw_mainloops_agree(cuda, T, M, N, acc):
             assert rel_err(out, ref) < 1e-2, (impl, m.gemm_dw_splits(T, M, N))
     finally:
         m.gemm_dw_impl(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,N,K", [(4096, 1024, 1024), (2048, 512, 4096), (1024, 256, 128)])
+def test_gemm_nt_add_bias(cuda, T, N, K):
+    """c = a·bᵀ + bias + r (gemm_nt EPI 5) on the 4-wave mainloop (K ≥ 256) and
+    the 8-wave ring (K = 128) against fp32."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    g = torch.Generator(device=cuda).manual_seed(T + K)
+    a = torch.randn(T, K, device=cuda, generator=g).bfloat16()
+    b = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g).bfloat16()
+    r = torch.randn(T, N, device=cuda, generator=g).bfloat16()
+    c = m.gemm_nt_add(a, b, r, bias=bias)
+    assert rel_err(c, a.float() @ b.float().t() + bias.float() + r.float()) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["proj", "mlp"])
+def test_residual_epilogue_layernorm_matches_unfused(cuda, which):
+    """The residual stream joined inside the output projection's GEMM epilogue
+    (bias + x added there, a one-input LayerNorm after: ops.linear_add_layer_norm
+    / ops.mlp_add_layer_norm) == the GEMM + fused add+LayerNorm path, for (h, y)
+    and every input / parameter gradient."""
+    ops = _ops()
+    T, C = 4096, 512
+    g = torch.Generator(device=cuda).manual_seed(11)
+    mk = lambda *s, sc=1.0: (sc * torch.randn(*s, device=cuda, generator=g)).bfloat16()  # noqa: E731
+    if which == "proj":
+        base = [mk(T, C), mk(C, C, sc=0.05), mk(C, sc=0.1), mk(T, C), 1 + mk(C, sc=0.1), mk(C, sc=0.1)]
+        fn = ops.linear_add_layer_norm
+    else:
+        base = [mk(T, C), mk(4 * C, C, sc=0.05), mk(4 * C, sc=0.1), mk(C, 4 * C, sc=0.05), mk(C, sc=0.1),
+                mk(T, C), 1 + mk(C, sc=0.1), mk(C, sc=0.1)]
+        fn = ops.mlp_add_layer_norm
+    dh, dy = mk(T, C), mk(T, C)
+    outs, grads = [], []
+    for fused in (True, False):
+        ops._RES_EPI[0] = fused
+        try:
+            ts = [t.clone().requires_grad_() for t in base]
+            h, y = fn(*ts)
+            torch.autograd.backward([h, y], [dh, dy])
+        finally:
+            ops._RES_EPI[0] = True
+        outs.append((h.detach().float(), y.detach().float()))
+        grads.append([t.grad.float() for t in ts])
+    assert rel_err(outs[0][0], outs[1][0]) < 1e-2 and rel_err(outs[0][1], outs[1][1]) < 1e-2
+    for i, (a, b) in enumerate(zip(grads[0], grads[1])):
+        assert rel_err(a, b) < 2e-2, i
