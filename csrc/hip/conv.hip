@@ -182,6 +182,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI
   if (!a.stats && !bnb) return;
   const int rows = (int)(a.M - m0 < BM ? a.M - m0 : BM);
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN] (the last k-step's barrier freed the stages)
+  // LDS-only barriers (lgkmcnt, no memory fence): __syncthreads() would also
+  // wait for every global store of this epilogue and, in the persistent stem
+  // kernel, for the next tile's LDS-DMA pieces (vmcnt(0))
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
   auto tile_sum = [&](float (&v)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -192,7 +199,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI
 #pragma unroll
       for (int j = 0; j < 4; ++j) red[wm * BN + wn * 64 + 4 * lane + j] = v[j];
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float s = 0.f;
@@ -200,7 +207,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI
       for (int u = 0; u < WM; ++u) s += red[u * BN + wn * 64 + 4 * (lane & 15) + j];
       v[j] = s;
     }
-    __syncthreads();
+    lds_barrier();
   };
   if (bnb) {
     // ---- BatchNorm backward partials of this M-tile: Σg, Σg·(x − mean) per channel
@@ -1132,120 +1139,6 @@ __global__ __launch_bounds__(256) void stem_dw_kernel(const float* __restrict__ 
   dw[i] = accumulate ? dw[i] + v : v;
 }
 
-// Persistent stem forward: 128-token × 64-channel tiles, a contiguous range of
-// tiles per workgroup (neighbouring tiles read the same z rows: one XCD's L2).
-// The K = 256 weight (32 KiB) stays in registers as MFMA B fragments for the
-// whole kernel; A (4 k-steps × 128 rows × 128 B = 64 KiB per tile) is double
-// buffered in LDS and the next tile's pieces are issued before this tile's
-// MFMAs, so their latency hides behind this tile's MFMAs and epilogue (the
-// 4-k-step tiles of conv_igemm_kernel waited out one load latency per k-step).
-constexpr int SBM = 128, STILE = 4 * SBM * 128;
-__global__ __launch_bounds__(CNT, 1) void stem_fwd_kernel(const ConvArgs a, int tiles_per_wg) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STILE + 4 * 64 * 4];
-  char* red = smem + 2 * STILE;  // the epilogue's [4][64] reduction rows
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long long ntm = (a.M + SBM - 1) / SBM;
-  const long long t0 = (long long)blockIdx.x * tiles_per_wg;
-  const long long t1 = t0 + tiles_per_wg < ntm ? t0 + tiles_per_wg : ntm;
-  if (t0 >= t1) return;
-  // B fragment (k-step kt, half kk, block j): output channel 4(l & 15) + j (the
-  // epilogue's column order), k 64kt + 32kk + 8(l >> 4) .. +7
-  bf16x8 fb[4][2][4];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fb[kt][kk][j] = *reinterpret_cast<const bf16x8*>(a.w + (4 * (lane & 15) + j) * 256 + 64 * kt + 32 * kk +
-                                                         8 * (lane >> 4));
-  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
-  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  // tile tm's A into buffer b: pieces p = w + 4i, rows 8p + (l >> 3), one DMA per k-step (kernel row)
-  auto issue = [&](long long tm, int b) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = w + 4 * i;
-      const int row = 8 * p + (lane >> 3);
-      const int cg = (lane & 7) ^ ((row >> 1) & 7);
-      const long long t = tm * SBM + row;
-      int hb = -(1 << 20), wl = 0, base = 0;
-      if (t < a.M) {
-        int q, ow, n, oh;
-        divmod((int)t, a.TB, a.inv_TB, q, ow);
-        divmod(q, a.TA, a.inv_TA, n, oh);
-        hb = oh - a.ipad;
-        base = ((n * a.IH + hb) * a.IW + ow - a.ipad) * 16 + cg * 8;
-        wl = ow - a.ipad + (cg >> 1);
-      }
-      const bool okw = (unsigned)wl < (unsigned)a.IW;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const bool ok = okw && (unsigned)(hb + kt) < (unsigned)a.IH;
-        bufld(ok ? (unsigned)((base + kt * a.IW * 16) * 2) : OOB, rsX,
-              lds0 + (unsigned)(b * STILE + kt * SBM * 128 + p * 1024));
-      }
-    }
-  };
-  const int sw = (lane >> 1) & 7;
-  const int ch0 = ((lane >> 4) ^ sw) << 4, ch1 = ((4 + (lane >> 4)) ^ sw) << 4;
-  const int rA = (w * 32 + (lane & 15)) * 128;
-  issue(t0, 0);
-  for (long long tm = t0; tm < t1; ++tm) {
-    const int b = (int)((tm - t0) & 1);
-    if (tm + 1 < t1) {
-      issue(tm + 1, b ^ 1);
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile tm landed (tile tm + 1 flies)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    f32x4 acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const char* st = smem + b * STILE;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 fa[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8*>(st + kt * SBM * 128 + rA + i * 2048 + (kk ? ch1 : ch0));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[kt][kk][j], acc[i][j], 0, 0, 0);
-      }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // buffer b's reads precede its refill (tile tm + 2, next iteration)
-    conv_epilogue<2, SBM, 64, 4>(a, acc, red, w, 0, lane, tm * SBM, tm, 0);
-  }
-}
-
-int stem_ncu() {
-  static const int n = [] {
-    int dev = 0, c = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      c = 256;
-    return c > 0 ? c : 256;
-  }();
-  return n;
-}
-
-// PDO_STEM_FWD=0: the stem forward on conv_igemm_kernel (256-row tiles) instead
-int stem_fwd_mode() {
-  static const int m = [] {
-    const char* e = getenv("PDO_STEM_FWD");
-    return e && *e ? atoi(e) : 1;
-  }();
-  return m;
-}
-
 // split count of the stem weight gradient: two workgroups per CU, ≥ 8 k-steps each
 int stem_splits(long long M) {
   static const int env = [] {
@@ -1308,21 +1201,11 @@ int stem_fwd(const bf16* z, int N, int IH, int IW, const bf16* w2, int Kout, bf1
     a.dw[t] = 0;
     a.bcol[t] = t * 64;
   }
-  if (!stem_fwd_mode() || Kout != 64) return run_igemm(a, st, nullptr);
-  a.inv_TA = 1.f / (float)a.TA;
-  a.inv_TB = 1.f / (float)a.TB;
-  const long long ntm = (a.M + SBM - 1) / SBM;
-  const long long nwg = ntm < stem_ncu() ? ntm : stem_ncu();
-  const int per = (int)((ntm + nwg - 1) / nwg);
-  stem_fwd_kernel<<<(unsigned)((ntm + per - 1) / per), CNT, 0, st>>>(a, per);
-  return 0;
+  return run_igemm(a, st, nullptr);
 }
 
-int stem_tile_rows() { return stem_fwd_mode() ? SBM : conv_fwd_tile_rows(64); }
-int stem_fwd_tiles(long long M) {
-  const int r = stem_tile_rows();
-  return (int)((M + r - 1) / r);
-}
+int stem_tile_rows() { return conv_fwd_tile_rows(64); }
+int stem_fwd_tiles(long long M) { return conv_fwd_tiles(M, 64); }
 
 long long stem_wgrad_scratch_floats(int N, int IH, int IW, int Kout) {
   return (long long)(stem_splits((long long)N * IH * IW) + 1) * Kout * 256;
