@@ -34,10 +34,17 @@ def short(name: str) -> str:
     return name[:120].replace("|", "/")
 
 
+def _is_opt(name: str) -> bool:
+    """One fused optimizer dispatch per training step: AdamW (GPT-2) or the
+    momentum-SGD pass (ResNet-50)."""
+    return "adamw" in name or "sgd_kernel" in name
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--steps", type=int, default=0, help="traced steps (0: count the AdamW dispatches)")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="traced steps (0: count the optimizer dispatches: fused AdamW or fused SGD)")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--title", default="")
     a = ap.parse_args()
@@ -54,7 +61,7 @@ def main():
     if a.steps <= 0:
         # traced steps = optimizer dispatches (one fused AdamW per step); a plain
         # trace without an optimizer has no step column
-        a.steps = sum(1 for r in rows if "adamw" in r[0])
+        a.steps = sum(1 for r in rows if _is_opt(r[0]))
     print(f"# rocprofv3 kernel summary {a.title}\n")
     if a.steps:
         print(f"ms/step = total ms / {a.steps} traced steps (optimizer dispatches)\n")
@@ -72,7 +79,7 @@ def main():
     # device idle inside the steady-state steps: steps end at the optimizer kernel
     # (one adamw dispatch per step); between the 2nd and the last one, busy = the
     # union of kernel intervals, idle = span - busy (launch gaps, host stalls)
-    ends = sorted(r[3] for r in rows if "adamw" in r[0])
+    ends = sorted(r[3] for r in rows if _is_opt(r[0]))
     if len(ends) >= 4:
         lo, hi = ends[1], ends[-1]
         iv = sorted((max(s, lo), min(e, hi)) for _, _, s, e in rows if e > lo and s < hi)
