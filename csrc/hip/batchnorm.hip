@@ -392,6 +392,148 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __r
   }
 }
 
+// ---------------------------------------------------------------------------
+// ResNet stem: BatchNorm + ReLU + 3×3 / stride-2 / pad-1 max-pool in one pass
+// each way.  Forward reads the conv output x once and writes only the pooled
+// activation, its window positions and the BatchNorm input at each maximum
+// (xsel; the unfused pair wrote and re-read the full-resolution activation).
+// A gradient reaches only window maxima, so the backward's statistics
+// (Σg, Σg·(x − mean), g = dy·[y > 0]) are bn_bwd_stats over the POOLED tensors
+// (dy, y, xsel: 1/4 of the pixels); its apply pass gathers the ≤ 4 window
+// gradients per input pixel (maxpool3s2_bwd's gather) straight into the
+// BatchNorm input gradient.  C / 8 must divide 256 (a lane's channel chunk is
+// fixed along its loop).
+typedef uint8_t u8x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(256) void bn_relu_pool_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ ss,
+                                                               int N, int H, int W, int C, int OH, int OW,
+                                                               bf16* __restrict__ y, uint8_t* __restrict__ arg,
+                                                               bf16* __restrict__ xsel) {
+  // flat grid-stride over (n, oh, ow, c8): rows of OW·C8 chunks do not fill 256 lanes evenly
+  const int C8 = C / 8;
+  const int c8 = threadIdx.x % C8;
+  Affine a;
+  a.sc = *reinterpret_cast<const f32x8*>(ss + c8 * 8);
+  a.sh = *reinterpret_cast<const f32x8*>(ss + C + c8 * 8);
+  const int total = N * OH * OW * C8;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+    const int t = j / C8, ow = t % OW, t2 = t / OW, oh = t2 % OH, n = t2 / OH;
+    const bf16* xn = x + (long long)n * H * W * C;
+    f32x8 best, xb;
+    u8x8 pos;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      best[q] = -INFINITY;
+      xb[q] = 0.f;
+      pos[q] = 0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = oh * 2 - 1 + kh;
+      if (h < 0 || h >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = ow * 2 - 1 + kw;
+        if (w < 0 || w >= W) continue;
+        const f32x8 xv = to_f32(*reinterpret_cast<const bf16x8*>(xn + ((long long)h * W + w) * C + c8 * 8));
+        f32x8 v = preact(xv, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+        v = to_f32(to_bf16(v));  // compare the bf16 activations, as the unfused max-pool does
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (v[q] > best[q]) {  // first maximum in scan order wins ties
+            best[q] = v[q];
+            xb[q] = xv[q];
+            pos[q] = (uint8_t)(kh * 3 + kw);
+          }
+        }
+      }
+    }
+    reinterpret_cast<bf16x8*>(y)[j] = to_bf16(best);  // j = ((n·OH + oh)·OW + ow)·C8 + c8
+    reinterpret_cast<u8x8*>(arg)[j] = pos;
+    reinterpret_cast<bf16x8*>(xsel)[j] = to_bf16(xb);  // exact: xb is a bf16 input value
+  }
+}
+
+// backward apply: a thread per 2 × 2 input block (rows 2k, 2k+1, columns 2m,
+// 2m+1) and 8 channels — exactly the windows (k | k+1, m | m+1) reach it, so
+// each window's dy / position vector is loaded once for the four pixels
+// (pixel (2k+a, 2m+b) takes window (k+i, m+j) for i ≤ a, j ≤ b, at position
+// (2 − 2i + ... ) = (a + 1 − 2i)·3 + (b + 1 − 2j)); g = the summed window
+// gradients, ReLU-masked; dx = k·g − k1 − k2·(x − μ).  One block per row pair.
+__global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(const bf16* __restrict__ dy,
+                                                                const uint8_t* __restrict__ arg,
+                                                                const bf16* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ wgt,
+                                                                const float* __restrict__ bia,
+                                                                const float* __restrict__ coef, int N, int H, int W,
+                                                                int C, int OH, int OW, bf16* __restrict__ dx) {
+  const int C8 = C / 8;
+  const int KH = (H + 1) / 2, MW = (W + 1) / 2;
+  const int c8 = threadIdx.x % C8;
+  const f32x8 mu = *reinterpret_cast<const f32x8*>(mean + c8 * 8);
+  const Affine a = affine8(mu, *reinterpret_cast<const f32x8*>(invstd + c8 * 8), wgt + c8 * 8, bia + c8 * 8);
+  const f32x8 k = *reinterpret_cast<const f32x8*>(coef + c8 * 8);
+  const f32x8 k1 = *reinterpret_cast<const f32x8*>(coef + C + c8 * 8);
+  const f32x8 k2 = *reinterpret_cast<const f32x8*>(coef + 2 * C + c8 * 8);
+  const int total = N * KH * MW * C8;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < total; j += gridDim.x * 256) {
+    const int t = j / C8, m = t % MW, t2 = t / MW, kr = t2 % KH, n = t2 / KH;
+    const bf16* xn = x + (long long)n * H * W * C;
+    bf16* dxn = dx + (long long)n * H * W * C;
+    const long long on = (long long)n * OH;
+    // the four windows (k + i, m + jj); absent ones give no gradient
+    f32x8 g[2][2];
+    u8x8 p[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int oh = kr + i, ow = m + jj;
+        if (oh < OH && ow < OW) {
+          const long long o = ((on + oh) * OW + ow) * C8 + c8;
+          g[i][jj] = to_f32(reinterpret_cast<const bf16x8*>(dy)[o]);
+          p[i][jj] = reinterpret_cast<const u8x8*>(arg)[o];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            g[i][jj][q] = 0.f;
+            p[i][jj][q] = 255;
+          }
+        }
+      }
+#pragma unroll
+    for (int ar = 0; ar < 2; ++ar) {
+      const int h = 2 * kr + ar;
+      if (h >= H) continue;
+#pragma unroll
+      for (int bc = 0; bc < 2; ++bc) {
+        const int w = 2 * m + bc;
+        if (w >= W) continue;
+        f32x8 acc = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i <= ar; ++i)
+#pragma unroll
+          for (int jj = 0; jj <= bc; ++jj) {
+            // window (kr + i, m + jj) starts at (2(kr + i) − 1, 2(m + jj) − 1)
+            const uint8_t me = (uint8_t)((ar + 1 - 2 * i) * 3 + (bc + 1 - 2 * jj));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] += p[i][jj][q] == me ? g[i][jj][q] : 0.f;
+          }
+        const long long e = ((long long)h * W + w) * C8 + c8;
+        const f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(xn)[e]);
+        const f32x8 v = preact(xv, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = v[q] > 0.f ? acc[q] : 0.f;
+        reinterpret_cast<bf16x8*>(dxn)[e] = to_bf16(k * acc - k1 - k2 * (xv - mu));
+      }
+    }
+  }
+}
+
 int pick_tx(int C) {
   const int c8 = C / 8;
   if (c8 >= 32) return 32;
@@ -514,4 +656,57 @@ int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, cons
   return 0;
 }
 
+// ---- stem BatchNorm + ReLU + max-pool (see bn_relu_pool_fwd_kernel) ----
+static bool pool_bn_ok(int N, int H, int W, int C) {
+  return C % 8 == 0 && 256 % (C / 8) == 0 && N > 0 && H > 0 && W > 0 && (long long)N * (H + 1) * (W + 1) * C < (1ll << 31);
+}
+
+int bn_relu_pool_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
+                           float* running_mean, float* running_var, int N, int H, int W, int C, float eps,
+                           float momentum, bf16* y, uint8_t* arg, bf16* xsel, float* mean, float* invstd, float* ss,
+                           hipStream_t st) {
+  if (!pool_bn_ok(N, H, W, C) || G < 1) return -2;
+  const long long M = (long long)N * H * W;
+  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
+                                                  running_var, mean, invstd, ss);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int tot = N * OH * OW * (C / 8);
+  bn_relu_pool_fwd_kernel<<<(unsigned)min((tot + 255) / 256, 8192), 256, 0, st>>>(x, ss, N, H, W, C, OH, OW, y, arg,
+                                                                                 xsel);
+  return 0;
+}
+
+int pool_bn_bwd_scratch_floats(int N, int H, int W, int C) {
+  const long long Mp = (long long)N * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1);
+  int gx, gy;
+  long long rpg;
+  stats_grid(Mp, C, pick_tx(C), &gx, &gy, &rpg);
+  return gy * 2 * C + 3 * C;
+}
+
+int pool_bn_bwd(const bf16* dy, const bf16* y, const bf16* xsel, const uint8_t* arg, const bf16* x, const float* mean,
+                const float* invstd, const float* w, const float* b, int N, int H, int W, int C, bf16* dx, float* dw,
+                float* db, int accumulate, float* scratch, hipStream_t st) {
+  if (!pool_bn_ok(N, H, W, C)) return -2;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const long long Mp = (long long)N * OH * OW;
+  const int TX = pick_tx(C);
+  int gx, gy;
+  long long rpg;
+  stats_grid(Mp, C, TX, &gx, &gy, &rpg);
+  float* part = scratch;
+  float* coef = scratch + (size_t)gy * 2 * C;
+  const dim3 grid(gx, gy);
+  // statistics over the pooled tensors (relu 1 with y: g = dy·[y > 0]; x = xsel)
+  if (TX == 32) bn_bwd_stats_kernel<32><<<grid, BN_THREADS, 0, st>>>(dy, y, xsel, mean, invstd, w, b, Mp, C, rpg, 1, part);
+  else if (TX == 16) bn_bwd_stats_kernel<16><<<grid, BN_THREADS, 0, st>>>(dy, y, xsel, mean, invstd, w, b, Mp, C, rpg, 1, part);
+  else bn_bwd_stats_kernel<8><<<grid, BN_THREADS, 0, st>>>(dy, y, xsel, mean, invstd, w, b, Mp, C, rpg, 1, part);
+  // ... normalised by the BatchNorm's full-resolution count
+  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, gy, (long long)N * H * W, C, w, invstd, dw, db,
+                                                        accumulate, coef);
+  const int tot = N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  pool_bn_bwd_apply_kernel<<<(unsigned)min((tot + 255) / 256, 8192), 256, 0, st>>>(dy, arg, x, mean, invstd, w, b,
+                                                                                  coef, N, H, W, C, OH, OW, dx);
+  return 0;
+}
 }  // namespace pdo

@@ -710,6 +710,69 @@ std::vector<at::Tensor> bn_act_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t
   return {y, mean, invstd, mask};
 }
 
+// ResNet stem BatchNorm + ReLU + max-pool 3×3/2 from the stem conv's tile statistics:
+// [pooled y, window positions (uint8), xsel (the BatchNorm input at each maximum), mean, invstd]
+std::vector<at::Tensor> bn_relu_pool_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t tile_rows, at::Tensor w,
+                                               at::Tensor b, c10::optional<at::Tensor> rm,
+                                               c10::optional<at::Tensor> rv, double eps, double momentum) {
+  CHECK_BF16(x); CHECK_F32(w); CHECK_F32(b); CHECK_F32(stats);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_relu_pool_fwd_tiles: channels_last bf16 input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "bn_relu_pool_fwd_tiles: C % 8 == 0 and (C / 8) | 256");
+  TORCH_CHECK(stats.dim() == 3 && stats.size(1) == 2 && stats.size(2) == C &&
+              stats.size(0) == (M + tile_rows - 1) / tile_rows, "bn_relu_pool_fwd_tiles: stats [tiles, 2, C]");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, OH, OW}, x.options(), at::MemoryFormat::ChannelsLast);
+  auto arg = at::empty({N * OH * OW * C}, x.options().dtype(at::kByte));
+  auto xsel = at::empty({N, C, OH, OW}, x.options(), at::MemoryFormat::ChannelsLast);
+  auto mean = at::empty({C}, w.options()), invstd = at::empty({C}, w.options());
+  auto ss = at::empty({2 * C}, w.options());
+  float* rmp = rm && rm->defined() ? fp(*rm) : nullptr;
+  float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
+  CHECK_RC(pdo::bn_relu_pool_fwd_tiles(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), fp(w), fp(b), rmp, rvp,
+                                       (int)N, (int)H, (int)W, (int)C, (float)eps, (float)momentum, bp(y),
+                                       arg.data_ptr<uint8_t>(), bp(xsel), fp(mean), fp(invstd), fp(ss), cur_stream()),
+           "bn_relu_pool_fwd_tiles");
+  return {y, arg, xsel, mean, invstd};
+}
+
+// its backward: [dx of the BatchNorm input, dgamma, dbeta] (dgamma / dbeta accumulated
+// into dw_into / db_into — the parameters' fp32 arena slices — when given)
+std::vector<at::Tensor> pool_bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor xsel, at::Tensor arg, at::Tensor x,
+                                    at::Tensor mean, at::Tensor invstd, at::Tensor w, at::Tensor b,
+                                    c10::optional<at::Tensor> dw_into, c10::optional<at::Tensor> db_into) {
+  CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(y); CHECK_BF16(xsel); CHECK_F32(w); CHECK_F32(b);
+  TORCH_CHECK(y.sizes() == dy.sizes() && xsel.sizes() == dy.sizes() &&
+              y.is_contiguous(at::MemoryFormat::ChannelsLast) && xsel.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "pool_bn_bwd: y / xsel as dy");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "pool_bn_bwd: channels_last dy, x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == C && dy.size(2) == OH && dy.size(3) == OW, "pool_bn_bwd: dy shape");
+  TORCH_CHECK(arg.scalar_type() == at::kByte && arg.numel() == N * OH * OW * C, "pool_bn_bwd: arg");
+  auto dx = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  const bool into = dw_into && dw_into->defined() && db_into && db_into->defined();
+  at::Tensor dw, db;
+  if (into) {
+    CHECK_F32((*dw_into)); CHECK_F32((*db_into));
+    TORCH_CHECK(dw_into->numel() == C && db_into->numel() == C && dw_into->is_contiguous() && db_into->is_contiguous());
+    dw = *dw_into;
+    db = *db_into;
+  } else {
+    dw = at::empty({C}, w.options());
+    db = at::empty({C}, w.options());
+  }
+  auto scratch = at::empty({(int64_t)pdo::pool_bn_bwd_scratch_floats((int)N, (int)H, (int)W, (int)C)}, w.options());
+  CHECK_RC(pdo::pool_bn_bwd(bp(dy), bp(y), bp(xsel), arg.data_ptr<uint8_t>(), bp(x), fp(mean), fp(invstd), fp(w),
+                            fp(b), (int)N,
+                            (int)H, (int)W, (int)C, bp(dx), fp(dw), fp(db), into ? 1 : 0, fp(scratch), cur_stream()),
+           "pool_bn_bwd");
+  if (into) return {dx, at::Tensor(), at::Tensor()};
+  return {dx, dw, db};
+}
+
 // ---------------------------------------------------------------- NHWC max-pool 3×3/2
 std::vector<at::Tensor> maxpool3s2_fwd(at::Tensor x) {
   CHECK_BF16(x);
@@ -996,6 +1059,10 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_act_bwd", &bn_act_bwd);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.def("bn_relu_pool_fwd_tiles", &bn_relu_pool_fwd_tiles);
+  m.def("pool_bn_bwd", &pool_bn_bwd, py::arg("dy"), py::arg("y"), py::arg("xsel"), py::arg("arg"), py::arg("x"),
+        py::arg("mean"), py::arg("invstd"),
+        py::arg("w"), py::arg("b"), py::arg("dw_into") = py::none(), py::arg("db_into") = py::none());
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("n_head"),

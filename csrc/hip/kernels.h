@@ -91,6 +91,17 @@ int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, co
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
                  float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st, unsigned char* mask = nullptr);
 int bn_fwd_scratch_floats(long long M, int C);
+// ResNet stem BatchNorm + ReLU + 3×3/2 max-pool fused (batchnorm.hip): forward from
+// the conv's tile statistics → pooled y and window positions; backward → dx of the
+// BatchNorm input and dgamma / dbeta (scratch: pool_bn_bwd_scratch_floats)
+int bn_relu_pool_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
+                           float* running_mean, float* running_var, int N, int H, int W, int C, float eps,
+                           float momentum, bf16* y, uint8_t* arg, bf16* xsel, float* mean, float* invstd, float* ss,
+                           hipStream_t st);
+int pool_bn_bwd_scratch_floats(int N, int H, int W, int C);
+int pool_bn_bwd(const bf16* dy, const bf16* y, const bf16* xsel, const uint8_t* arg, const bf16* x, const float* mean,
+                const float* invstd, const float* w, const float* b, int N, int H, int W, int C, bf16* dx, float* dw,
+                float* db, int accumulate, float* scratch, hipStream_t st);
 int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float* running_mean, float* running_var,
            long long M, int C, float eps, float momentum, int relu, bf16* y, float* mean, float* invstd,
            float* scratch, hipStream_t st, unsigned char* mask = nullptr);

@@ -84,8 +84,8 @@ class ResNet(nn.Module):
                 nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x):
-        x = ops.conv_bn_act(self.conv1, self.bn1, x)  # the space-to-depth stem on the HIP path
-        x = ops.max_pool_3x3s2(x)
+        # the space-to-depth stem with BatchNorm + ReLU + max-pool fused on the HIP path
+        x = ops.conv_bn_relu_maxpool(self.conv1, self.bn1, x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

@@ -1289,6 +1289,56 @@ def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool =
     return (out, x) if fork else out
 
 
+class _BNReluPoolFn(torch.autograd.Function):
+    """max_pool_3x3s2(ReLU(BN(x))) for ResNet's stem in one forward pass (from the
+    stem convolution's tile statistics) and a two-pass backward
+    (csrc/hip/batchnorm.hip bn_relu_pool_* / pool_bn_*): the full-resolution
+    activation (256 × 64 × 112 × 112 at batch 256, 411 MB) is neither written
+    nor re-read, and its gradient is never materialised — only the BatchNorm
+    input gradient the stem's weight gradient reads.  The backward statistics
+    run over the pooled tensors (dy, y and the BatchNorm input at each window
+    maximum, ``xsel``): a gradient reaches no other pixel."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, running_mean, running_var, eps, momentum, stats, tile_rows):
+        m = _native.require_hip()
+        y, arg, xsel, mean, invstd = m.bn_relu_pool_fwd_tiles(x, stats, tile_rows, w, b, running_mean, running_var,
+                                                              eps, momentum)
+        ctx.save_for_backward(x, y, xsel, arg, mean, invstd, w, b)
+        ctx.params = (w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x, y, xsel, arg, mean, invstd, w, b = ctx.saved_tensors
+        pw, pb = ctx.params
+        direct = _direct_ok(pw) and _direct_ok(pb) and pw.grad.dtype == torch.float32
+        dwi, dbi = (pw.grad, pb.grad) if direct else (None, None)
+        dx, dw, db = m.pool_bn_bwd(dy.contiguous(memory_format=torch.channels_last), y, xsel, arg, x, mean, invstd,
+                                   w, b, dwi, dbi)
+        if direct:
+            pw._pdo_ready(pw)
+            pb._pdo_ready(pb)
+            dw = db = None
+        return dx, dw, db, None, None, None, None, None, None
+
+
+_STEM_POOL = [os.environ.get("PDO_STEM_POOL", "1") != "0"]
+
+
+def conv_bn_relu_maxpool(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x):
+    """ResNet stem: max_pool_3x3s2(ReLU(BN(conv(x)))) — the space-to-depth stem
+    convolution (_StemFn) with the BatchNorm, ReLU and max-pool fused into one
+    pass each way (_BNReluPoolFn) on the HIP path; else conv_bn_act + max-pool."""
+    if _STEM_POOL[0] and _stem_ok(conv, x) and _bn_fused_ok(bn, None):
+        y, st = _StemFn.apply(x, conv.weight)
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        return _BNReluPoolFn.apply(y, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, mom, st,
+                                   _native.require_hip().stem_tile_rows())
+    return max_pool_3x3s2(conv_bn_act(conv, bn, x))
+
+
 class _MaxPool3s2Fn(torch.autograd.Function):
     """3×3 / stride 2 / pad 1 max-pool, NHWC bf16 (csrc/hip/pool.hip)."""
 

@@ -362,3 +362,39 @@ def test_resnet_stem_hip_path_matches_framework_conv():
         e_hip, e_fw = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
         assert e_hip < 1.5 * e_fw + 1e-2, (n, e_hip, e_fw)
     torch.testing.assert_close(a["bn1"].running_mean, c["bn1"].running_mean, rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,H", [(4, 64), (3, 30), (2, 18)])
+def test_stem_bn_relu_pool_fused_matches_unfused(N, H):
+    """The stem's BatchNorm + ReLU + 3×3/2 max-pool in one pass each way
+    (ops._BNReluPoolFn) against the same block through bn_act + max-pool: the
+    pooled output bit-identical, the conv / BatchNorm gradients and running
+    statistics equal to bf16 accuracy (odd pooled sizes: 15 → 8, 9 → 5)."""
+    import copy
+
+    from paddle_operator_amd import ops
+
+    torch.manual_seed(N + H)
+    a = torch.nn.ModuleDict({"conv1": torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
+                             "bn1": torch.nn.BatchNorm2d(64)}).cuda().to(memory_format=torch.channels_last)
+    torch.nn.init.uniform_(a["bn1"].weight, -0.5, 1.5)  # some negative scales: the max is not at max(x)
+    torch.nn.init.uniform_(a["bn1"].bias, -0.2, 0.2)
+    b = copy.deepcopy(a)
+    x = torch.randn(N, 3, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for mod, fused in ((a, True), (b, False)):
+        prev = ops._STEM_POOL[0]
+        ops._STEM_POOL[0] = fused
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = ops.conv_bn_relu_maxpool(mod["conv1"], mod["bn1"], x)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        finally:
+            ops._STEM_POOL[0] = prev
+        outs.append(y)
+    assert outs[0].shape == outs[1].shape == (N, 64, (H // 2 - 1) // 2 + 1, (H // 2 - 1) // 2 + 1)
+    assert torch.equal(outs[0], outs[1])
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert _rel(pa.grad, pb.grad) < 1e-2, n
+    torch.testing.assert_close(a["bn1"].running_mean, b["bn1"].running_mean)
+    torch.testing.assert_close(a["bn1"].running_var, b["bn1"].running_var)
