@@ -304,9 +304,8 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-__global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                     float* __restrict__ lse, int B, int S, int H, float c2,
-                                                     int order) {
+__device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                              float* __restrict__ lse, int B, int S, int H, float c2, int order) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
   const int nqb = S / 128;
@@ -430,6 +429,21 @@ __global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv
   store_acc_rows(orow, o0, 0, hh, inv);
   store_acc_rows(orow, o1, 32, hh, inv);
   if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                     float* __restrict__ lse, int B, int S, int H, float c2,
+                                                     int order) {
+  attn_fwd_body(qkv, out, lse, B, S, H, c2, order);
+}
+// the same body capped at 168 registers for 3 waves per SIMD — the default:
+// 142.20 / 142.32 vs 142.49 / 142.61 ms per GPT-2-medium step for the
+// 2-wave build (PDO_ATTN_FWD3=0, its A/B alternative), no spills (165 VGPRs);
+// a 4-wave cap spills (29 VGPRs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd3_d64(
+    const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int S, int H, float c2,
+    int order) {
+  attn_fwd_body(qkv, out, lse, B, S, H, c2, order);
 }
 
 // ============================================================================
@@ -733,7 +747,11 @@ static int attn_order() {
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
-  attn_fwd_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  static const int fwd3 = env_int("PDO_ATTN_FWD3", 1);
+  if (fwd3)
+    attn_fwd3_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  else
+    attn_fwd_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   return 0;
 }
 
