@@ -398,3 +398,32 @@ def test_stem_bn_relu_pool_fused_matches_unfused(N, H):
         assert _rel(pa.grad, pb.grad) < 1e-2, n
     torch.testing.assert_close(a["bn1"].running_mean, b["bn1"].running_mean)
     torch.testing.assert_close(a["bn1"].running_var, b["bn1"].running_var)
+
+
+def test_stem_arena_grads_match_autograd():
+    """The stem's weight gradient (stem_wgrad, accumulated into the fp32 arena
+    slice) and its BatchNorm γ/β gradients (pool_bn_bwd into the arena) on the
+    arena-direct path equal the same kernels' returned gradients under plain
+    autograd — a dropped, doubled or misplaced arena write is an O(1) error."""
+    import copy
+
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(3)
+    a = torch.nn.ModuleDict({"conv1": torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
+                             "bn1": torch.nn.BatchNorm2d(64)}).cuda().to(memory_format=torch.channels_last)
+    torch.nn.init.uniform_(a["bn1"].weight, 0.5, 1.5)
+    b = copy.deepcopy(a)
+    flat = FlatParams(a, dtype=torch.float32, device="cuda")
+    x = torch.randn(4, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    flat.zero_grad()
+    for mod in (a, b):
+        assert ops._stem_ok(mod["conv1"], x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ops.conv_bn_relu_maxpool(mod["conv1"], mod["bn1"], x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+    torch.cuda.synchronize()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert pa.grad.data_ptr() >= flat.grads.data_ptr(), n
+        assert _rel(pa.grad, pb.grad) < 2e-3, n
