@@ -9,12 +9,14 @@ MI355X-first rather than a transcription of any reference implementation:
   fused cross-entropy kernel, so the loss is exactly the 50257-way loss;
 * QKV stays packed ([B, S, 3, H, D]) and the flash-attention kernel reads it in
   place — no transpose/contiguous copies around attention;
-* residual add + LayerNorm are one kernel, bias + GELU is one kernel (with the
-  bias gradient reduced inside the backward kernel), embedding gather + position
-  add is one kernel;
-* dense projections run on the hand-written gemm_nt4 / gemm_dw4 kernels where
-  a fused epilogue pays (ops.mlp, weight gradients) and on hipBLASLt or
-  gemm_nt4 (PDO_NT_ALL) otherwise.
+* the attention output projection and fc2 add their bias and the residual
+  stream in the GEMM epilogue, so the next LayerNorm reads the stream once
+  (ops.linear_add_layer_norm / ops.mlp_add_layer_norm); bias + GELU and GELU'
+  run in the fc1 / fc2 GEMM epilogues; embedding gather + position add is one
+  kernel;
+* every dense projection (forward, input gradient, weight gradient, LM head)
+  runs on the hand-written gemm_nt4 / gemm_dw4 kernels; the library GEMMs are
+  only the PDO_NT_ALL=0 / PDO_HIP_DW=0 fallbacks.
 
 The reference operator has no model code at all; this workload
 is what a PaddleJob launches (``deploy/examples/resnet.yaml:14-19`` pattern).

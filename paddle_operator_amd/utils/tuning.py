@@ -1,7 +1,9 @@
 """Pre-tuned hipBLASLt/rocBLAS GEMM selection (PyTorch TunableOp) for gfx950.
 
-The dense projections are plain library GEMMs.  Instead of hipBLASLt's
-heuristic pick, every GEMM shape of the flagship step was benchmarked once on
+The flagship steps' GEMMs run on the hand-written gemm_nt4 / gemm_dw4 kernels;
+library GEMMs remain for shapes outside their contracts, the tiny classifier
+heads and the PDO_NT_ALL=0 / PDO_HIP_DW=0 fallbacks.  For those, instead of
+hipBLASLt's heuristic pick, every GEMM shape of the flagship step was benchmarked once on
 an MI355X (all hipBLASLt + rocBLAS solutions, TunableOp) and the winners are
 shipped in ``paddle_operator_amd/tuning/*.csv`` (validated against the
 PyTorch/HIP/hipBLASLt versions and the gcnArchName recorded in the file).
