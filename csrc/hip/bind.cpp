@@ -336,7 +336,8 @@ at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c
 
 // c = a·bᵀ + r (r: [M, N] contiguous bf16), one pass
 // c = a·bᵀ (+ bias) + r, one rounding on the 4-wave mainloop
-at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r, c10::optional<at::Tensor> bias) {
+at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r, c10::optional<at::Tensor> bias,
+                       c10::optional<at::Tensor> mask) {
   nt_check(a, b);
   CHECK_IN(r); CHECK_BF16(r);
   const int M = a.size(0), N = b.size(0), K = a.size(1);
@@ -347,8 +348,16 @@ at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r, c10::optional<a
     TORCH_CHECK(bias->numel() == N, "gemm_nt_add: bias must have N elements");
     bptr = bp(*bias);
   }
+  int epi = bptr ? 5 : 4;
+  if (mask && mask->defined()) {  // c = a·bᵀ + r ⊙ keep (bit j of byte i keeps element 8i + j of r)
+    TORCH_CHECK(!bptr, "gemm_nt_add: bias and mask are exclusive");
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                mask->numel() == (int64_t)M * N / 8 && N % 8 == 0, "gemm_nt_add: mask [M·N/8] uint8");
+    bptr = reinterpret_cast<const bf16*>(mask->data_ptr<uint8_t>());
+    epi = 6;
+  }
   auto c = at::empty({M, N}, a.options());
-  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, bptr ? 5 : 4, bptr, bp(r), N, nullptr, cur_stream()),
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, epi, bptr, bp(r), N, nullptr, cur_stream()),
            "gemm_nt_add");
   return c;
 }
@@ -1050,7 +1059,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("conv_weight_t_batched", &conv_weight_t_batched);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wt"), py::arg("C"), py::arg("R"), py::arg("S"),
         py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("add") = py::none());
-  m.def("gemm_nt_add", &gemm_nt_add, py::arg("a"), py::arg("b"), py::arg("r"), py::arg("bias") = py::none());
+  m.def("gemm_nt_add", &gemm_nt_add, py::arg("a"), py::arg("b"), py::arg("r"), py::arg("bias") = py::none(),
+        py::arg("mask") = py::none());
   m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("conv_wgrad_mode", &pdo::conv_wgrad_mode);
   m.def("conv_wgrad_c64_mode", &pdo::conv_wgrad_c64_mode);

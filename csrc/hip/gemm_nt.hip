@@ -210,6 +210,13 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
       // the addend joins after the bf16 staging: two roundings (the 4-wave path has one)
       const f32x8 r = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n));
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(to_f32(v) + r);
+    } else if constexpr (EPI == 6) {
+      // the addend masked by its keep bits (8 columns per byte): a branch gradient's ReLU
+      f32x8 r = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n));
+      const unsigned bits = reinterpret_cast<const unsigned char*>(bias)[(m * ldy + n) >> 3];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r[q] = (bits >> q) & 1u ? r[q] : 0.f;
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(to_f32(v) + r);
     } else {
       const f32x8 x = to_f32(*reinterpret_cast<const bf16x8*>(Y + m * ldy + n)) + bv8;
       const f32x8 dy = to_f32(v);
@@ -260,7 +267,8 @@ int gemm_nt_get_impl() { return g_impl; }
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
   if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
-  if (((epi >= 1 && epi <= 3) || epi == 5) && !bias) return -3;
+  if (((epi >= 1 && epi <= 3) || epi >= 5) && !bias) return -3;  // EPI 6: bias = the addend's keep mask
+  if (epi == 6 && ldy % 8) return -3;
   if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
   if (nt4_path(K))
@@ -275,6 +283,7 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
     case 3: gemm_nt_kernel<3><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 4: gemm_nt_kernel<4><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 5: gemm_nt_kernel<5><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 6: gemm_nt_kernel<6><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     default: return -4;
   }
   return 0;

@@ -228,10 +228,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const int g4 = lane >> 4;
     const int nb = n0 + wn * 128 + 8 * (lane & 15);
     const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
-    bf16x8 pre[EPI >= 3 ? 32 : 1];  // EPI 3: the GELU pre-activation; EPI 4 / 5: the addend
+    bf16x8 pre[EPI >= 3 ? 32 : 1];  // EPI 3: the GELU pre-activation; EPI 4 / 5 / 6: the addend
+    unsigned char mk[EPI == 6 ? 32 : 1];  // EPI 6: the addend's keep bits (8 columns per byte)
     if constexpr (EPI >= 3) {
 #pragma unroll
       for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
+    }
+    if constexpr (EPI == 6) {
+      const unsigned char* mask = reinterpret_cast<const unsigned char*>(bias);
+#pragma unroll
+      for (int u = 0; u < 32; ++u) mk[u] = mask[((mr + 16 * (u >> 2) + (u & 3)) * ldy + nb) >> 3];
     }
     f32x8 bv8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr ((EPI >= 1 && EPI <= 3) || EPI == 5) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
@@ -269,6 +275,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           st16(crow, to_bf16(v + to_f32(pre[4 * i + e])));  // C = A·Bᵀ + Y, one rounding
         } else if constexpr (EPI == 5) {
           st16(crow, to_bf16(v + bv8 + to_f32(pre[4 * i + e])));  // C = A·Bᵀ + bias + Y (residual stream)
+        } else if constexpr (EPI == 6) {
+          // C = A·Bᵀ + Y ⊙ keep: a branch gradient whose ReLU mask is applied here
+          const unsigned bits = mk[4 * i + e];
+          f32x8 r = to_f32(pre[4 * i + e]);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) r[q] = (bits >> q) & 1u ? r[q] : 0.f;
+          st16(crow, to_bf16(v + r));
         } else {
           const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
           const f32x8& dy = v;  // the fp32 product, not its bf16 rounding
@@ -476,6 +489,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
       case 3: gemm_nt4_kernel<3, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       case 4: gemm_nt4_kernel<4, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       case 5: gemm_nt4_kernel<5, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
+      case 6: gemm_nt4_kernel<6, MI, DF><<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m); break;
       default: return -4;
     }
     return 0;

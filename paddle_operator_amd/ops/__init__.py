@@ -963,7 +963,7 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu, stats=None, tile_rows=0,
-                link=None):
+                link=None, rlink=None):
         m = _native.require_hip()
         # mask: with a residual under the ReLU, the 1-bit ReLU mask the backward reads
         # instead of the bf16 output (1/16 of the bytes, both backward passes)
@@ -979,6 +979,9 @@ class _BNActFn(torch.autograd.Function):
         ctx.link = link
         if link is not None:
             link.bn = (x, mean, invstd, w, b, relu)
+        # residual = a forked convolution input (identity block): its gradient's
+        # ReLU mask is applied by that convolution's dX epilogue (_ResMaskLink)
+        ctx.rlink = rlink if (rlink is not None and relu and residual is not None and mask is not None) else None
         return y
 
     @staticmethod
@@ -990,16 +993,21 @@ class _BNActFn(torch.autograd.Function):
         direct = _direct_ok(pw) and _direct_ok(pb) and pw.grad.dtype == torch.float32
         dwi, dbi = (pw.grad, pb.grad) if direct else (None, None)
         part = ctx.link.take(dy) if ctx.link is not None else None
+        want_dres = ctx.has_res and ctx.rlink is None
         if part is not None:
-            dx, dres, dw, db = m.bn_act_bwd_part(part, dy, y, x, mean, invstd, w, b, ctx.relu, ctx.has_res, dwi, dbi)
+            dx, dres, dw, db = m.bn_act_bwd_part(part, dy, y, x, mean, invstd, w, b, ctx.relu, want_dres, dwi, dbi)
         else:
-            dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, ctx.relu, ctx.has_res, dwi, dbi)
+            dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, ctx.relu, want_dres, dwi, dbi)
         ctx.link = None
+        if ctx.rlink is not None:
+            dres = dy  # unmasked: the forking convolution's dX epilogue applies the mask
+            ctx.rlink.give(dy, y)
+            ctx.rlink = None
         if direct:
             pw._pdo_ready(pw)
             pb._pdo_ready(pb)
             dw = db = None
-        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None
+        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None
 
 
 class _BNLink:
@@ -1034,12 +1042,53 @@ class _BNLink:
 
 _BN_LINK_USED = [0]  # backward passes that took their statistics from a convolution epilogue (tests)
 
+class _ResMaskLink:
+    """Hand-off for a residual branch that is a convolution's forked input
+    (ResNet's identity block: bn3's residual is the x conv1 forked).  The
+    residual BatchNorm's backward does not write dres = dy ⊙ relu-mask: it
+    returns dy itself as the residual's gradient and parks (dy, mask) here; the
+    forking convolution's input-gradient GEMM applies the mask to that addend in
+    its epilogue (gemm_nt_add EPI 6).  A gradient arriving there that is not
+    that exact tensor (storage and version) would mean something else was added
+    to it — an error, raised, never silently masked."""
+
+    __slots__ = ("dy", "ver", "mask")
+
+    def __init__(self):
+        self.dy = self.mask = None
+        self.ver = -1
+
+    def give(self, dy, mask):
+        self.dy, self.ver, self.mask = dy, dy._version, mask
+
+    def take(self, dalias):
+        dy, ver, mask = self.dy, self.ver, self.mask
+        self.dy = self.mask = None
+        if mask is None:
+            return None
+        if dalias is None or dalias.data_ptr() != dy.data_ptr() or dalias._version != ver:
+            raise RuntimeError("residual mask hand-off: the forked input's gradient is not the residual "
+                               "BatchNorm's dy (another consumer added to it)")
+        _RES_MASK_USED[0] += 1
+        return mask
+
+
+_RES_MASK_USED = [0]  # identity-branch gradients masked in the conv1 dX epilogue (tests)
+_RES_MASK = [os.environ.get("PDO_RES_MASK", "1") != "0"]
+
+
+def _apply_bitmask(t, mask):
+    """t ⊙ keep for a channels_last tensor and its [N·H·W·C / 8] ReLU bitmask."""
+    bits = ((mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1).view(-1)
+    flat = t.permute(0, 2, 3, 1).reshape(-1) * bits.to(t.dtype)
+    return flat.view(t.shape[0], t.shape[2], t.shape[3], t.shape[1]).permute(0, 3, 1, 2)
+
 
 _BN_FUSED = [os.environ.get("PDO_BN_FUSED", "1") != "0"]
 _BN_LINK = [os.environ.get("PDO_BN_LINK", "1") != "0"]
 
 
-def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
+def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None, rlink=None):
     """Training BatchNorm → (+ residual) → ReLU in one HIP forward pass over the
     activation (plus a statistics pass), and one backward pass (plus stats).
     Falls back to PyTorch ops outside the fused case (eval mode, CPU, NCHW,
@@ -1053,7 +1102,7 @@ def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None):
         mom = bn.momentum if bn.momentum is not None else 0.1
         link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
         y = _BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu,
-                           None, 0, link)
+                           None, 0, link, rlink)
         if link is not None:
             y._pdo_bn = link  # read by _ConvFn when y feeds an implicit-GEMM convolution
         return y
@@ -1100,7 +1149,7 @@ class _ConvFn(torch.autograd.Function):
     gradients on ResNet-50 (profiles/r3t_resnet50_kernels.md)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pad, want_stats, fork=False):
+    def forward(ctx, x, w, stride, pad, want_stats, fork=False, rlink=None):
         m = _native.require_hip()
         sh = getattr(w, "_pdo_shadow", None)  # the arena's bf16 copy, cast once per step (FlatParams.shadow_scope)
         ctx.wt = None
@@ -1123,6 +1172,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.wparam = w
         link = getattr(x, "_pdo_bn", None)
         ctx.link = link if link is not None and link.bn is not None else None
+        ctx.rlink = rlink if fork else None
         ctx.set_materialize_grads(False)
         if st is not None:
             ctx.mark_non_differentiable(st)
@@ -1136,8 +1186,10 @@ class _ConvFn(torch.autograd.Function):
         N, _, H, W_ = x.shape
         T = N * H * W_
         link, ctx.link = ctx.link, None
+        rlink, ctx.rlink = ctx.rlink, None
+        amask = rlink.take(dalias) if rlink is not None else None  # dalias ⊙ amask is the branch's gradient
         if dy is None:  # y unused: only the alias carried a gradient
-            return dalias, None, None, None, None, None
+            return (_apply_bitmask(dalias, amask) if amask is not None else dalias), None, None, None, None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dalias is not None:
             dalias = dalias.contiguous(memory_format=torch.channels_last)
@@ -1148,10 +1200,13 @@ class _ConvFn(torch.autograd.Function):
             if ctx.one and _gemm_dgrad_1x1(m, T, C, K):
                 dy2 = dy.permute(0, 2, 3, 1).reshape(T, K)
                 wt2 = transpose(wb.view(K, C))
-                dx = (m.gemm_nt_add(dy2, wt2, dalias.permute(0, 2, 3, 1).reshape(T, C)) if dalias is not None
-                      else m.gemm_nt(dy2, wt2))
+                dx = (m.gemm_nt_add(dy2, wt2, dalias.permute(0, 2, 3, 1).reshape(T, C), mask=amask)
+                      if dalias is not None else m.gemm_nt(dy2, wt2))
+                amask = None
                 dx = dx.view(N, H, W_, C).permute(0, 3, 1, 2)
             else:
+                if amask is not None:
+                    dalias, amask = _apply_bitmask(dalias, amask).contiguous(memory_format=torch.channels_last), None
                 wt = ctx.wt if ctx.wt is not None else m.conv_weight_t(wb)
                 if link is not None and link.bn is not None:
                     # the producing BatchNorm's backward statistics from this epilogue
@@ -1174,7 +1229,7 @@ class _ConvFn(torch.autograd.Function):
                 p._pdo_ready(p)
             else:
                 dw = m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad).to(p.dtype)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 _HIP_CONV = [os.environ.get("PDO_HIP_CONV", "1") != "0"]
@@ -1261,6 +1316,14 @@ def _bn_fused_ok(bn: torch.nn.BatchNorm2d, residual) -> bool:
 
 def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None,
                 fork: bool = False):
+    """see _conv_bn_act; ``residual`` may be a forked input whose only other
+    consumer is this BatchNorm (ResNet's identity block): then its ReLU-masked
+    gradient is formed in the forking convolution's dX epilogue."""
+    return _conv_bn_act(conv, bn, x, relu, residual, fork)
+
+
+def _conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None,
+                 fork: bool = False):
     """act(BN(conv(x)) [+ residual]) — on the hand-written convolutions with the
     BatchNorm statistics taken in the implicit GEMM's epilogue where that kernel
     runs the forward; otherwise the framework convolution + ops.bn_act.
@@ -1268,20 +1331,24 @@ def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool =
     then joins this convolution's dX in its epilogue (_ConvFn)."""
     stem = not fork and _stem_ok(conv, x)
     if (stem or _hip_conv_ok(conv, x)) and _bn_fused_ok(bn, residual):
+        rl = _ResMaskLink() if (fork and _RES_MASK[0] and torch.is_grad_enabled()) else None
         if stem:
             y, st = _StemFn.apply(x, conv.weight)
             xa = None
         else:
-            y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork)
+            y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork, rl)
+            if rl is not None and xa is not None:
+                xa._pdo_rlink = rl  # read by the residual BatchNorm when xa is its residual
+        rres = getattr(residual, "_pdo_rlink", None) if residual is not None else None
         if st is None:
-            out = bn_act(bn, y, relu=relu, residual=residual)
+            out = bn_act(bn, y, relu=relu, residual=residual, rlink=rres)
         else:
             mom = bn.momentum if bn.momentum is not None else 0.1
             m = _native.require_hip()
             rows = m.stem_tile_rows() if stem else m.conv_tile_rows(conv.out_channels)
             link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
             out = _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom,
-                                 relu, st, rows, link)
+                                 relu, st, rows, link, rres)
             if link is not None:
                 out._pdo_bn = link
         return (out, xa) if fork else out

@@ -427,3 +427,54 @@ def test_stem_arena_grads_match_autograd():
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert pa.grad.data_ptr() >= flat.grads.data_ptr(), n
         assert _rel(pa.grad, pb.grad) < 2e-3, n
+
+
+def test_identity_bottleneck_residual_mask_in_dx_epilogue():
+    """An identity bottleneck (no downsample): bn3's residual gradient dy ⊙ relu'
+    is formed in conv1's dX GEMM epilogue (gemm_nt_add EPI 6) instead of being
+    written by the BatchNorm backward — same output and gradients as with the
+    hand-off off (PDO_RES_MASK=0 path), and the hand-off is taken."""
+    import copy
+
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(5)
+    a = Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last)
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 256, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for mod, on in ((a, True), (b, False)):
+        prev = ops._RES_MASK[0]
+        ops._RES_MASK[0] = on
+        used = ops._RES_MASK_USED[0]
+        try:
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = mod(xx)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        finally:
+            ops._RES_MASK[0] = prev
+        assert (ops._RES_MASK_USED[0] - used) == (1 if on else 0)
+        outs.append((y, xx.grad))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert _rel(outs[0][1], outs[1][1]) < 1e-2
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert _rel(pa.grad, pb.grad) < 1e-2, n
+
+
+@pytest.mark.parametrize("T,N,K", [(4096, 1024, 1024), (2048, 256, 64)])
+def test_gemm_nt_add_masked(hip, T, N, K):
+    """c = a·bᵀ + r ⊙ keep (gemm_nt EPI 6) on the 4-wave (K ≥ 256) and 8-wave
+    (K = 64) mainloops against fp32."""
+    g = torch.Generator(device="cuda").manual_seed(T + N + K)
+    a = torch.randn(T, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    r = torch.randn(T, N, device="cuda", generator=g).bfloat16()
+    mask = torch.randint(0, 256, (T * N // 8,), device="cuda", generator=g, dtype=torch.int64).to(torch.uint8)
+    keep = ((mask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).view(T, N).float()
+    c = hip.gemm_nt_add(a, b, r, mask=mask)
+    assert _rel(c, a.float() @ b.float().t() + r.float() * keep) < 1e-2
