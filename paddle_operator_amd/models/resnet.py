@@ -48,7 +48,7 @@ class Bottleneck(nn.Module):
         out = ops.conv_bn_act(self.conv2, self.bn2, out)
         idt = xa
         if self.downsample is not None:
-            idt = ops.conv_bn_act(self.downsample[0], self.downsample[1], xa, relu=False)
+            idt = ops.conv_bn_act(self.downsample[0], self.downsample[1], xa, relu=False, as_residual=True)
         return ops.conv_bn_act(self.conv3, self.bn3, out, relu=True, residual=idt)
 
 

@@ -963,7 +963,7 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, residual, running_mean, running_var, eps, momentum, relu, stats=None, tile_rows=0,
-                link=None, rlink=None):
+                link=None, rlink=None, mlink=None):
         m = _native.require_hip()
         # mask: with a residual under the ReLU, the 1-bit ReLU mask the backward reads
         # instead of the bf16 output (1/16 of the bytes, both backward passes)
@@ -982,6 +982,9 @@ class _BNActFn(torch.autograd.Function):
         # residual = a forked convolution input (identity block): its gradient's
         # ReLU mask is applied by that convolution's dX epilogue (_ResMaskLink)
         ctx.rlink = rlink if (rlink is not None and relu and residual is not None and mask is not None) else None
+        # this output is another BatchNorm's residual (ResNet's downsample branch): that
+        # BatchNorm may hand over (its dy, its ReLU mask) instead of writing dy ⊙ mask
+        ctx.mlink = mlink if (mlink is not None and not relu and residual is None) else None
         return y
 
     @staticmethod
@@ -994,10 +997,15 @@ class _BNActFn(torch.autograd.Function):
         dwi, dbi = (pw.grad, pb.grad) if direct else (None, None)
         part = ctx.link.take(dy) if ctx.link is not None else None
         want_dres = ctx.has_res and ctx.rlink is None
+        relu = ctx.relu
+        gmask = ctx.mlink.take(dy) if ctx.mlink is not None else None
+        ctx.mlink = None
+        if gmask is not None:  # dy ⊙ gmask is this BatchNorm's output gradient: the bitmask mode (y = mask)
+            y, relu = gmask, True
         if part is not None:
-            dx, dres, dw, db = m.bn_act_bwd_part(part, dy, y, x, mean, invstd, w, b, ctx.relu, want_dres, dwi, dbi)
+            dx, dres, dw, db = m.bn_act_bwd_part(part, dy, y, x, mean, invstd, w, b, relu, want_dres, dwi, dbi)
         else:
-            dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, ctx.relu, want_dres, dwi, dbi)
+            dx, dres, dw, db = m.bn_act_bwd(dy, y, x, mean, invstd, w, b, relu, want_dres, dwi, dbi)
         ctx.link = None
         if ctx.rlink is not None:
             dres = dy  # unmasked: the forking convolution's dX epilogue applies the mask
@@ -1007,7 +1015,7 @@ class _BNActFn(torch.autograd.Function):
             pw._pdo_ready(pw)
             pb._pdo_ready(pb)
             dw = db = None
-        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None
+        return dx, dw, db, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None, None, None
 
 
 class _BNLink:
@@ -1088,7 +1096,7 @@ _BN_FUSED = [os.environ.get("PDO_BN_FUSED", "1") != "0"]
 _BN_LINK = [os.environ.get("PDO_BN_LINK", "1") != "0"]
 
 
-def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None, rlink=None):
+def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None, rlink=None, mlink=None):
     """Training BatchNorm → (+ residual) → ReLU in one HIP forward pass over the
     activation (plus a statistics pass), and one backward pass (plus stats).
     Falls back to PyTorch ops outside the fused case (eval mode, CPU, NCHW,
@@ -1102,9 +1110,11 @@ def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None, rlink=
         mom = bn.momentum if bn.momentum is not None else 0.1
         link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
         y = _BNActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom, relu,
-                           None, 0, link, rlink)
+                           None, 0, link, rlink, mlink)
         if link is not None:
             y._pdo_bn = link  # read by _ConvFn when y feeds an implicit-GEMM convolution
+        if mlink is not None and not relu and residual is None:
+            y._pdo_rlink = mlink  # read by the BatchNorm this output is the residual of
         return y
     y = bn(x)
     if residual is not None:
@@ -1315,15 +1325,18 @@ def _bn_fused_ok(bn: torch.nn.BatchNorm2d, residual) -> bool:
 
 
 def conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None,
-                fork: bool = False):
-    """see _conv_bn_act; ``residual`` may be a forked input whose only other
-    consumer is this BatchNorm (ResNet's identity block): then its ReLU-masked
-    gradient is formed in the forking convolution's dX epilogue."""
-    return _conv_bn_act(conv, bn, x, relu, residual, fork)
+                fork: bool = False, as_residual: bool = False):
+    """see _conv_bn_act.  ``residual`` may be a forked input whose only consumer
+    besides the forking convolution is this BatchNorm (ResNet's identity
+    block): then its ReLU-masked gradient is formed in the forking
+    convolution's dX epilogue.  ``as_residual``: the output's only consumer is
+    another BatchNorm's residual (ResNet's downsample branch): that BatchNorm
+    hands over (dy, ReLU mask) and this backward applies the mask itself."""
+    return _conv_bn_act(conv, bn, x, relu, residual, fork, as_residual)
 
 
 def _conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None,
-                 fork: bool = False):
+                 fork: bool = False, as_residual: bool = False):
     """act(BN(conv(x)) [+ residual]) — on the hand-written convolutions with the
     BatchNorm statistics taken in the implicit GEMM's epilogue where that kernel
     runs the forward; otherwise the framework convolution + ops.bn_act.
@@ -1340,17 +1353,21 @@ def _conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool 
             if rl is not None and xa is not None:
                 xa._pdo_rlink = rl  # read by the residual BatchNorm when xa is its residual
         rres = getattr(residual, "_pdo_rlink", None) if residual is not None else None
+        ml = (_ResMaskLink() if as_residual and not relu and residual is None and _RES_MASK[0]
+              and torch.is_grad_enabled() else None)
         if st is None:
-            out = bn_act(bn, y, relu=relu, residual=residual, rlink=rres)
+            out = bn_act(bn, y, relu=relu, residual=residual, rlink=rres, mlink=ml)
         else:
             mom = bn.momentum if bn.momentum is not None else 0.1
             m = _native.require_hip()
             rows = m.stem_tile_rows() if stem else m.conv_tile_rows(conv.out_channels)
             link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
             out = _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom,
-                                 relu, st, rows, link, rres)
+                                 relu, st, rows, link, rres, ml)
             if link is not None:
                 out._pdo_bn = link
+            if ml is not None:
+                out._pdo_rlink = ml  # read by the BatchNorm this output is the residual of
         return (out, xa) if fork else out
     out = bn_act(bn, conv(x), relu=relu, residual=residual)
     return (out, x) if fork else out

@@ -429,18 +429,23 @@ def test_stem_arena_grads_match_autograd():
         assert _rel(pa.grad, pb.grad) < 2e-3, n
 
 
-def test_identity_bottleneck_residual_mask_in_dx_epilogue():
-    """An identity bottleneck (no downsample): bn3's residual gradient dy ⊙ relu'
-    is formed in conv1's dX GEMM epilogue (gemm_nt_add EPI 6) instead of being
-    written by the BatchNorm backward — same output and gradients as with the
-    hand-off off (PDO_RES_MASK=0 path), and the hand-off is taken."""
+@pytest.mark.parametrize("downsample", [False, True])
+def test_identity_bottleneck_residual_mask_in_dx_epilogue(downsample):
+    """bn3's residual gradient dy ⊙ relu' is not written by its BatchNorm
+    backward: in an identity bottleneck conv1's dX GEMM epilogue forms it
+    (gemm_nt_add EPI 6), in a downsample bottleneck the downsample BatchNorm's
+    backward applies the mask (bitmask mode) — same output and gradients as with
+    the hand-off off (PDO_RES_MASK=0 path), and the hand-off is taken."""
     import copy
 
     from paddle_operator_amd import ops
     from paddle_operator_amd.models.resnet import Bottleneck
 
     torch.manual_seed(5)
-    a = Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last)
+    ds = (torch.nn.Sequential(torch.nn.Conv2d(256, 512, 1, stride=2, bias=False), torch.nn.BatchNorm2d(512))
+          if downsample else None)
+    a = Bottleneck(256, 128 if downsample else 64, stride=2 if downsample else 1,
+                   downsample=ds).cuda().to(memory_format=torch.channels_last)
     for mod in a.modules():
         if isinstance(mod, torch.nn.BatchNorm2d):
             torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
