@@ -637,6 +637,17 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t R, int64_t S, int64_t
   return dw;
 }
 
+// dx (channels_last [N, C, H, W]) += add at the stride-2 pixels (add: [N, C, ceil(H/2), ceil(W/2)])
+void conv_stride2_add(at::Tensor dx, at::Tensor add) {
+  CHECK_BF16(dx); CHECK_BF16(add);
+  TORCH_CHECK(dx.is_cuda() && dx.dim() == 4 && dx.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              add.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_stride2_add: channels_last bf16");
+  const int N = (int)dx.size(0), C = (int)dx.size(1), H = (int)dx.size(2), W = (int)dx.size(3);
+  TORCH_CHECK(add.size(0) == N && add.size(1) == C && add.size(2) == (H - 1) / 2 + 1 && add.size(3) == (W - 1) / 2 + 1,
+              "conv_stride2_add: add shape");
+  CHECK_RC(pdo::conv_stride2_add(bp(dx), bp(add), N, H, W, C, cur_stream()), "conv_stride2_add");
+}
+
 // ResNet stem 7×7 / stride 2 / pad 3 (3 → 64 channels) through the space-to-depth
 // 4×4 implicit GEMM: [y, BatchNorm tile statistics (with_stats), z = the 16-channel
 // image the weight gradient reads]
@@ -1051,6 +1062,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("with_stats") = false);
   m.def("conv_tile_rows", &conv_tile_rows);
+  m.def("conv_stride2_add", &conv_stride2_add);
   m.def("stem_ok", &stem_ok);
   m.def("stem_tile_rows", &pdo::stem_tile_rows);
   m.def("stem_fwd", &stem_fwd, py::arg("x"), py::arg("w"), py::arg("with_stats") = true);

@@ -1083,6 +1083,34 @@ int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, i
   return 0;
 }
 
+// dx[n][2a][2b][:] += add[n][a][b][:] — the input gradient of a 1×1 stride-2
+// convolution (ResNet's downsample branch) joining the forking convolution's dX
+// at the pixels it reaches: the downsample's dX stays compact ([N][Ho][Wo][C],
+// a plain GEMM), no zero-filled full-resolution tensor is written or re-read
+namespace {
+__global__ __launch_bounds__(256) void stride2_add_kernel(bf16* __restrict__ dx, const bf16* __restrict__ add, int H,
+                                                         int W, int Ho, int Wo, int C8, long long total) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c8 = (int)(i % C8);
+    const long long t = i / C8;
+    const int b = (int)(t % Wo);
+    const long long t2 = t / Wo;
+    const int a = (int)(t2 % Ho);
+    const long long n = t2 / Ho;
+    bf16x8* d = reinterpret_cast<bf16x8*>(dx) + ((n * H + 2 * a) * W + 2 * b) * C8 + c8;
+    *d = to_bf16(to_f32(*d) + to_f32(reinterpret_cast<const bf16x8*>(add)[i]));
+  }
+}
+}  // namespace
+
+int conv_stride2_add(bf16* dx, const bf16* add, int N, int H, int W, int C, hipStream_t st) {
+  if (C % 8) return -2;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long total = (long long)N * Ho * Wo * (C / 8);
+  stride2_add_kernel<<<stream_grid(total, 256), 256, 0, st>>>(dx, add, H, W, Ho, Wo, C / 8, total);
+  return 0;
+}
+
 // ============================================================================
 // ResNet stem: y = conv7×7/2(x, w), pad 3, C = 3 → 64 channels.  With
 // z[n][i][j][(2p + q)·3 + c] = x[n][2i + p][2j + q][c] (channels 12-15 zero) and

@@ -75,6 +75,8 @@ int bn_bwd_part(const float* part, int G, const bf16* dy, const bf16* y, const b
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad);
 int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st);
+// dx[n][2a][2b] += add[n][a][b] (NHWC bf16): a compact 1×1 stride-2 input gradient joining dX
+int conv_stride2_add(bf16* dx, const bf16* add, int N, int H, int W, int C, hipStream_t st);
 // ResNet stem (7×7 / stride 2 / pad 3, 3 → Kout = 64 channels) as a space-to-depth
 // 4×4 stride-1 convolution over a 16-channel image on the implicit GEMM (conv.hip)
 int stem_supported(int N, int H, int W, int C, int Kout);

@@ -1082,6 +1082,33 @@ class _ResMaskLink:
 
 
 _RES_MASK_USED = [0]  # identity-branch gradients masked in the conv1 dX epilogue (tests)
+
+class _CompactGradLink:
+    """Hand-off from a 1×1 stride-2 convolution (ResNet's downsample) to the
+    convolution that forked its input (conv1): the downsample's input gradient is
+    nonzero only at the stride-2 pixels, so it is computed compact ([N, C, Ho, Wo],
+    one GEMM) and added into conv1's dX at those pixels (conv_stride2_add) instead
+    of a zero-filled full-resolution tensor that conv1's GEMM re-reads as its
+    addend.  The downsample returns no input gradient through autograd; any other
+    gradient of the forked input still arrives as conv1's dalias and is added."""
+
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+    def give(self, t):
+        self.t = t if self.t is None else self.t + t
+
+    def take(self):
+        t, self.t = self.t, None
+        if t is not None:
+            _DS_COMPACT_USED[0] += 1
+        return t
+
+
+_DS_COMPACT_USED = [0]
+_DS_COMPACT = [os.environ.get("PDO_DS_COMPACT", "1") != "0"]
 _RES_MASK = [os.environ.get("PDO_RES_MASK", "1") != "0"]
 
 
@@ -1159,7 +1186,7 @@ class _ConvFn(torch.autograd.Function):
     gradients on ResNet-50 (profiles/r3t_resnet50_kernels.md)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pad, want_stats, fork=False, rlink=None):
+    def forward(ctx, x, w, stride, pad, want_stats, fork=False, rlink=None, slink=None, clink=None):
         m = _native.require_hip()
         sh = getattr(w, "_pdo_shadow", None)  # the arena's bf16 copy, cast once per step (FlatParams.shadow_scope)
         ctx.wt = None
@@ -1183,6 +1210,8 @@ class _ConvFn(torch.autograd.Function):
         link = getattr(x, "_pdo_bn", None)
         ctx.link = link if link is not None and link.bn is not None else None
         ctx.rlink = rlink if fork else None
+        ctx.slink = slink if fork else None  # conv1: compact downsample gradients to add into dX
+        ctx.clink = clink if (R == 1 and stride == 2 and pad == 0) else None  # downsample: give dX compact
         ctx.set_materialize_grads(False)
         if st is not None:
             ctx.mark_non_differentiable(st)
@@ -1197,14 +1226,33 @@ class _ConvFn(torch.autograd.Function):
         T = N * H * W_
         link, ctx.link = ctx.link, None
         rlink, ctx.rlink = ctx.rlink, None
+        slink, ctx.slink = ctx.slink, None
+        clink, ctx.clink = ctx.clink, None
         amask = rlink.take(dalias) if rlink is not None else None  # dalias ⊙ amask is the branch's gradient
         if dy is None:  # y unused: only the alias carried a gradient
-            return (_apply_bitmask(dalias, amask) if amask is not None else dalias), None, None, None, None, None, None
+            cadd = slink.take() if slink is not None else None
+            if cadd is not None:  # (y unused) the forked input's gradient = dalias + the compact downsample part
+                base = (_apply_bitmask(dalias, amask) if amask is not None else dalias)
+                base = (base.contiguous(memory_format=torch.channels_last).clone() if base is not None else
+                        torch.zeros(ctx.saved_tensors[0].shape, device=cadd.device,
+                                    dtype=cadd.dtype).contiguous(memory_format=torch.channels_last))
+                m.conv_stride2_add(base, cadd.contiguous(memory_format=torch.channels_last))
+                return base, None, None, None, None, None, None, None, None
+            return ((_apply_bitmask(dalias, amask) if amask is not None else dalias), None, None, None, None, None, None,
+                    None, None)
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dalias is not None:
             dalias = dalias.contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and clink is not None and dalias is None:
+            # the downsample's dX, compact: [N·Ho·Wo, K] · W [K, C] on gemm_nt, for the forking conv1
+            No, _, Ho, Wo = dy.shape
+            T4 = No * Ho * Wo
+            if m.gemm_nt_supported(T4, C, K):
+                g = m.gemm_nt(dy.permute(0, 2, 3, 1).reshape(T4, K), transpose(wb.view(K, C)))
+                clink.give(g.view(No, Ho, Wo, C).permute(0, 3, 1, 2))
+                clink = "given"
+        if ctx.needs_input_grad[0] and clink != "given":
             # the GEMM where it is faster, even past a BatchNorm link (that
             # BatchNorm then takes its own statistics pass)
             if ctx.one and _gemm_dgrad_1x1(m, T, C, K):
@@ -1227,6 +1275,10 @@ class _ConvFn(torch.autograd.Function):
                         dx = dx + dalias
                 else:
                     dx = m.conv_dgrad(dy, wt, C, R, S, H, W_, ctx.stride, ctx.pad, dalias)
+        cadd = slink.take() if slink is not None else None
+        if cadd is not None and dx is not None:
+            dx = dx.contiguous(memory_format=torch.channels_last)
+            m.conv_stride2_add(dx, cadd.contiguous(memory_format=torch.channels_last))
         if ctx.needs_input_grad[1]:
             p = ctx.wparam
             if ctx.one and _gemm_wgrad_1x1(C, K):
@@ -1239,7 +1291,7 @@ class _ConvFn(torch.autograd.Function):
                 p._pdo_ready(p)
             else:
                 dw = m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad).to(p.dtype)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 _HIP_CONV = [os.environ.get("PDO_HIP_CONV", "1") != "0"]
@@ -1345,13 +1397,19 @@ def _conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool 
     stem = not fork and _stem_ok(conv, x)
     if (stem or _hip_conv_ok(conv, x)) and _bn_fused_ok(bn, residual):
         rl = _ResMaskLink() if (fork and _RES_MASK[0] and torch.is_grad_enabled()) else None
+        # compact downsample gradients: not past a BatchNorm link (its partials come from dX's epilogue)
+        sl = (_CompactGradLink() if (fork and _DS_COMPACT[0] and torch.is_grad_enabled()
+                                      and getattr(x, "_pdo_bn", None) is None) else None)
+        cl = getattr(x, "_pdo_slink", None) if not fork else None
         if stem:
             y, st = _StemFn.apply(x, conv.weight)
             xa = None
         else:
-            y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork, rl)
+            y, st, xa = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, fork, rl, sl, cl)
             if rl is not None and xa is not None:
                 xa._pdo_rlink = rl  # read by the residual BatchNorm when xa is its residual
+            if sl is not None and xa is not None:
+                xa._pdo_slink = sl  # read by a 1×1 stride-2 convolution of xa (the downsample)
         rres = getattr(residual, "_pdo_rlink", None) if residual is not None else None
         ml = (_ResMaskLink() if as_residual and not relu and residual is None and _RES_MASK[0]
               and torch.is_grad_enabled() else None)

@@ -483,3 +483,41 @@ def test_gemm_nt_add_masked(hip, T, N, K):
     keep = ((mask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).view(T, N).float()
     c = hip.gemm_nt_add(a, b, r, mask=mask)
     assert _rel(c, a.float() @ b.float().t() + r.float() * keep) < 1e-2
+
+
+def test_downsample_compact_input_gradient():
+    """A stride-2 downsample bottleneck: the downsample's input gradient is
+    computed compact and added into conv1's dX at the stride-2 pixels
+    (ops._CompactGradLink, conv_stride2_add) — same input / parameter gradients
+    as the zero-filled full-resolution path (PDO_DS_COMPACT=0), hand-off taken."""
+    import copy
+
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(9)
+    ds = torch.nn.Sequential(torch.nn.Conv2d(256, 512, 1, stride=2, bias=False), torch.nn.BatchNorm2d(512))
+    a = Bottleneck(256, 128, stride=2, downsample=ds).cuda().to(memory_format=torch.channels_last)
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+    b = copy.deepcopy(a)
+    x = torch.randn(4, 256, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for mod, on in ((a, True), (b, False)):
+        prev = ops._DS_COMPACT[0]
+        ops._DS_COMPACT[0] = on
+        used = ops._DS_COMPACT_USED[0]
+        try:
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = mod(xx)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        finally:
+            ops._DS_COMPACT[0] = prev
+        assert (ops._DS_COMPACT_USED[0] - used) == (1 if on else 0)
+        outs.append((y, xx.grad))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert _rel(outs[0][1], outs[1][1]) < 1e-2
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert _rel(pa.grad, pb.grad) < 1e-2, n
