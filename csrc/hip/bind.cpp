@@ -29,6 +29,83 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 inline bf16* bp(const at::Tensor& t) { return reinterpret_cast<bf16*>(t.data_ptr()); }
 inline float* fp(const at::Tensor& t) { return t.data_ptr<float>(); }
 
+// ---------------------------------------------------------------- deferred column sums
+// The bias / norm-weight gradients that kernels reduce into the gradient arena
+// (LayerNorm γ/β and the fused residual bias, fc1's bias in the dGELU epilogue,
+// the QKV bias in the attention backward) are column sums of fp32 partial rows.
+// Inside a colsum_defer(true) window (the trainer's backward) they are queued
+// with their partial buffers kept alive and run by colsum_flush() as a few
+// batched launches — before each bucket all-reduce and at the end of the
+// backward — instead of two launches per parameter group (194 per GPT-2-medium
+// step).  Only arena destinations (accumulate) are deferred.
+struct PendingColsum {
+  at::Tensor keep;
+  pdo::ColsumJob job;
+};
+static std::vector<PendingColsum> g_colsum_q;
+static bool g_colsum_defer = false;
+
+static void colsum_or_defer(const at::Tensor& part, int G, int C, int ld, const pdo::ColOut& co, bool defer_ok) {
+  const float* p = fp(part);
+  float* scratch = fp(part) + (size_t)G * ld;
+  if (g_colsum_defer && defer_ok) {
+    g_colsum_q.push_back({part, pdo::ColsumJob{p, scratch, G, C, ld, co}});
+    return;
+  }
+  pdo::colsum(p, G, C, ld, co, scratch, cur_stream());
+}
+
+// destinations of two jobs overlap (both accumulate into the same arena slice,
+// e.g. a LayerNorm run by two graphs before one backward)
+static bool colsum_overlap(const pdo::ColsumJob& a, const pdo::ColsumJob& b) {
+  auto segs = [](const pdo::ColsumJob& j, int k, const bf16*& lo, const bf16*& hi) {
+    if (!j.co.p[k]) return false;
+    const int n = j.C < (k + 1) * j.co.seg ? j.C - k * j.co.seg : j.co.seg;
+    lo = j.co.p[k];
+    hi = j.co.p[k] + (n > 0 ? n : 0);
+    return n > 0;
+  };
+  for (int i = 0; i < 3; ++i) {
+    const bf16 *alo, *ahi;
+    if (!segs(a, i, alo, ahi)) continue;
+    for (int k = 0; k < 3; ++k) {
+      const bf16 *blo, *bhi;
+      if (segs(b, k, blo, bhi) && alo < bhi && blo < ahi) return true;
+    }
+  }
+  return false;
+}
+
+void colsum_flush() {
+  if (g_colsum_q.empty()) return;
+  // jobs of one batched launch run concurrently: a job whose destination another
+  // job of the batch also accumulates into starts the next batch (launch order
+  // keeps the read-modify-writes ordered)
+  std::vector<pdo::ColsumJob> jobs;
+  jobs.reserve(g_colsum_q.size());
+  for (const auto& q : g_colsum_q) {
+    bool clash = false;
+    for (const auto& j : jobs) clash = clash || colsum_overlap(j, q.job);
+    if (clash) {
+      CHECK_RC(pdo::colsum_batched(jobs.data(), (int)jobs.size(), cur_stream()), "colsum_batched");
+      jobs.clear();
+    }
+    jobs.push_back(q.job);
+  }
+  CHECK_RC(pdo::colsum_batched(jobs.data(), (int)jobs.size(), cur_stream()), "colsum_batched");
+  g_colsum_q.clear();  // the partial buffers return to the caching allocator in stream order
+}
+
+// returns the previous mode; turning deferral off flushes the queue
+bool colsum_defer(bool on) {
+  const bool prev = g_colsum_defer;
+  if (!on) colsum_flush();
+  g_colsum_defer = on;
+  return prev;
+}
+
+int64_t colsum_pending() { return (int64_t)g_colsum_q.size(); }
+
 // ---------------------------------------------------------------- layernorm
 std::vector<at::Tensor> layernorm_fwd(at::Tensor x, at::Tensor w, at::Tensor b, double eps) {
   CHECK_IN(x); CHECK_IN(w); CHECK_IN(b); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b);
@@ -101,7 +178,9 @@ std::vector<at::Tensor> ln_bwd_impl(at::Tensor dy, at::Tensor x, at::Tensor w, a
     for (int i = 0; i < NA; ++i) co.p[i] = bp(out) + (size_t)i * C;
   }
   CHECK_RC(pdo::layernorm_bwd(bp(dy), bp(x), bp(w), fp(mean), fp(rstd), dr, bp(dx), fp(part),
-                              fp(part) + (size_t)G * NA * C, co, rbias, N, C, cur_stream()), "layernorm_bwd");
+                              fp(part) + (size_t)G * NA * C, co, rbias, N, C, cur_stream(), false), "layernorm_bwd");
+  // scratch must follow the partial rows (colsum_or_defer's layout): ld = NA·C
+  colsum_or_defer(part, G, NA * C, NA * C, co, grads.has_value());
   if (grads.has_value()) return {dx};
   if (rbias) return {dx, out[0], out[1], out[2]};
   return {dx, out[0], out[1]};
@@ -301,6 +380,29 @@ bool gemm_dw(at::Tensor dy, at::Tensor x, at::Tensor out, bool accumulate, int64
   return true;
 }
 
+// every matrix of `table` (int64 [n, 5]: first tile, src offset, dst offset, R, C)
+// transposed from src into dst in one launch (ops: the step's Wᵀ operands).
+// `host` is the CPU tensor the device `table` was copied from: the entries are
+// validated there, so no device → host copy runs per call.
+void transpose_batched(at::Tensor src, at::Tensor dst, at::Tensor table, at::Tensor host, int64_t tiles) {
+  CHECK_IN(src); CHECK_IN(dst); CHECK_IN(table); CHECK_BF16(src); CHECK_BF16(dst);
+  TORCH_CHECK(table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 5, "table: int64 [n, 5]");
+  TORCH_CHECK(!host.is_cuda() && host.scalar_type() == at::kLong && host.is_contiguous() &&
+              host.sizes() == table.sizes(), "transpose_batched: host table must mirror the device table");
+  const at::Tensor& t = host;
+  const int64_t* e = t.data_ptr<int64_t>();
+  int64_t want = 0;
+  for (int64_t i = 0; i < t.size(0); ++i, e += 5) {
+    TORCH_CHECK(e[0] == want && e[3] % 64 == 0 && e[4] % 64 == 0 && e[3] > 0 && e[4] > 0, "transpose_batched: bad entry ", i);
+    TORCH_CHECK(e[1] >= 0 && e[1] + e[3] * e[4] <= src.numel() && e[2] >= 0 && e[2] + e[3] * e[4] <= dst.numel(),
+                "transpose_batched: entry ", i, " out of range");
+    want += (e[3] / 64) * (e[4] / 64);
+  }
+  TORCH_CHECK(want == tiles, "transpose_batched: tile count mismatch");
+  CHECK_RC(pdo::transpose_bf16_batched(bp(src), bp(dst), reinterpret_cast<const long long*>(table.data_ptr<int64_t>()), (int)table.size(0), tiles,
+                                       cur_stream()), "transpose_batched");
+}
+
 // ---- forward-layout GEMM with fused epilogues (gemm_nt.hip) ----
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
   return M < (1LL << 31) && N < (1LL << 31) && pdo::gemm_nt_ok((int)M, (int)N, (int)K, (int)K, (int)K, (int)N);
@@ -398,7 +500,7 @@ std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre
     db = at::empty_like(bias);
     co = pdo::ColOut::one(bp(db), N);
   }
-  pdo::colsum(fp(part), G, N, N, co, fp(part) + (size_t)G * N, cur_stream());
+  colsum_or_defer(part, G, N, N, co, db_out.has_value());
   if (db_out.has_value()) return {dx};
   return {dx, db};
 }
@@ -861,7 +963,7 @@ std::vector<at::Tensor> attn_bwd(at::Tensor dout, at::Tensor qkv, at::Tensor o, 
     db = at::empty({NC}, qkv.options());
     co = pdo::ColOut::one(bp(db), NC);
   }
-  pdo::colsum(fp(part), G, NC, NC, co, fp(part) + (size_t)G * NC, cur_stream());
+  colsum_or_defer(part, G, NC, NC, co, db_out.has_value());
   if (db_out.has_value()) return {dqkv};
   return {dqkv, db};
 }
@@ -877,6 +979,14 @@ void scale_dev_(at::Tensor x, at::Tensor s) {
   CHECK_IN(x); CHECK_BF16(x); CHECK_IN(s);
   TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() >= 1, "scale must be an fp32 device scalar");
   CHECK_RC(pdo::scale_dev_bf16(bp(x), x.numel(), fp(s), cur_stream()), "scale_dev_bf16");
+}
+
+// y += s[0] · x in place (bf16, same length; s: fp32 device scalar)
+void axpy_dev_(at::Tensor y, at::Tensor x, at::Tensor s) {
+  CHECK_IN(y); CHECK_IN(x); CHECK_BF16(y); CHECK_BF16(x); CHECK_IN(s);
+  TORCH_CHECK(y.numel() == x.numel(), "axpy_dev_: length mismatch");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() >= 1, "scale must be an fp32 device scalar");
+  CHECK_RC(pdo::axpy_dev_bf16(bp(y), bp(x), y.numel(), fp(s), cur_stream()), "axpy_dev_bf16");
 }
 
 // g += h; h = 0 (bf16, same length)
@@ -1038,6 +1148,11 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("sgd_flat", &sgd_flat);
   m.def("splitk_add", &splitk_add);
   m.def("transpose", &transpose, py::arg("x"), py::arg("out") = py::none());
+  m.def("transpose_batched", &transpose_batched);
+  m.def("colsum_defer", &colsum_defer);
+  m.def("colsum_flush", &colsum_flush);
+  m.def("colsum_pending", &colsum_pending);
+  m.def("axpy_dev_", &axpy_dev_);
   m.def("gemm_dw", &gemm_dw, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = true,
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);

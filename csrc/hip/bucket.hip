@@ -87,6 +87,28 @@ __global__ __launch_bounds__(256) void fold_zero_kernel(bf16* __restrict__ g, bf
   }
 }
 
+// y += *s · x in fp32, one rounding (a private gradient added into the arena,
+// scaled by the loss gradient read on device)
+__global__ __launch_bounds__(256) void axpy_dev_kernel(bf16* __restrict__ y, const bf16* __restrict__ x,
+                                                       long long nvec, const float* __restrict__ s) {
+  const float f = *s;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    bf16x8* py = reinterpret_cast<bf16x8*>(y) + i;
+    const f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(x)[i]);
+    f32x8 yv = to_f32(*py);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) yv[k] = __builtin_fmaf(xv[k], f, yv[k]);
+    *py = to_bf16(yv);
+  }
+}
+
+int axpy_dev_bf16(bf16* y, const bf16* x, long long n, const float* s, hipStream_t st) {
+  if (n % 8) return -2;
+  if (n == 0) return 0;
+  axpy_dev_kernel<<<stream_grid(n / 8, 256), 256, 0, st>>>(y, x, n / 8, s);
+  return 0;
+}
+
 int scale_dev_bf16(bf16* x, long long n, const float* s, hipStream_t st) {
   if (n % 8) return -2;
   if (n == 0) return 0;

@@ -29,14 +29,31 @@ int layernorm_fwd(const bf16* x, const bf16* r, const bf16* rb, const bf16* w, c
                   float* mean, float* rstd, int N, int C, float eps, hipStream_t st);
 int layernorm_bwd_grid(int N);
 // out: where dgamma | dbeta | (drbias) go (ColOut segments of C columns)
+// reduce = false: only the partial rows are written (the caller reduces part later)
 int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
                   const bf16* dres, bf16* dx, float* part, float* scratch, const ColOut& out, bool rbias, int N,
-                  int C, hipStream_t st);
+                  int C, hipStream_t st, bool reduce = true);
 
 // reduce.hip
 int colsum_scratch_floats(int G, int C);
 void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st);
 void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* scratch, hipStream_t st);
+// A column sum to run later (deferred bias / norm-weight gradients): part [G][ld]
+// f32 → co; scratch ≥ colsum_scratch_floats(G, C).  colsum_batched runs n of them
+// in two launches per COLSUM_BATCH jobs (the jobs are passed as kernel arguments).
+struct ColsumJob {
+  const float* part;
+  float* scratch;
+  int G, C, ld;
+  ColOut co;
+};
+constexpr int COLSUM_BATCH = 24;
+struct ColsumBatch {
+  int n;
+  int l1[COLSUM_BATCH + 1], l2[COLSUM_BATCH + 1];
+  ColsumJob j[COLSUM_BATCH];
+};
+int colsum_batched(const ColsumJob* jobs, int n, hipStream_t st);
 int bias_grad_scratch_floats(long long N, int F);
 int bias_grad(const bf16* dy, long long N, int F, bf16* db, float* scratch, hipStream_t st, int accumulate = 0);
 // NHWC BatchNorm (+ReLU, +residual) training forward / backward (batchnorm.hip)
@@ -143,6 +160,10 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
 void gemm_nt_set_impl(int impl);
 int gemm_nt_get_impl();
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
+// every matrix of a table in one launch: table = n × {first tile, src offset, dst
+// offset, R, C} int64 (device), elements relative to src / dst; tiles = Σ (R/64)(C/64)
+int transpose_bf16_batched(const bf16* src, bf16* dst, const long long* table, int n, long long tiles,
+                           hipStream_t st);
 int splitk_add(const bf16* part, int s, long long n, bf16* out, int accumulate, hipStream_t st);
 
 // gelu.hip
@@ -191,6 +212,8 @@ int bucket_copy(int dtype, bool flatten, void* flat, long long total, int n, voi
 int cast_scale_bf16_f32(const bf16* src, float* dst, long long n, float s, hipStream_t st);
 int scale_bf16(bf16* x, long long n, float s, hipStream_t st);
 int scale_dev_bf16(bf16* x, long long n, const float* s, hipStream_t st);
+// y = bf16(y + s·x) with the fp32 scale read on device
+int axpy_dev_bf16(bf16* y, const bf16* x, long long n, const float* s, hipStream_t st);
 int fold_zero_bf16(bf16* g, bf16* h, long long n, hipStream_t st);
 
 }  // namespace pdo

@@ -226,7 +226,7 @@ int layernorm_bwd_grid(int N) {
 // scratch: colsum_scratch_floats(grid, NA*C)
 int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mean, const float* rstd,
                   const bf16* dres, bf16* dx, float* part, float* scratch, const ColOut& out, bool rbias, int N,
-                  int C, hipStream_t st) {
+                  int C, hipStream_t st, bool reduce) {
   if (C % 8 != 0 || C > 4096) return -2;
   if (rbias && !dres) return -4;
   if (out.seg != C) return -5;
@@ -241,7 +241,7 @@ int layernorm_bwd(const bf16* dy, const bf16* x, const bf16* w, const float* mea
   } else {
     LN_DISPATCH(vpl, ln_bwd_kernel<V, false, 2><<<grid, 256, 0, st>>>(dy, x, w, mean, rstd, dres, dx, part, N, C))
   }
-  colsum(part, grid, NA * C, NA * C, out, scratch, st);
+  if (reduce) colsum(part, grid, NA * C, NA * C, out, scratch, st);
   return 0;
 }
 

@@ -14,12 +14,15 @@ namespace pdo {
 
 constexpr int RPB = 64;  // rows per level-1 workgroup
 
-__global__ __launch_bounds__(512) void colsum_f32_pass(const float* __restrict__ in, int G, int C, int ld, int rpb,
-                                                       float* __restrict__ out_part, ColOut co) {
-  __shared__ f32x4 red[8][64];
+// one level-1 / level-2 block of the column sum: columns (bx·64 + lane)·4 ..+3,
+// rows [by·rpb, by·rpb + rpb); 8 waves stride the rows, combine in LDS, and
+// the block writes a partial row (out_part) or the final bf16 values (co)
+__device__ __forceinline__ void colsum_block(const float* __restrict__ in, int G, int C, int ld, int rpb,
+                                             float* __restrict__ out_part, const ColOut& co, int bx, int by,
+                                             f32x4 (*red)[64]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col = (blockIdx.x * 64 + lane) * 4;
-  const int r0 = blockIdx.y * rpb;
+  const int col = (bx * 64 + lane) * 4;
+  const int r0 = by * rpb;
   const int r1 = min(G, r0 + rpb);
   f32x4 s = {0, 0, 0, 0};
   if (col < C) {
@@ -44,9 +47,15 @@ __global__ __launch_bounds__(512) void colsum_f32_pass(const float* __restrict__
       bf16x4 o = {(bf16)t[0], (bf16)t[1], (bf16)t[2], (bf16)t[3]};
       *reinterpret_cast<bf16x4*>(dst) = o;
     } else {
-      *reinterpret_cast<f32x4*>(out_part + (size_t)blockIdx.y * C + col) = t;
+      *reinterpret_cast<f32x4*>(out_part + (size_t)by * C + col) = t;
     }
   }
+}
+
+__global__ __launch_bounds__(512) void colsum_f32_pass(const float* __restrict__ in, int G, int C, int ld, int rpb,
+                                                       float* __restrict__ out_part, ColOut co) {
+  __shared__ f32x4 red[8][64];
+  colsum_block(in, G, C, ld, rpb, out_part, co, blockIdx.x, blockIdx.y, red);
 }
 
 __global__ __launch_bounds__(512) void colsum_bf16_pass(const bf16* __restrict__ in, int N, int F, int rpb,
@@ -89,6 +98,59 @@ void colsum(const float* part, int G, int C, int ld, const ColOut& out, float* s
 
 void colsum(const float* part, int G, int C, int ld, bf16* out, float* scratch, hipStream_t st) {
   colsum(part, G, C, ld, ColOut::one(out, C), scratch, st);
+}
+
+// ---- many column sums in two launches (deferred bias / norm-weight gradients) ----
+// Level 1: every job's (column stripe × row slice) blocks back to back in one
+// grid — a job of ≤ RPB rows is finished here, the others write partial rows
+// to their scratch; level 2 folds those.  Jobs travel as kernel arguments.
+__device__ __forceinline__ int batch_job(const int* start, int n, int b) {
+  int e = 0;
+  while (e + 1 < n && b >= start[e + 1]) ++e;
+  return e;
+}
+
+__global__ __launch_bounds__(512) void colsum_batch_l1(ColsumBatch bt) {
+  __shared__ f32x4 red[8][64];
+  const int e = batch_job(bt.l1, bt.n, blockIdx.x);
+  const ColsumJob& j = bt.j[e];
+  const int b = blockIdx.x - bt.l1[e], gx = (j.C / 4 + 63) / 64;
+  const int gs = (j.G + RPB - 1) / RPB;
+  colsum_block(j.part, j.G, j.C, j.ld, RPB, j.scratch, gs == 1 ? j.co : ColOut{}, b % gx, b / gx, red);
+}
+
+__global__ __launch_bounds__(512) void colsum_batch_l2(ColsumBatch bt) {
+  __shared__ f32x4 red[8][64];
+  const int e = batch_job(bt.l2, bt.n, blockIdx.x);
+  const ColsumJob& j = bt.j[e];
+  const int gs = (j.G + RPB - 1) / RPB;
+  colsum_block(j.scratch, gs, j.C, j.C, gs, nullptr, j.co, blockIdx.x - bt.l2[e], 0, red);
+}
+
+int colsum_batched(const ColsumJob* jobs, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += COLSUM_BATCH) {
+    ColsumBatch bt{};
+    bt.n = n - i0 < COLSUM_BATCH ? n - i0 : COLSUM_BATCH;
+    int b1 = 0, b2 = 0;
+    for (int e = 0; e < bt.n; ++e) {
+      const ColsumJob& j = jobs[i0 + e];
+      if (j.C % 4 || j.G < 1 || !j.co.p[0]) return -2;
+      bt.j[e] = j;
+      const int gx = (j.C / 4 + 63) / 64, gs = (j.G + RPB - 1) / RPB;
+      bt.l1[e] = b1;
+      bt.l2[e] = b2;
+      b1 += gx * gs;
+      if (gs > 1) b2 += gx;
+    }
+    bt.l1[bt.n] = b1;
+    bt.l2[bt.n] = b2;
+    colsum_batch_l1<<<b1, 512, 0, st>>>(bt);
+    if (b2) {
+      // jobs finished in level 1 get no level-2 blocks: their l2 range is empty
+      colsum_batch_l2<<<b2, 512, 0, st>>>(bt);
+    }
+  }
+  return 0;
 }
 
 int bias_grad_scratch_floats(long long N, int F) {

@@ -16,11 +16,9 @@ namespace pdo {
 constexpr int TT = 64;       // tile edge
 constexpr int TLD = TT + 8;  // LDS row pitch (elements): 144 B keeps 16-B alignment
 
-__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
-                                                             int R, int C) {
-  __shared__ __attribute__((aligned(16))) bf16 t[TT * TLD];
-  const int tiles_c = C / TT;
-  const int tr = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+// one 64×64 tile (tr, tc) of out[C][R] = in[R][C]
+__device__ __forceinline__ void transpose_tile(const bf16* __restrict__ in, bf16* __restrict__ out, int R, int C,
+                                               int tr, int tc, bf16* t) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -39,6 +37,40 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
     for (int e = 0; e < 8; ++e) v[e] = t[(rg * 8 + e) * TLD + col];
     *reinterpret_cast<bf16x8*>(out + (size_t)(tc * TT + c) * R + tr * TT + rg * 8) = v;
   }
+}
+
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                             int R, int C) {
+  __shared__ __attribute__((aligned(16))) bf16 t[TT * TLD];
+  const int tiles_c = C / TT;
+  transpose_tile(in, out, R, C, blockIdx.x / tiles_c, blockIdx.x % tiles_c, t);
+}
+
+// The step's weight transposes (every dX GEMM's Wᵀ operand, GPT-2: 97 matrices)
+// in one launch: block b belongs to the table entry whose first tile is the
+// last one ≤ b (binary search over the n entries).
+__global__ __launch_bounds__(256) void transpose_bf16_batched_kernel(const bf16* __restrict__ src,
+                                                                     bf16* __restrict__ dst,
+                                                                     const long long* __restrict__ table, int n) {
+  __shared__ __attribute__((aligned(16))) bf16 t[TT * TLD];
+  const long long b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (table[5 * mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long* e = table + 5 * lo;
+  const int R = (int)e[3], C = (int)e[4];
+  const int local = (int)(b - e[0]), tiles_c = C / TT;
+  transpose_tile(src + e[1], dst + e[2], R, C, local / tiles_c, local % tiles_c, t);
+}
+
+int transpose_bf16_batched(const bf16* src, bf16* dst, const long long* table, int n, long long tiles,
+                           hipStream_t st) {
+  if (n < 1 || tiles < 1 || tiles > 0x7fffffffLL) return -2;
+  transpose_bf16_batched_kernel<<<(unsigned)tiles, 256, 0, st>>>(src, dst, table, n);
+  return 0;
 }
 
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st) {

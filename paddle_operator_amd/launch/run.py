@@ -97,7 +97,7 @@ def run_collective(args, jenv) -> int:
         st, start_step = ckpt.load_latest(args.ckpt_dir)
         if st is not None:
             if args.workload == "gpt2":
-                trainer.flat.params.copy_(st["params"].to(dev))
+                trainer.flat.load_params(st["params"])
                 trainer.opt.load_state_dict({k: v.to(dev) if torch.is_tensor(v) else v
                                              for k, v in st["opt"].items()})
             else:

@@ -347,6 +347,15 @@ def _input_grad(dy2, w):
     return dy2 @ w
 
 
+def _live_wt(w):
+    """The arena's prebuilt Wᵀ of ``w`` (parallel.flat.FlatParams.enable_wt) while
+    it is live (inside the trainer's wt_scope), else None."""
+    t = getattr(w, "_pdo_wt", None)
+    if t is not None and t[0].wt_live:
+        return t[1]
+    return None
+
+
 def _transposable(w) -> bool:
     return (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] % 64 == 0
             and w.shape[1] % 64 == 0 and w.is_contiguous())
@@ -358,6 +367,10 @@ def transpose(w, out=None):
     (Measured, round 3: the step's 97 transposes prefetched on a side stream
     under the forward GEMMs made the step 1 ms slower — 148.2 vs 147.2 ms,
     profiles/r3_attention_variants_a5.md — so they stay in-stream.)"""
+    if out is None:
+        wt = _live_wt(w)
+        if wt is not None:
+            return wt
     if _transposable(w):
         if out is not None:
             return _native.require_hip().transpose(w, out)
@@ -438,6 +451,33 @@ def _arena_grads(params):
             return None
         out.append(p.grad.view(-1))
     return out
+
+
+class deferred_reductions:
+    """Scope (the trainer's backward) in which the bias / norm-weight gradient
+    column sums that kernels reduce into the arena are queued and run in a few
+    batched launches (``flush_deferred``: before each bucket all-reduce, and on
+    exit) — csrc/hip/bind.cpp colsum_or_defer."""
+
+    def __init__(self, device):
+        self.on = torch.device(device).type == "cuda" and _native.ops_mode() != "torch"
+        self.prev = False
+
+    def __enter__(self):
+        if self.on:
+            self.prev = _native.require_hip().colsum_defer(True)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _native.require_hip().colsum_defer(self.prev)  # off: flushes the queue
+
+
+def flush_deferred():
+    """Run the queued column sums now (stream-ordered; a no-op when none)."""
+    m = _native.hip_ext()
+    if m is not None and m.colsum_pending():
+        m.colsum_flush()
 
 
 def _signal_ready(params):
@@ -747,11 +787,13 @@ class _LMHeadXentFn(torch.autograd.Function):
     """loss = CE(h·Wᵀ, target) with the LM head and the cross-entropy run over
     token chunks: per chunk the logits GEMM (gemm_nt4), the softmax statistics,
     dlogits written in place, the chunk's dX GEMM and its dW GEMM accumulated
-    into one [Vp, C] gradient — so only a [chunk, Vp] logits buffer exists
-    (16384 tokens: 1.6 GB instead of the 6.6 GB [65536, 50304] tensor).  The
-    gradients are computed in the forward, for dloss = 1, and scaled by dloss in
-    the backward (the loss is the graph's last node).  Chunks of 16384 tokens
-    keep the dX GEMM at ≥ 256 output tiles (one per CU)."""
+    into one [Vp, C] gradient — so only a [chunk, Vp] logits buffer exists.
+    The chunk is ``PDO_LM_CHUNK`` tokens (``lm_head_xent``): 16384 caps the
+    buffer at 1.6 GB; the default (-1) is one chunk of every token, i.e. the
+    whole [tokens, Vp] logits tensor (6.6 GB at GPT-2-medium B = 64), which
+    ran 0.5 ms/step faster (profiles/r3_xent_fused.md).  The gradients are
+    computed in the forward, for dloss = 1, and applied scaled by dloss in the
+    backward (the loss is the graph's last node)."""
 
     @staticmethod
     def forward(ctx, h, w, target, vocab, chunk):
@@ -768,11 +810,13 @@ class _LMHeadXentFn(torch.autograd.Function):
         inv_cnt = (1.0 / valid.clamp(min=1.0)).reshape(1)
         logits = torch.empty(chunk, Vp, device=h.device, dtype=h.dtype)
         dh = torch.empty_like(h2)
-        # a split tied weight (parallel/flat.py): dW goes straight into its
-        # head-gradient arena slot, all-reduced as bucket 0 once the backward starts
+        # dW stays private to this node until its backward: a split tied weight
+        # (parallel/flat.py) then adds it, scaled by dloss, into its head-gradient
+        # slot (bucket 0) — two forwards before one backward each add their own
+        # part, and a forward whose graph is dropped leaves the slot untouched
         sp = getattr(w, "_pdo_split", None)
         ctx.split = sp
-        dw = sp.grad if sp is not None else torch.empty(Vp, C, device=h.device, dtype=h.dtype)
+        dw = torch.empty(Vp, C, device=h.device, dtype=h.dtype)
         loss_sum = torch.zeros((), device=h.device, dtype=torch.float32)
         for c0 in range(0, N, chunk):
             hc, tc = h2[c0:c0 + chunk], t[c0:c0 + chunk]
@@ -793,7 +837,7 @@ class _LMHeadXentFn(torch.autograd.Function):
                     dw.copy_(dl.t() @ hc)
                 else:
                     dw.addmm_(dl.t(), hc)
-        ctx.save_for_backward(dh, dw if sp is None else None)
+        ctx.save_for_backward(dh, dw)
         ctx.shape = h.shape
         return loss_sum if fused else loss_sum / valid
 
@@ -808,7 +852,7 @@ class _LMHeadXentFn(torch.autograd.Function):
         m.scale_dev_(dh, d)
         sp = ctx.split
         if sp is not None:
-            m.scale_dev_(sp.grad, d)
+            m.axpy_dev_(sp.grad.view(-1), dw.view(-1), d)  # slot += dloss · dW, one rounding
             sp.ready(sp)
             return dh.view(ctx.shape), None, None, None, None
         m.scale_dev_(dw, d)

@@ -34,7 +34,7 @@ class FlatAdamW:
 
     def grad_norm_sq(self, grad_scale=1.0):
         """Device scalar of ||grad_scale * g||^2 (no sync)."""
-        g = self.flat.grads
+        g = self.flat.param_grads
         if use_hip(g):
             m = _native.require_hip()
             m.sumsq(g, self._norm_buf, grad_scale)
@@ -54,14 +54,14 @@ class FlatAdamW:
         if clip > 0:
             self.grad_norm_sq(grad_scale)
         f = self.flat
-        if use_hip(f.grads):
+        if use_hip(f.param_grads):
             m = _native.require_hip()
-            m.adamw_flat(f.params, f.grads, self.master, self.m, self.v, f.decay_chunks,
+            m.adamw_flat(f.params, f.param_grads, self.master, self.m, self.v, f.decay_chunks,
                          self._norm_buf, lr, self.b1, self.b2, self.eps, self.wd,
                          bc1, bc2, grad_scale, clip)
             return
         # reference path (fp32 math, identical formula to the kernel)
-        g = f.grads.float() * grad_scale
+        g = f.param_grads.float() * grad_scale
         if clip > 0:
             norm = torch.sqrt(self._norm_buf[0])
             g = g * torch.clamp(clip / (norm + 1e-6), max=1.0)
@@ -77,6 +77,8 @@ class FlatAdamW:
         return {"master": self.master, "m": self.m, "v": self.v, "step": self.step_count}
 
     def load_state_dict(self, sd):
+        if sd["master"].numel() != self.master.numel():
+            raise ValueError(f"optimizer state has {sd['master'].numel()} elements, the arena {self.master.numel()}")
         self.master.copy_(sd["master"])
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])

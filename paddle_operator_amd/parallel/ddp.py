@@ -59,7 +59,7 @@ class BucketedDDP:
         # an fp32 arena is reduced in fp32 either way (no staging needed)
         self.stage = None
         if mode == "fp32" and flat.dtype != torch.float32 and self.enabled:
-            self.stage = torch.zeros(flat.numel, dtype=torch.float32, device=flat.device)
+            self.stage = torch.zeros(flat.grads.numel(), dtype=torch.float32, device=flat.device)
         self.grad_reduce = "fp32" if (mode == "fp32" or flat.dtype == torch.float32) else "bf16"
         self._pending = [0] * len(flat.buckets)
         self._sizes = [len(b.slots) for b in flat.buckets]
@@ -116,6 +116,7 @@ class BucketedDDP:
     def finish(self):
         """Call after backward: launch stragglers, make the compute stream wait,
         then fold split parameters' head-gradient slots into their gradients."""
+        _flush_reductions(buf_device=self.flat.device)
         if self.enabled and self._sync:
             while self._next < len(self.flat.buckets):
                 self._launch(self._next)
@@ -161,6 +162,9 @@ class BucketedDDP:
 
     def _launch(self, i):
         b = self.flat.buckets[i]
+        # queued bias / norm-weight column sums land in the arena first
+        # (ops.deferred_reductions; stream-ordered before the all-reduce)
+        _flush_reductions(buf_device=self.flat.device)
         self._launched[i] = True
         self._next = i + 1
         buf = self.flat.grads[b.start:b.end]
@@ -183,6 +187,12 @@ class BucketedDDP:
             _native.require_hip().cast_f32_bf16(st, g)
         else:
             g.copy_(st)
+
+
+def _flush_reductions(buf_device):
+    if buf_device.type == "cuda":
+        from ..ops import flush_deferred
+        flush_deferred()
 
 
 def _cast_scale(src: torch.Tensor, dst: torch.Tensor, scale: float):

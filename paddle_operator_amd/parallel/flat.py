@@ -18,11 +18,14 @@ SURVEY §2.4 "GPU collectives — no call site in the reference"):
   one float per ``ALIGN`` elements;
 * ``split`` names (the tied ``wte``): the parameter's gradient has two
   producers far apart in the backward — the LM head (first node of the
-  backward) and the embedding (last).  The LM-head part gets its own arena slot
-  at the FRONT of the ready order (``AuxGrad``, bucket 0), so its all-reduce
+  backward) and the embedding (last).  The LM-head part gets its own gradient
+  slot (``AuxGrad``) that is bucket 0 of the ready order, so its all-reduce
   overlaps the whole backward; only the embedding part stays in the last
   bucket.  ``fold_split()`` adds the reduced head part into the parameter's
-  gradient and zeroes the slot (the optimizer never sees it).
+  gradient and zeroes the slot.  The slot sits AFTER the parameter range of
+  the gradient buffer: ``params`` / the optimizer state / checkpoints cover
+  only ``[0, numel)`` and are the same with or without a split
+  (``param_grads`` is the optimizer's view of the gradients).
 """
 from __future__ import annotations
 
@@ -104,18 +107,21 @@ class FlatParams:
         unknown = set(split) - set(params)
         if unknown:
             raise ValueError(f"split names not among the trainable parameters: {sorted(unknown)}")
-        self.aux_slots: list[Slot] = []
         off = 0
-        for n in split:
-            p = params[n]
-            self.aux_slots.append(Slot(n + "#head", None, off, p.numel(), p.shape, False))
-            off = _round_up(off + p.numel(), ALIGN)
         for n, p in order:
             self.slots.append(Slot(n, p, off, p.numel(), p.shape, not no_decay(n, p)))
             off = _round_up(off + p.numel(), ALIGN)
-        self.numel = off
+        self.numel = off  # the parameter range: params, optimizer state, checkpoints
+        # split parameters' head-gradient slots after the parameter range (bucket 0)
+        self.aux_slots: list[Slot] = []
+        goff = off
+        for n in split:
+            p = params[n]
+            self.aux_slots.append(Slot(n + "#head", None, goff, p.numel(), p.shape, False))
+            goff = _round_up(goff + p.numel(), ALIGN)
         self.params = torch.zeros(off, dtype=dtype, device=device)
-        self.grads = torch.zeros(off, dtype=dtype, device=device)
+        self.grads = torch.zeros(goff, dtype=dtype, device=device)
+        self.param_grads = self.grads[:off]
         # keep each parameter's memory format (e.g. channels_last conv weights
         # for MIOpen NHWC kernels): the arena slice is viewed with its strides
         self._strides = {}
@@ -175,6 +181,48 @@ class FlatParams:
                 self._wt_max = max(self._wt_max, R * S * ((K + 63) // 64) * ((C + 63) // 64))  # 64 × 64 tiles
             self._wt_table = torch.tensor(rows, dtype=torch.int32, device=self.device)
 
+    def enable_wt(self):
+        """A transposed copy Wᵀ of every 2-D weight (dims multiples of 64), for the
+        input-gradient GEMMs dX = dY·W that run as F.linear(dY, Wᵀ) on gemm_nt:
+        built for all of them in ONE launch per step (``wt_scope``) instead of one
+        transpose per weight per backward.  Each such parameter gets
+        ``_pdo_wt = (arena, Wᵀ view)``, read only while ``arena.wt_live``."""
+        rows, tile = [], 0
+        for s in self.slots:
+            p = s.param
+            if len(s.shape) == 2 and s.shape[0] % 64 == 0 and s.shape[1] % 64 == 0 and p.is_contiguous():
+                R, C = s.shape
+                rows.append((tile, s.offset, s.offset, R, C))
+                tile += (R // 64) * (C // 64)
+        self.wt, self.wt_live = None, False
+        if not rows or self.device.type != "cuda" or self.dtype != torch.bfloat16:
+            return
+        self.wt = torch.empty(self.numel, dtype=self.dtype, device=self.device)
+        self._wt_host = torch.tensor(rows, dtype=torch.int64)
+        self._wt_dev = self._wt_host.to(self.device)
+        self._wt_tiles = tile
+        by_off = {s.offset: s for s in self.slots}
+        for (_, off, _, R, C) in rows:
+            by_off[off].param._pdo_wt = (self, self.wt[off:off + R * C].view(C, R))
+
+    def wt_scope(self):
+        """Build every Wᵀ (one launch) and mark them live for the scope: the
+        trainer's forward + backward, where the weights do not change."""
+        flat = self
+
+        class _Scope:
+            def __enter__(self):
+                if getattr(flat, "wt", None) is not None:
+                    from .. import _native
+                    _native.require_hip().transpose_batched(flat.params, flat.wt, flat._wt_dev, flat._wt_host,
+                                                            flat._wt_tiles)
+                    flat.wt_live = True
+
+            def __exit__(self, *exc):
+                flat.wt_live = False
+
+        return _Scope()
+
     def shadow_scope(self):
         flat = self
 
@@ -202,16 +250,20 @@ class FlatParams:
         esz = torch.empty((), dtype=self.dtype).element_size()
         cap = max(ALIGN, bucket_bytes // esz)
         buckets, cur = [], None
-        for s in self.aux_slots + self.slots:
-            if cur is None:
-                cur = Bucket(len(buckets), s.offset, s.offset)
-            cur.slots.append(s)
-            cur.end = _round_up(s.offset + s.numel, ALIGN)
-            if cur.numel >= cap:
+        # the head slots (after the parameter range) never share a bucket with
+        # parameters: a bucket is one contiguous slice of the gradient buffer
+        for group in (self.aux_slots, self.slots):
+            for s in group:
+                if cur is None:
+                    cur = Bucket(len(buckets), s.offset, s.offset)
+                cur.slots.append(s)
+                cur.end = _round_up(s.offset + s.numel, ALIGN)
+                if cur.numel >= cap:
+                    buckets.append(cur)
+                    cur = None
+            if cur is not None:
                 buckets.append(cur)
                 cur = None
-        if cur is not None:
-            buckets.append(cur)
         return buckets
 
     def bucket_of(self):
@@ -253,3 +305,12 @@ class FlatParams:
 
     def state_dict(self):
         return {s.name: s.param.detach() for s in self.slots}
+
+    def load_params(self, flat_params: torch.Tensor):
+        """Copy a checkpointed flat parameter buffer into the arena, refusing a
+        buffer of another layout (a different model or an arena from before the
+        head slot moved out of the parameter range)."""
+        if flat_params.numel() != self.numel:
+            raise ValueError(f"checkpoint arena has {flat_params.numel()} elements, this model's has {self.numel}: "
+                             "saved by a different model or arena layout")
+        self.params.copy_(flat_params.to(self.params.device))

@@ -15,6 +15,7 @@ import torch
 import torch.distributed as dist
 
 from .models.gpt2 import GPT2, GPT2Config
+from .ops import deferred_reductions
 from .ops.optim import FlatAdamW
 from .parallel.ddp import BucketedDDP
 from .parallel.flat import FlatParams
@@ -101,6 +102,8 @@ class GPT2Trainer:
         split = ("wte",) if os.environ.get("PDO_SPLIT_WTE", "1") != "0" else ()
         self.flat = FlatParams(model, dtype=dtype, device=self.device, bucket_bytes=bucket_bytes, late=("wte",),
                                split=split)
+        # every dX GEMM's Wᵀ operand built in one launch per step (wt_scope)
+        self.flat.enable_wt()
         self.ddp = BucketedDDP(self.flat)
         self.opt = FlatAdamW(self.flat, lr=lr)
         self.gen = torch.Generator(device=self.device)
@@ -120,10 +123,13 @@ class GPT2Trainer:
             idx, tgt = self.batch()
         self.flat.zero_grad()
         self.ddp.prepare()
-        with trace.range("forward"):
-            loss = self.model(idx, tgt)
-        with trace.range("backward"):
-            loss.backward()
+        with self.flat.wt_scope():
+            with trace.range("forward"):
+                loss = self.model(idx, tgt)
+            # bias / norm-weight column sums batched (flushed before each bucket
+            # all-reduce and at the end of the backward)
+            with trace.range("backward"), deferred_reductions(self.device):
+                loss.backward()
         with trace.range("allreduce_drain"):
             self.ddp.finish()
         with trace.range("optimizer"):

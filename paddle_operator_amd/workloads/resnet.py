@@ -38,7 +38,7 @@ class FlatSGD:
 
     @torch.no_grad()
     def step(self, grad_scale=1.0):
-        g = self.flat.grads
+        g = self.flat.param_grads
         if g.is_cuda and g.dtype == torch.float32:
             from .. import _native
             _native.require_hip().sgd_flat(self.flat.params, g, self.buf, self.flat.decay_chunks, self.lr, self.mom,

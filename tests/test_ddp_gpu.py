@@ -95,3 +95,51 @@ def test_ddp_ranks_hip_path_matches_full_batch(tmp_path, cuda, world):
         if not err < 3e-2:
             bad.append(f"{n}: rel err {err:.3g} (|ref| {r.abs().max().item():.3g}, |ddp| {g0[n].abs().max().item():.3g})")
     assert not bad, "\n".join(bad)
+
+
+def _split_grads(split, micro, two_forwards=False):
+    """Arena gradients of the trainer's HIP path (Wᵀ arena, deferred column sums,
+    DDP finish → fold_split) with or without the split tied-embedding slot."""
+    from paddle_operator_amd.models.gpt2 import GPT2
+    from paddle_operator_amd.ops import deferred_reductions
+    from paddle_operator_amd.parallel.ddp import BucketedDDP
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    cfg = _cfg()
+    dev = torch.device("cuda", 0)
+    model = GPT2(cfg).to(device=dev, dtype=torch.bfloat16)
+    flat = FlatParams(model, dtype=torch.bfloat16, device=dev, bucket_bytes=1 << 20, late=("wte",), split=split)
+    flat.enable_wt()
+    ddp = BucketedDDP(flat)
+    g = torch.Generator().manual_seed(7)
+    # few distinct ids: long runs of equal tokens in the sorted embedding backward
+    idx = torch.randint(0, 40, (micro, 4, 129), generator=g).to(dev)
+    flat.zero_grad()
+    for k in range(micro):  # gradient accumulation: no zero_grad between micro-steps
+        ddp.prepare()
+        with flat.wt_scope():
+            x, y = idx[k, :, :-1], idx[k, :, 1:]
+            loss = model(x, y)
+            if two_forwards:  # two graphs through the LM head before one backward
+                loss = loss + 0.5 * model(x.flip(0), y.flip(0))
+            with deferred_reductions(dev):
+                loss.backward()
+        ddp.finish()
+    torch.cuda.synchronize()
+    assert not any(float(a.param.grad.abs().max()) for a in flat.aux_slots), "head slot not folded"
+    return {n: p.grad.float().clone() for n, p in model.named_parameters()}
+
+
+@pytest.mark.parametrize("micro,two", [(1, False), (2, False), (1, True)])
+def test_split_wte_head_slot_matches_unsplit(cuda, micro, two):
+    """The default split tied embedding (LM-head dW in its own slot, scaled by
+    dloss in the LM head's backward; embedding dW by the sorted segment sum
+    straight into the arena) gives the gradients of the one-slot layout —
+    with accumulation micro-steps and two forwards before one backward."""
+    a = _split_grads(("wte",), micro, two)
+    b = _split_grads((), micro, two)
+    for n in a:
+        den = float(b[n].norm()) + 1e-12
+        err = float((a[n] - b[n]).norm()) / den
+        assert err < 2e-2, (n, err)

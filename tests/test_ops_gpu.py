@@ -463,6 +463,7 @@ def test_adamw_matches_reference(cuda):
         params_before = fp_.params.clone()
         ref.flat = type("F", (), {})()
         ref.flat.grads = g0.bfloat16()
+        ref.flat.param_grads = ref.flat.grads
         ref.flat.params = params_before
         ref.flat.decay_chunks = fp_.decay_chunks
         ref.flat.numel = fp_.numel
