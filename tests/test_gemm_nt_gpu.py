@@ -174,12 +174,17 @@ def test_nt4_half_width_last_tile(hip, impl):
     torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=3e-2, atol=0.5)
 
 
+@pytest.mark.parametrize("M,N", [(16384, 4096), (2048, 1024), (65536, 4096), (4352, 2048)])
 @pytest.mark.parametrize("impl", [1, 2])
-def test_nt4_fused_epilogues_many_tiles_vs_fp32(hip, impl):
-    """The GELU and GELU'+bias-grad epilogues on a grid with several tiles per
-    persistent workgroup (16384 x 4096 x 1024: 1024 tiles over 256 workgroups),
-    against fp32: pre-activation, activation, input gradient, bias gradient."""
-    M, N, K = 16384, 4096, 1024
+def test_nt4_fused_epilogues_many_tiles_vs_fp32(hip, impl, M, N):
+    """The GELU and GELU'+bias-grad epilogues against fp32 (pre-activation,
+    activation, input gradient, bias gradient) at K = 1024, where impl 1 defers
+    the activation pass under the next tile's k-loop (gemm_nt4.hip DEF): 4 tiles
+    per persistent workgroup (16384 x 4096), one (2048 x 1024: the first k-loop's
+    pass runs on the workgroup's own tile and is overwritten), 16 (the GPT-2-medium
+    fc1 / fc2-dX shape) and an uneven 2-3 (4352 x 2048: 136 tiles, 17 tile rows).
+    impl 2 = every epilogue immediate."""
+    K = 1024
     g = torch.Generator(device="cuda").manual_seed(21)
     a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
     b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
@@ -199,5 +204,7 @@ def test_nt4_fused_epilogues_many_tiles_vs_fp32(hip, impl):
     xp = (pre.float() + bias.float()).requires_grad_(True)
     torch.nn.functional.gelu(xp, approximate="tanh").backward(ref.to(torch.bfloat16).float())
     assert bool(((dx.float() - xp.grad).abs() <= 2e-2 + 1e-2 * xp.grad.abs()).all())
-    torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=2e-2, atol=0.5)
+    # the reference takes dy = bf16(A·Bᵀ); the immediate epilogue (impl 2) the fp32
+    # product: per-row differences of 2^-9 |dy| add up like √M over the column
+    torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=2e-2, atol=0.5 * (M / 16384) ** 0.5)
 
