@@ -242,9 +242,8 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
 }  // namespace
 
 // impl 0 = the 8-wave ring below; impl 1 (default) = the 4-wave persistent
-// mainloop (gemm_nt4.hip) wherever K allows it; impl 2 = impl 1 with the
-// deferred store drain (its A/B alternative, profiles/r3_nt4_deferred_drain.md).
-// PDO_NT_IMPL overrides (A/B in the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=1 PDO_NT_IMPL=2')
+// mainloop (gemm_nt4.hip) wherever K allows it.  PDO_NT_IMPL overrides (A/B in
+// the training step: tools/gpu.sh 'stepab:PDO_NT_IMPL=0 PDO_NT_IMPL=1')
 static int g_impl = [] {
   const char* e = getenv("PDO_NT_IMPL");
   return e && *e ? atoi(e) : 1;
@@ -272,7 +271,7 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
   if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
   if (epi == 3 && !dbias_part) return -3;
   if (nt4_path(K))
-    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st, g_impl == 2 ? 1 : 0);
+    return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st);
   const long long grid = (long long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffLL) return -2;
   const int nk = K / BK;

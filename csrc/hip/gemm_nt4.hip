@@ -38,21 +38,13 @@
 // writes LDS linearly (1 KiB = 8 rows per wave-instruction) and applies the
 // swizzle on the per-lane global source address.
 //
-// Deferred activation epilogues (DEF, EPI 2 and 3 at K = 1024: fc1 + GELU and
-// fc2 dX ⊙ GELU′).  With one wave per SIMD the GELU / GELU′ VALU work of a row
-// epilogue ran with the matrix pipe idle (≈ 7-11 VALU per output element,
-// profiles/r3_nt4_deferred_drain.md).  In DEF mode a tile's epilogue only
-// stores the raw product (bf16, 32 stores per wave) and the activation pass
-// runs during the NEXT tile's 16 k-tiles: k-tile t reloads chunk pair t of the
-// previous tile (2 × 1 KiB per wave and operand, LDS-DMA into a per-wave
-// staging ring after the operand buffers, issued one k-tile ahead), computes
-// its 16 elements per lane one pipeline stage per MFMA slot, and stores the
-// result after the k-tile's third barrier — the VALU work fills MFMA issue
-// gaps instead of serialising after them.  A CU's last tile keeps the
-// immediate epilogue.  (Earlier schedule variants — one barrier per k-tile,
-// LDS-staged / permlane epilogues, buffer_load DMA, non-persistent grids, the
-// deferred store drain — measured slower and were removed: profiles/r2_gemm_nt4.md,
-// profiles/r3_gemm_nt4_*.md, profiles/r3_nt4_deferred_drain.md.)
+// Measured and removed (numbers in profiles/): the round-2/3 schedule variants
+// — one barrier per k-tile, LDS-staged and permlane-transposed epilogues,
+// buffer_load DMA, non-persistent grids (r2_gemm_nt4.md, r3_gemm_nt4_*.md) —,
+// the deferred store drain (r3_nt4_deferred_drain.md) and, in round 5, the
+// deferred activation epilogue that ran the GELU / GELU′ pass one element
+// stage per MFMA slot under the next tile's k-loop: fc1 + GELU 565 vs 496 µs,
+// fc2 dX ⊙ GELU′ 730 vs 552 µs (r5_deferred_activation_epilogue.md).
 #include <type_traits>
 #include <utility>
 
@@ -82,24 +74,13 @@ constexpr int OPB = 256 * BK * 2;  // bytes of one operand tile [256][64] bf16 =
 // MIR: runs of 8 MFMAs share the SrcA operand (A fragment i, as hipBLASLt's
 //      loop does) and the operands trade places in the read / release / refill
 //      order; otherwise runs share the B fragment.
-// DEF: deferred activation epilogue (EPI 2 / 3, nk == 16; header comment).
-template <int EPI>
-struct DefCfg {
-  static constexpr int NOP = EPI == 3 ? 2 : 1;          // reloaded operands per chunk: raw (+ pre-activation)
-  static constexpr int STG = 4 * 2 * 2 * NOP * 1024;    // bytes: 4 waves × 2 parities × 2 chunks × NOP × 1 KiB
-};
-
-template <int EPI, bool MIR, bool DEF>
+template <int EPI, bool MIR>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
                                                            const bf16* __restrict__ bias, bf16* __restrict__ Y,
                                                            int ldy, float* __restrict__ dbias_part, int group_m) {
-  static_assert(!DEF || EPI == 2 || EPI == 3, "DEF: activation epilogues only");
-  constexpr int STG = DEF ? DefCfg<EPI>::STG : 0;
-  // [buf][A|B][256][64] operand tiles, then (DEF) the staging ring
-  // [wave][parity][operand][chunk][64 lanes × 16 B]; one __shared__ array
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * 256 * BK + STG / 2];
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * 256 * BK];  // [buf][A|B][256][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -236,19 +217,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const int g4 = lane >> 4;
     const int nb = n0 + wn * 128 + 8 * (lane & 15);
     const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
-    // EPI 4 / 5 / 6 (and 3 without DEF): the addend / GELU pre-activation, all
-    // 32 rows up front; EPI 3 with DEF (a CU's last tile): 4 rows ahead, which
-    // keeps the kernel inside the register file beside the DEF state
-    constexpr bool PRE_ALL = EPI >= 4 || (EPI == 3 && !DEF);
-    bf16x8 pre[PRE_ALL ? 32 : EPI == 3 ? 8 : 1];
+    bf16x8 pre[EPI >= 3 ? 32 : 1];  // EPI 3: the GELU pre-activation; EPI 4 / 5 / 6: the addend
     unsigned char mk[EPI == 6 ? 32 : 1];  // EPI 6: the addend's keep bits (8 columns per byte)
-    if constexpr (PRE_ALL) {
+    if constexpr (EPI >= 3) {
 #pragma unroll
       for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
-    }
-    if constexpr (EPI == 3 && !PRE_ALL) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + u) * ldy + nb);
     }
     if constexpr (EPI == 6) {
       const unsigned char* mask = reinterpret_cast<const unsigned char*>(bias);
@@ -265,13 +238,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       f32x4 a[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) a[j] = rd_acc(acc[i][j]);
-      if constexpr (EPI == 3 && !PRE_ALL) {  // the next 4 rows' pre-activations in flight under this group
-        if (i + 1 < 8) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            pre[4 * ((i + 1) & 1) + u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (i + 1) + u) * ldy + nb);
-        }
-      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const f32x8 v = {a[0][e], a[1][e], a[2][e], a[3][e], a[4][e], a[5][e], a[6][e], a[7][e]};
@@ -306,7 +272,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           for (int q = 0; q < 8; ++q) r[q] = (bits >> q) & 1u ? r[q] : 0.f;
           st16(crow, to_bf16(v + r));
         } else {
-          const f32x8 x = to_f32(pre[PRE_ALL ? 4 * i + e : 4 * (i & 1) + e]) + bv8;
+          const f32x8 x = to_f32(pre[4 * i + e]) + bv8;
           const f32x8& dy = v;  // the fp32 product, not its bf16 rounding
           f32x8 d;
 #pragma unroll
@@ -361,188 +327,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     for (int p = 0; p < 16; ++p) dma(s1, B1{}, p);
   };
 
-  // ---- DEF: the deferred activation pass --------------------------------
-  // The tile whose activation pass runs under the current k-loop ("deferred
-  // tile"): chunk c = 4i + e of a wave is rows 16i + e + 4(l >> 4) of its
-  // 128-row block, 8 columns 8(l & 15) per lane — the row epilogue's layout.
-  // K-tile t handles chunk pair t (c = 2t, 2t + 1); its operands were LDS-DMAed
-  // in k-tile t - 2, after that k-tile's third barrier (pairs 0 and 1: the
-  // epilogue writes the raw product into the staging LDS itself and DMAs EPI 3's
-  // pre-activation).  Staging per wave: [parity][op][chunk] KiB, parity = pair & 1.
-  constexpr int NOP = DefCfg<EPI>::NOP;
-  int d_m0 = 0, d_n0 = 0, d_tm = 0;  // wave-uniform
-  f32x8 dbv = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // its bias (this lane's 8 columns)
-  f32x8 dcol = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // EPI 3: its bias-gradient column partials
-  const unsigned dvC = (unsigned)((((lane >> 4) * 4) * ldc + 8 * (lane & 15)) * 2);
-  const unsigned dvY = (unsigned)((((lane >> 4) * 4) * ldy + 8 * (lane & 15)) * 2);
-  const unsigned stg = lds0 - (unsigned)(w * 1024) + (unsigned)(2 * 2 * OPB) + (unsigned)(w * (STG / 4));
-  const int stg_rd = 2 * 2 * OPB + w * (STG / 4) + 16 * lane;  // this lane's 16 B of a staged chunk (bytes)
-  auto drow = [&](int c) -> size_t { return (size_t)(d_m0 + wm * 128 + 16 * (c >> 2) + (c & 3)); };
-  // the DMA base must live in SGPRs: make its uniformity explicit to hipcc
-  auto uni = [](const bf16* p) -> const bf16* {
-    const uint64_t u = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-    return reinterpret_cast<const bf16*>(((uint64_t)hi << 32) | lo);
-  };
-  // LDS-DMA of chunk pair `pair` (raw product from C; EPI 3: pre-activation from Y) into parity PAR
-  auto ddma = [&](int pair, auto par_tag, auto raw_tag) {
-    constexpr int PAR = decltype(par_tag)::value;
-    constexpr bool RAW = decltype(raw_tag)::value;
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch) {
-      const size_t r = drow(2 * pair + ch);
-      if constexpr (RAW)
-        glds(dvC, uni(C + r * ldc + d_n0 + wn * 128),
-             __builtin_amdgcn_readfirstlane(stg + (unsigned)(((PAR * NOP + 0) * 2 + ch) * 1024)));
-      if constexpr (EPI == 3)
-        glds(dvY, uni(Y + r * ldy + d_n0 + wn * 128),
-             __builtin_amdgcn_readfirstlane(stg + (unsigned)(((PAR * NOP + NOP - 1) * 2 + ch) * 1024)));
-    }
-  };
-  auto dld = [&](int PAR, int op, int ch) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(lds + stg_rd + ((PAR * NOP + op) * 2 + ch) * 1024);
-  };
-  // element pipeline (element k of a chunk = column 8(l & 15) + k): the chunk's
-  // 8 elements in two groups of 4, one stage per MFMA slot, a group's stages 4
-  // slots apart; chunk 1 reuses chunk 0's registers once chunk 0 is packed
-  float dx[8], dt[8], de[8];
-  bf16x8 draw[2], dpre[2], dres[2];
-  // each stage ends in an empty asm that takes its results as operands: the
-  // stage then stays in its slot (hipcc otherwise sinks a whole element's chain
-  // into the slot of its last use and SLP-packs neighbours into v_pk_* ops)
-  auto pin = [](float& v) { asm volatile("" : "+v"(v)); };
-  auto dstage = [&](auto ch_tag, auto k_tag, auto j_tag) {
-    constexpr int CH = decltype(ch_tag)::value, K = decltype(k_tag)::value, J = decltype(j_tag)::value;
-    if constexpr (EPI == 2) {  // y = gelu(raw + bias)
-      if constexpr (J == 0) {
-        dx[K] = (float)draw[CH][K] + dbv[K];
-        pin(dx[K]);
-        de[K] = dx[K] * dx[K];
-        pin(de[K]);
-      } else if constexpr (J == 1) {
-        de[K] = dx[K] * __builtin_fmaf(de[K], -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);
-        pin(de[K]);
-      } else if constexpr (J == 2) {
-        de[K] = __builtin_amdgcn_exp2f(de[K]);
-        pin(de[K]);
-      } else if constexpr (J == 3) {
-        de[K] = __builtin_amdgcn_rcpf(de[K] + 1.f);
-        pin(de[K]);
-      } else if constexpr (J == 4) {
-        dt[K] = dx[K] * de[K];
-        pin(dt[K]);
-      }
-    } else {  // d = raw · gelu'(pre + bias), column partials
-      if constexpr (J == 0) {
-        dx[K] = (float)dpre[CH][K] + dbv[K];
-        pin(dx[K]);
-        dt[K] = dx[K] * dx[K];
-        pin(dt[K]);
-      } else if constexpr (J == 1) {
-        de[K] = dx[K] * __builtin_fmaf(dt[K], -2.f * GK0 * GK1 * GL2E, -2.f * GK0 * GL2E);
-        pin(de[K]);
-        dt[K] = __builtin_fmaf(dt[K], 6.f * GK0 * GK1, 2.f * GK0);  // 2u'
-        pin(dt[K]);
-      } else if constexpr (J == 2) {
-        de[K] = __builtin_amdgcn_exp2f(de[K]);
-        pin(de[K]);
-      } else if constexpr (J == 3) {
-        de[K] = __builtin_amdgcn_rcpf(de[K] + 1.f);  // s
-        pin(de[K]);
-      } else if constexpr (J == 4) {
-        dt[K] = __builtin_fmaf(-dx[K], de[K], dx[K]) * dt[K];  // x(1 - s)·2u'
-        pin(dt[K]);
-      } else if constexpr (J == 5) {
-        const float d = (float)draw[CH][K] * __builtin_fmaf(de[K], dt[K], de[K]);
-        float c = dcol[K] + d;
-        pin(c);
-        dcol[K] = c;
-        dt[K] = d;
-        pin(dt[K]);
-      }
-    }
-  };
-  constexpr int NSTAGE = EPI == 3 ? 6 : 5;
-  constexpr int GSPAN = 4 * NSTAGE + 2;                 // slots per group of 4 elements (+2 gap)
-  constexpr int DBASE = 4;                              // first slot of group 0
-  constexpr int DPACK0 = DBASE + 2 * GSPAN - 2, DPACK1 = DBASE + 4 * GSPAN - 2;  // chunk packs
-  constexpr int DLD1 = DBASE + 2 * GSPAN - 1;           // chunk 1's LDS reads
-  constexpr int DST0 = 96, DST1 = DPACK1 + 2 > 98 ? DPACK1 + 2 : 98;  // stores (after barrier 3's wait)
-  static_assert(!DEF || (DPACK0 < 93 && DLD1 < 93 && DST1 + 2 < 126), "DEF slot plan");
-  // the deferred work of slot S of k-tile t (BUF = t & 1; FIRST: t = 0, T1: t = 1,
-  // LOAD: t < nk - 2, MORE: t < nk - 1)
-  auto defw = [&](int t, auto s_tag, auto buf_tag, auto first_tag, auto t1_tag, auto load_tag, auto more_tag) {
-    constexpr int S = decltype(s_tag)::value, BUF = decltype(buf_tag)::value;
-    constexpr bool FIRST = decltype(first_tag)::value, T1 = decltype(t1_tag)::value;
-    constexpr bool LOAD = decltype(load_tag)::value, MORE = decltype(more_tag)::value;
-    // pair t+2 into this pair's parity (its LDS reads are retired by then), after
-    // barrier 3: the mainloop's DMA bases are dead there (SGPR budget)
-    if constexpr (S == 95 && LOAD) ddma(t + 2, std::integral_constant<int, BUF>{}, std::true_type{});
-    // chunk CH's operands: raw product and EPI 3's pre-activation
-    auto ld = [&](auto ch_tag) {
-      constexpr int CH = decltype(ch_tag)::value;
-      draw[CH] = dld(BUF, 0, CH);
-      if constexpr (EPI == 3) dpre[CH] = dld(BUF, 1, CH);
-    };
-    if constexpr (S == 2) ld(std::integral_constant<int, 0>{});
-    if constexpr (S == DLD1) ld(std::integral_constant<int, 1>{});
-    constexpr int L = S - DBASE;
-    if constexpr (L >= 0 && L < 4 * GSPAN) {
-      constexpr int G = L / GSPAN, R = L % GSPAN;  // group G (chunk G >> 1, elements 4(G & 1) ..+3)
-      if constexpr (R < 4 * NSTAGE)
-        dstage(std::integral_constant<int, (G >> 1)>{}, std::integral_constant<int, 4 * (G & 1) + (R & 3)>{},
-               std::integral_constant<int, (R >> 2)>{});
-    }
-    if constexpr (S == DPACK0 || S == DPACK1) {  // the chunk's 8 results
-      dres[S == DPACK0 ? 0 : 1] = to_bf16(f32x8{dt[0], dt[1], dt[2], dt[3], dt[4], dt[5], dt[6], dt[7]});
-    }
-    if constexpr (S == DST0 || S == DST1) {
-      constexpr int SC = S == DST0 ? 0 : 1;
-      const size_t r = drow(2 * t + SC) + 4 * (lane >> 4);
-      const int col = d_n0 + wn * 128 + 8 * (lane & 15);
-      if constexpr (EPI == 2) st16(Y + r * ldy + col, dres[SC]);
-      else st16(C + r * ldc + col, dres[SC]);
-    }
-    if constexpr (EPI == 3 && !MORE && S == DST1 + 2) {
-      // the deferred tile's bias-gradient partial row 4·wm + (l >> 4) of its M-tile's 8
-      float* prow = dbias_part + (size_t)(8 * d_tm + 4 * wm + (lane >> 4)) * N + d_n0 + wn * 128 + 8 * (lane & 15);
-      *reinterpret_cast<f32x4*>(prow) = f32x4{dcol[0], dcol[1], dcol[2], dcol[3]};
-      *reinterpret_cast<f32x4*>(prow + 4) = f32x4{dcol[4], dcol[5], dcol[6], dcol[7]};
-    }
-  };
-  // DEF row epilogue: the raw product only; the tile becomes the deferred tile
-  auto def_epilogue = [&]() {
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    const int g4 = lane >> 4;
-    const int nb = n0 + wn * 128 + 8 * (lane & 15);
-    const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
-    d_m0 = m0;
-    d_n0 = n0;
-    d_tm = tm;
-    // kept in VGPRs (the mainloop's DMA bases need every SGPR; uni() brings the
-    // deferred tile's bases back to SGPRs where a DMA needs them)
-    asm volatile("" : "+v"(d_m0), "+v"(d_n0), "+v"(d_tm));
-    if constexpr (EPI == 3) {  // pairs 0 and 1's pre-activation (input data)
-      ddma(0, B0{}, std::false_type{});
-      ddma(1, B1{}, std::false_type{});
-    }
-    dbv = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
-    dcol = f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      f32x4 a[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = rd_acc(acc[i][j]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bf16x8 raw = to_bf16(f32x8{a[0][e], a[1][e], a[2][e], a[3][e], a[4][e], a[5][e], a[6][e], a[7][e]});
-        st16(C + (mr + 16 * i + e) * ldc + nb, raw);
-        if (i == 0)  // chunk e = pair e >> 1: staged by hand (a DMA could race this wave's own store)
-          *reinterpret_cast<bf16x8*>(const_cast<unsigned char*>(lds) + stg_rd + (((e >> 1) * NOP) * 2 + (e & 1)) * 1024) = raw;
-      }
-    }
-  };
-
   // slot s = MFMA index in the tile (128); run r = s >> 3 keeps B fragment
   // (r & 7) stationary over A fragments 0-7 (MIR: A stationary), k half s >> 6.
   //   s  0-14 (even)  F1 A reads           s 23        lgkmcnt(0), barrier 1
@@ -550,17 +334,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   //   s 51            lgkmcnt(0), barrier 2
   //   s 52-87 (÷5)    B pieces of t+2      s 93        vmcnt(t+2 pieces), barrier 3
   //   s 94-124 (even) F0 reads of t+1 (other buffer)
-  // DEFW (a deferred tile exists): s 2-3 this pair's LDS reads, s 4-103 one
-  // element stage per slot, s 95 the DMA of chunk pair t+2 and s 96 and 98 / 106
-  // the two result stores (all younger than barrier 3's wait, so its count is
-  // unchanged; the next k-tile's barrier-3 wait retires the DMA)
-  auto tile3 = [&](int t, auto buf_tag, auto first_tag, auto more_tag, auto load_tag, auto defw_tag,
-                   auto t1_tag) {
+  auto tile3 = [&](int t, auto buf_tag, auto first_tag, auto more_tag, auto load_tag) {
     constexpr int BUF = decltype(buf_tag)::value;
     constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
     constexpr bool LOAD = decltype(load_tag)::value;
-    constexpr bool DEFW = decltype(defw_tag)::value;
     using NB = std::integral_constant<int, BUF ^ 1>;
     using SB = std::integral_constant<int, BUF>;
     Src sn2{};
@@ -574,7 +352,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       } else {
         mma(acc[i][j], fa1[i], fb1[j]);
       }
-      if constexpr (DEFW) defw(t, sc, buf_tag, first_tag, t1_tag, load_tag, more_tag);
       // MIR swaps the operands' roles below: B's k 32-63 fragments first, B's
       // half of the buffer released at barrier 1 and refilled first, A's at barrier 2
       if constexpr (s < 16 && (s & 1) == 0) {
@@ -598,10 +375,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       }
       if constexpr (LOAD && s >= 52 && s < 92 && (s - 52) % 5 == 0) dma(sn2, SB{}, (MIR ? 0 : 8) + (s - 52) / 5);
       if constexpr (MORE && s == 93) {
-        // this wave's tile t+1 pieces (and DEFW: its chunk pair t+1) retired; its
-        // 16 tile t+2 pieces may stay in flight
-        if constexpr (LOAD) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in flight)
+        if constexpr (LOAD) {
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
       }
@@ -611,25 +390,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  // the k-loop of one output tile (DEFW: with the deferred tile's activation pass)
-  auto ktiles = [&](auto defw_tag) {
-    tile3(0, B0{}, T_{}, T_{}, T_{}, defw_tag, F_{});
-    tile3(1, B1{}, F_{}, T_{}, T_{}, defw_tag, T_{});
-    for (int t = 2; t < nk - 2; t += 2) {
-      tile3(t, B0{}, F_{}, T_{}, T_{}, defw_tag, F_{});
-      tile3(t + 1, B1{}, F_{}, T_{}, T_{}, defw_tag, F_{});
-    }
-    tile3(nk - 2, B0{}, F_{}, T_{}, F_{}, defw_tag, F_{});
-    tile3(nk - 1, B1{}, F_{}, F_{}, F_{}, defw_tag, F_{});
-  };
-  // DEF: a CU's first k-loop has no deferred tile; it runs the activation
-  // pass anyway, on its own tile's region (d_* = this tile) — the garbage it
-  // stores there is overwritten later by the same wave (its raw epilogue, its
-  // own deferred pass, or the immediate epilogue of a single-tile CU): one
-  // k-loop instance instead of two (two cost ≈ 50 VGPRs and spilled)
-  d_m0 = m0;
-  d_n0 = n0;
-  d_tm = tm;
   issue01();
   for (;;) {
     // tile 0 landed (tile 1 may fly)
@@ -640,7 +400,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 #pragma unroll
     for (int q = 0; q < 16; ++q) rdF0(B0{}, q);
     // nk is even and ≥ 4 (host contract): pairs of tiles keep the buffer index static
-    ktiles(std::integral_constant<bool, DEF>{});
+    tile3(0, B0{}, T_{}, T_{}, T_{});
+    tile3(1, B1{}, F_{}, T_{}, T_{});
+    for (int t = 2; t < nk - 2; t += 2) {
+      tile3(t, B0{}, F_{}, T_{}, T_{});
+      tile3(t + 1, B1{}, F_{}, T_{}, T_{});
+    }
+    tile3(nk - 2, B0{}, F_{}, T_{}, F_{});
+    tile3(nk - 1, B1{}, F_{}, F_{}, F_{});
     const int vn = vcur + (int)gridDim.x;
     if (vn >= nwg) break;
     int ntm, ntn;
@@ -654,11 +421,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     baseB = B + ((size_t)ntn * BN + 64 * (w & 1) + (w >> 1)) * ldb;
     dhalfn = ntn * BN + BN > N;
     issue01();
-    if constexpr (DEF) {
-      def_epilogue();  // of this tile: the raw product; its activation pass runs under the next k-loop
-    } else {
-      row_epilogue();  // of this tile (m0, n0, tm, halfn)
-    }
+    row_epilogue();  // of this tile (m0, n0, tm, halfn)
     vcur = vn;
     tm = ntm;
     tn = ntn;
@@ -666,7 +429,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     n0 = tn * BN;
     halfn = dhalfn;
   }
-  row_epilogue();  // a CU's last tile: immediate
+  row_epilogue();
 }
 
 }  // namespace
@@ -682,13 +445,10 @@ static int persistent_grid(long long tiles) {
   return (int)(tiles < ncu ? tiles : ncu);
 }
 
-// variant 0 = the production schedule (B-stationary runs for K ≤ 1024,
-// mirrored above: tools/nt4_probe.py, profiles/r3_gemm_nt4_rows.md) with the
-// deferred activation epilogue where it applies (EPI 2 / 3, nk = 16, whole
-// 256-column tiles); variant 1 = the same with every epilogue immediate (the
-// A/B alternative)
+// B-stationary runs for K ≤ 1024, mirrored above (tools/nt4_probe.py,
+// profiles/r3_gemm_nt4_rows.md)
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
-             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant) {
+             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
   if (N % BN && N % BN != BN / 2) return -2;
   const long long tiles = (long long)(M / BM) * ((N + BN - 1) / BN);
   if (tiles > 0x7fffffffLL) return -2;
@@ -698,27 +458,24 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   // NT shapes (row-major = 1: wide K = 1024 GEMM 501 -> 451 us, fc2 dX ⊙ GELU' 642 -> 607, qkv 433 -> 419)
   constexpr int group_m = 8;
   const int g = persistent_grid(tiles);
-  const bool mir = K > 1024;
-  const bool def = variant == 0 && (epi == 2 || epi == 3) && nk == 16 && N % BN == 0 && !mir;
   auto go = [&](auto kern) {
     kern<<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m);
     return 0;
   };
-  if (def) return epi == 2 ? go(gemm_nt4_kernel<2, false, true>) : go(gemm_nt4_kernel<3, false, true>);
   auto launch = [&](auto mir_tag) -> int {
     constexpr bool MI = decltype(mir_tag)::value;
     switch (epi) {
-      case 0: return go(gemm_nt4_kernel<0, MI, false>);
-      case 1: return go(gemm_nt4_kernel<1, MI, false>);
-      case 2: return go(gemm_nt4_kernel<2, MI, false>);
-      case 3: return go(gemm_nt4_kernel<3, MI, false>);
-      case 4: return go(gemm_nt4_kernel<4, MI, false>);
-      case 5: return go(gemm_nt4_kernel<5, MI, false>);
-      case 6: return go(gemm_nt4_kernel<6, MI, false>);
+      case 0: return go(gemm_nt4_kernel<0, MI>);
+      case 1: return go(gemm_nt4_kernel<1, MI>);
+      case 2: return go(gemm_nt4_kernel<2, MI>);
+      case 3: return go(gemm_nt4_kernel<3, MI>);
+      case 4: return go(gemm_nt4_kernel<4, MI>);
+      case 5: return go(gemm_nt4_kernel<5, MI>);
+      case 6: return go(gemm_nt4_kernel<6, MI>);
       default: return -4;
     }
   };
-  return mir ? launch(std::true_type{}) : launch(std::false_type{});
+  return K > 1024 ? launch(std::true_type{}) : launch(std::false_type{});
 }
 
 }  // namespace pdo

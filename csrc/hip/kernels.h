@@ -153,10 +153,10 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);
 // gemm_nt4.hip: the same contract on the 4-wave / 128 × 128-per-wave mainloop
 int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
-             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st, int variant = 0);
-// (N % 256 = 128 allowed: half-width last tile column; variant 1 = deferred store drain)
+             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);
+// (N % 256 = 128 allowed: half-width last tile column)
 // which mainloop gemm_nt() runs: 0 = 8-wave ring (gemm_nt.hip), 1 = 4-wave
-// (gemm_nt4.hip, default), 2 = 4-wave with the deferred store drain
+// (gemm_nt4.hip, default)
 void gemm_nt_set_impl(int impl);
 int gemm_nt_get_impl();
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);

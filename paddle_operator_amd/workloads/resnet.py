@@ -1,21 +1,16 @@
 """ResNet-50 data-parallel training step (collective mode).
 
-MIOpen convolution choice: the default (dynamic hybrid) find mode benchmarks
-every convolution config on first use — 65 s before the first step on MI355X
-at batch 256 — and FAST mode without a find-db hit falls back to immediate-mode
-kernels that run ~25× slower (213 vs 5954 img/s, tools/bench_resnet.py).  So
+Every convolution runs on the hand-written kernels (``ops.resnet``); MIOpen
+serves only the framework reference path (``PDO_OPS=torch``).  For that path
 the find results measured once on an MI355X ship in
-``paddle_operator_amd/tuning/miopen`` and every rank starts from a copy of
-them (utils.tuning.use_shipped_miopen_db): normal find mode, no benchmarking
-for the shipped shapes.
+``paddle_operator_amd/tuning/miopen`` and are installed when the trainer is
+built in torch mode (utils.tuning.use_shipped_miopen_db): the default find
+mode would otherwise benchmark every convolution config on first use (65 s
+before the first step at batch 256).
 """
 from __future__ import annotations
 
 import os
-
-from ..utils.tuning import use_shipped_miopen_db
-
-use_shipped_miopen_db()
 
 import torch
 import torch.distributed as dist
@@ -62,6 +57,10 @@ class FlatSGD:
 
 class ResNetTrainer:
     def __init__(self, batch: int, device, tiny: bool = False, bucket_mb: int = 25, channels_last: bool = True):
+        from .. import _native
+        if _native.ops_mode() == "torch":  # the framework reference path: MIOpen convolutions
+            from ..utils.tuning import use_shipped_miopen_db
+            use_shipped_miopen_db()
         self.device = torch.device(device)
         self.B = batch
         self.tiny = tiny

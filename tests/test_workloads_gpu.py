@@ -85,3 +85,72 @@ def test_resnet_arena_grads_match_autograd(cuda, deterministic_convs):
         err = (pa.grad.float() - pb.grad.float()).norm() / (pb.grad.float().norm() + 1e-12)
         assert err < 2e-3, f"{n}: {err}"
 
+
+
+def _resnet_fwd(m, x):
+    """ResNet forward with the stem output's gradient retained (the network
+    input of the HIP stem needs none: compare the gradient entering layer1)."""
+    from paddle_operator_amd import ops
+    h = ops.conv_bn_relu_maxpool(m.conv1, m.bn1, x)
+    h.retain_grad()
+    y = m.layer4(m.layer3(m.layer2(m.layer1(h))))
+    return m.fc(torch.flatten(torch.nn.functional.adaptive_avg_pool2d(y, 1), 1)), h
+
+
+@pytest.mark.gpu
+def test_resnet50_width_hip_vs_fp32(cuda):
+    """Full-width ResNet-50 (64 … 2048 channels, every stage and block type) on
+    the production HIP path — fp32 master arena, bf16 shadow weights + autocast,
+    the space-to-depth stem with fused BN + ReLU + max-pool, implicit-GEMM and
+    token-major convolutions, BatchNorm statistics from conv epilogues, the
+    residual ReLU mask in conv1's dX epilogue, the compact stride-2 input
+    gradient — against the SAME weights in fp32 on the framework ops (CPU):
+    loss, logits, the gradient entering layer1, every parameter gradient and the
+    BatchNorm running statistics.  Batch 16 at 128 × 128: every stage's token
+    count is a multiple of 256, so the token-major GEMM paths run too; BN γ / β
+    re-drawn so no branch is zeroed (bn3's zero-init would hide its gradients)."""
+    import copy
+
+    from paddle_operator_amd.models.resnet import resnet50
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    ref = resnet50()
+    for m in ref.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+            torch.nn.init.uniform_(m.bias, -0.1, 0.1)
+    hip = copy.deepcopy(ref).to(cuda).to(memory_format=torch.channels_last)
+    flat = FlatParams(hip, dtype=torch.float32, device=cuda, bucket_bytes=25 << 20)
+    flat.enable_shadow(torch.bfloat16)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(16, 3, 128, 128, generator=g)
+    y = torch.randint(0, 1000, (16,), generator=g)
+
+    flat.zero_grad()
+    xh = x.to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with flat.shadow_scope(), torch.autocast("cuda", dtype=torch.bfloat16):
+        logits_h, h_h = _resnet_fwd(hip, xh)
+    loss_h = torch.nn.functional.cross_entropy(logits_h.float(), y.to(cuda))
+    loss_h.backward()
+    torch.cuda.synchronize()
+
+    logits_r, h_r = _resnet_fwd(ref, x)  # CPU: the framework ops in fp32
+    loss_r = torch.nn.functional.cross_entropy(logits_r, y)
+    loss_r.backward()
+
+    def rel(a, b):
+        a, b = a.detach().float().cpu(), b.detach().float().cpu()
+        return float((a - b).norm() / (b.norm() + 1e-12))
+
+    assert abs(loss_h.item() - loss_r.item()) < 2e-2 * abs(loss_r.item()), (loss_h.item(), loss_r.item())
+    assert rel(logits_h, logits_r) < 5e-2
+    assert rel(h_h.grad, h_r.grad) < 6e-2
+    rp = dict(ref.named_parameters())
+    errs = {n: rel(p.grad, rp[n].grad) for n, p in hip.named_parameters()}
+    bad = {n: e for n, e in errs.items() if not e < 6e-2}
+    assert not bad, bad
+    rb = dict(ref.named_buffers())
+    stats = {n: rel(b, rb[n]) for n, b in hip.named_buffers() if "running" in n}
+    bad = {n: e for n, e in stats.items() if not e < 2e-2}
+    assert not bad, bad
