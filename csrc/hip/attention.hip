@@ -446,6 +446,171 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   attn_fwd_body(qkv, out, lse, B, S, H, c2, order);
 }
 
+// ----- forward, 64 query rows per wave -----
+// A workgroup = 4 waves = 256 queries of one (b, h); wave w owns two 32-row
+// sub-blocks, rows 32w + li (u = 0) and 128 + 32w + li (u = 1) of the block,
+// so every wave needs the same key tiles to within one (causal balance).  Each
+// K row fragment and V transposed fragment read from LDS feeds the MFMAs of
+// both sub-blocks, every staged K/V tile serves 256 queries instead of 128, and
+// the two sub-blocks' softmax chains interleave in one wave (ILP).  The score
+// MFMAs start from 0 and the row maximum is subtracted in the exponent (packed
+// fp32 subtract): no −m broadcast accumulators, which keeps the kernel at
+// 2 waves per SIMD.
+__device__ __forceinline__ void attn_fwd64_body(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                float* __restrict__ lse, int B, int S, int H, float c2, int order) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int nqb = S / 256;
+  int bh, r_;
+  attn_block(order, nqb, B * H, bh, r_);
+  const int qb = nqb - 1 - r_;  // heaviest query blocks first
+  const int b = bh / H, h = bh % H;
+  const size_t rs = (size_t)3 * H * HD;
+  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
+  const bf16* kbase = qbase + (size_t)H * HD;
+  const bf16* vbase = qbase + (size_t)2 * H * HD;
+
+  int q[2], qmin[2];
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    qmin[u] = qb * 256 + 128 * u + 32 * w;
+    q[u] = qmin[u] + li;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      qf[u][ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q[u] * rs + 16 * ks + 8 * hh);
+  }
+  retire(qf[0]);
+  retire(qf[1]);
+  prescale(qf[0], c2);
+  prescale(qf[1], c2);
+
+  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
+  f32x16 o[2][2] = {{zero16(), zero16()}, {zero16(), zero16()}};
+  float m[2] = {0.f, 0.f}, l[2] = {0.f, 0.f};
+  const int ntiles = (qb * 256 + 256) / TROWS;
+
+  Stage sk, sv;
+  stage_load(sk, kbase, rs, 0, tid);
+  stage_load(sv, vbase, rs, 0, tid);
+  stage_store(sk, smem, tid);
+  stage_store_v(sv, smem + TROWS * HD, tid);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
+    const bf16* Vt = Kt + TROWS * HD;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+    }
+    const int key0 = t * TROWS;
+    const bool act0 = key0 <= qmin[0] + 31;  // sub-block 0 still has keys (wave-uniform); u = 1 always
+    f32x16 sc[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 k0 = row_frag(Kt, 0, ks, lane), k1 = row_frag(Kt, 32, ks, lane);
+      if (ks == 0) {
+        sc[1][0] = mfma(k0, qf[1][0], zero16());
+        sc[1][1] = mfma(k1, qf[1][0], zero16());
+        if (act0) {
+          sc[0][0] = mfma(k0, qf[0][0], zero16());
+          sc[0][1] = mfma(k1, qf[0][0], zero16());
+        }
+      } else {
+        sc[1][0] = mfma(k0, qf[1][ks], sc[1][0]);
+        sc[1][1] = mfma(k1, qf[1][ks], sc[1][1]);
+        if (act0) {
+          sc[0][0] = mfma(k0, qf[0][ks], sc[0][0]);
+          sc[0][1] = mfma(k1, qf[0][ks], sc[0][1]);
+        }
+      }
+    }
+    // softmax of sub-block u: mask its diagonal tile, defer-max (T13), exponentiate, row sums
+    auto softmax = [&](int u) {
+      f32x16& s0 = sc[u][0];
+      f32x16& s1 = sc[u][1];
+      if (key0 + TROWS - 1 > qmin[u]) {  // diagonal tile (wave-uniform)
+        const int d = q[u] - key0 - 4 * hh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = (r & 3) + 8 * (r >> 2);
+          s0[r] = c > d ? -INFINITY : s0[r];
+          s1[r] = c + 32 > d ? -INFINITY : s1[r];
+        }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+      tmax = xhalf_max(tmax);
+      if (t == 0) {  // key 0 is unmasked for every query: finite
+        m[u] = tmax;
+      } else if (__any(tmax - m[u] > 8.f)) {
+        const float d = tmax - m[u] > 8.f ? tmax - m[u] : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        m[u] += d;
+        l[u] *= alpha;
+        o[u][0] *= alpha;
+        o[u][1] *= alpha;
+      }
+      const f32x2 nm = {-m[u], -m[u]};
+      f32x2 ls2 = {0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 a0 = f32x2{s0[r], s0[r + 1]} + nm, a1 = f32x2{s1[r], s1[r + 1]} + nm;
+        s0[r] = __builtin_amdgcn_exp2f(a0[0]);
+        s0[r + 1] = __builtin_amdgcn_exp2f(a0[1]);
+        s1[r] = __builtin_amdgcn_exp2f(a1[0]);
+        s1[r + 1] = __builtin_amdgcn_exp2f(a1[1]);
+        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+      }
+      l[u] += ls2[0] + ls2[1];
+    };
+    softmax(1);
+    if (act0) softmax(0);
+    const bf16* V0 = Vt + vb0;
+    const bf16* V1 = Vt + vb1;
+    auto pv = [&](auto k_tag, int sst, int half) {
+      constexpr int K0 = decltype(k_tag)::value;
+      const bf16x8 va = tr_frag_v<K0>(V0), vbv = tr_frag_v<K0>(V1);
+      const bf16x8 p1 = pack8(sc[1][half], sst);
+      o[1][0] = mfma(va, p1, o[1][0]);
+      o[1][1] = mfma(vbv, p1, o[1][1]);
+      if (act0) {
+        const bf16x8 p0 = pack8(sc[0][half], sst);
+        o[0][0] = mfma(va, p0, o[0][0]);
+        o[0][1] = mfma(vbv, p0, o[0][1]);
+      }
+    };
+    pv(std::integral_constant<int, 0>{}, 0, 0);
+    pv(std::integral_constant<int, 32>{}, 0, 1);
+    pv(std::integral_constant<int, 16>{}, 1, 0);
+    pv(std::integral_constant<int, 48>{}, 1, 1);
+    if (more) {
+      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
+      stage_store(sk, Kn, tid);
+      stage_store_v(sv, Kn + TROWS * HD, tid);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const float lt = xhalf_sum(l[u]);
+    const float inv = 1.f / lt;
+    bf16* orow = out + ((size_t)(b * S + q[u]) * H + h) * HD;
+    store_acc_rows(orow, o[u][0], 0, hh, inv);
+    store_acc_rows(orow, o[u][1], 32, hh, inv);
+    if (hh == 0) lse[(size_t)bh * S + q[u]] = (m[u] + log2f(lt)) * LN2;
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd64_d64(
+    const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int S, int H, float c2,
+    int order) {
+  attn_fwd64_body(qkv, out, lse, B, S, H, c2, order);
+}
+
 // ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
@@ -748,7 +913,9 @@ static int attn_order() {
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
   static const int fwd3 = env_int("PDO_ATTN_FWD3", 1);
-  if (fwd3)
+  if (fwd3 == 2 && S % 256 == 0)
+    attn_fwd64_d64<<<B * H * (S / 256), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  else if (fwd3)
     attn_fwd3_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
   else
     attn_fwd_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());

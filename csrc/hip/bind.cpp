@@ -319,8 +319,9 @@ at::Tensor embed_bwd_sorted(at::Tensor dy, at::Tensor keys, at::Tensor perm, at:
   const int B = dy.size(0), S = dy.size(1), C = dy.size(2);
   TORCH_CHECK(S <= P && dwte.dim() == 2 && dwte.size(1) == C);
   auto dwpe = at::empty({P, C}, dy.options());
-  CHECK_RC(pdo::embed_bwd_sorted(bp(dy), keys.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), bp(dwte), bp(dwpe), B,
-                                 S, C, (int)dwte.size(0), (int)P, 1, cur_stream()), "embed_bwd_sorted");
+  auto part = at::empty({pdo::embed_sorted_part_floats(B * S, C)}, dy.options().dtype(at::kFloat));
+  CHECK_RC(pdo::embed_bwd_sorted(bp(dy), keys.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), bp(dwte), bp(dwpe),
+                                 fp(part), B, S, C, (int)dwte.size(0), (int)P, 1, cur_stream()), "embed_bwd_sorted");
   return dwpe;
 }
 

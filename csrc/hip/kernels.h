@@ -185,8 +185,10 @@ int xent_bwd(const bf16* logits, const int64_t* tgt, const float* lse, const flo
 int embed_fwd(const int64_t* idx, const bf16* wte, const bf16* wpe, bf16* y, int B, int S, int C, hipStream_t st);
 int embed_bwd(const bf16* dy, const int64_t* idx, float* acc, bf16* dwte, bf16* dwpe, int B, int S, int C, int Vp,
               int P, hipStream_t st);
-int embed_bwd_sorted(const bf16* dy, const int64_t* keys, const int64_t* perm, bf16* dwte, bf16* dwpe, int B, int S,
-                     int C, int Vp, int P, int accumulate, hipStream_t st);
+// part: embed_sorted_part_floats(B·S, C) fp32 scratch (partials of runs that cross segments)
+int embed_sorted_part_floats(int N, int C);
+int embed_bwd_sorted(const bf16* dy, const int64_t* keys, const int64_t* perm, bf16* dwte, bf16* dwpe, float* part,
+                     int B, int S, int C, int Vp, int P, int accumulate, hipStream_t st);
 int sgd_flat(float* w, const float* g, float* buf, const float* decay_chunks, long long n, float lr, float mom,
              float wd, float grad_scale, hipStream_t st);
 int cast_f32_bf16(const float* in, bf16* out, long long n, hipStream_t st);

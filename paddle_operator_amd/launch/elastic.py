@@ -235,6 +235,22 @@ class ElasticAgent:
             return bad[0]
         return 0 if all(rc == 0 for rc in rcs) else None
 
+    def wait_workers(self, timeout: float) -> int:
+        """Wait for the local ranks to finish: the first non-zero exit stops the
+        others and is returned; past ``timeout`` every rank is stopped (rc 124)."""
+        t_end = time.time() + timeout
+        while True:
+            rc = self.poll_workers()
+            if rc is not None:
+                if rc != 0:
+                    self.stop_workers(5.0)
+                return rc
+            if time.time() >= t_end:
+                _log(f"workers still running {timeout:.0f}s after the generation completed: stopping them")
+                self.stop_workers(5.0)
+                return 124
+            time.sleep(self.poll / 2)
+
     def stop_workers(self, grace: float = 20.0):
         live = [p for p in self.procs if p.poll() is None]
         for p in live:
@@ -274,9 +290,10 @@ class ElasticAgent:
                     self.ensure_registered()
                     if self.changed(world):
                         if self.gen_done(world):
-                            # generation completed: let this pod's workers finish too
-                            rcs = [p.wait() for p in self.procs]
-                            rc = next((r for r in rcs if r), 0)
+                            # generation completed: let this pod's workers finish too —
+                            # polled with a deadline: a local rank that fails now must
+                            # not leave its siblings hanging in a collective
+                            rc = self.wait_workers(self.timeout)
                             break
                         _log("membership/np changed → stopping workers for re-rendezvous")
                         self.stop_workers()

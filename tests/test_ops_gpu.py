@@ -373,6 +373,36 @@ def test_embedding_sorted_backward_into_arena(cuda):
     assert torch.equal(slot, slot2)  # deterministic
 
 
+@pytest.mark.parametrize("skew", ["one_token", "runs_across_segments"])
+def test_embedding_sorted_backward_skewed_ids(cuda, skew):
+    """Skewed token ids (a frequent EOS/padding id): runs of equal ids longer
+    than the 256-row segments of the sorted embedding backward are summed in
+    pieces and folded in segment order — against an fp32 index_add reference,
+    deterministic, ids outside the table ignored."""
+    from paddle_operator_amd import _native
+    m = _native.require_hip()
+    B, S, C, Vp, P = 16, 512, 256, 1024, 512
+    g = torch.Generator(device=cuda).manual_seed(21)
+    idx = torch.randint(0, 900, (B, S), device=cuda, generator=g)
+    if skew == "one_token":
+        idx[torch.rand(B, S, device=cuda, generator=g) < 0.7] = 3  # 70 %: ~5700 rows of one id
+    else:
+        idx.view(-1)[:1000] = 11        # runs crossing 3 segment boundaries
+        idx.view(-1)[1000:1300] = 12
+        idx[-1, -20:] = Vp + 5          # outside the table: contributes nothing
+    dy = torch.randn(B, S, C, device=cuda, generator=g).bfloat16()
+    keys, perm = torch.sort(idx.reshape(-1), stable=True)
+    base = torch.randn(Vp, C, device=cuda, generator=g).bfloat16()
+    slot = base.clone()
+    m.embed_bwd_sorted(dy, keys, perm, slot, P)
+    ok = idx.reshape(-1) < Vp
+    ref = torch.zeros(Vp, C, device=cuda).index_add_(0, idx.reshape(-1)[ok], dy.reshape(-1, C)[ok].float())
+    torch.testing.assert_close(slot.float(), base.float() + ref, atol=5e-2, rtol=1e-2)
+    slot2 = base.clone()
+    m.embed_bwd_sorted(dy, keys, perm, slot2, P)
+    assert torch.equal(slot, slot2)
+
+
 def test_sgd_flat_matches_reference(cuda):
     """The fused momentum-SGD pass (ResNet-50's optimizer) equals the bulk-op formula."""
     from paddle_operator_amd import _native

@@ -104,12 +104,20 @@ def test_resnet50_width_hip_vs_fp32(cuda):
     the space-to-depth stem with fused BN + ReLU + max-pool, implicit-GEMM and
     token-major convolutions, BatchNorm statistics from conv epilogues, the
     residual ReLU mask in conv1's dX epilogue, the compact stride-2 input
-    gradient — against the SAME weights in fp32 on the framework ops (CPU):
-    loss, logits, the gradient entering layer1, every parameter gradient and the
-    BatchNorm running statistics.  Batch 16 at 128 × 128: every stage's token
-    count is a multiple of 256, so the token-major GEMM paths run too; BN γ / β
-    re-drawn so no branch is zeroed (bn3's zero-init would hide its gradients)."""
+    gradient — against the SAME weights in fp32 on the framework ops (CPU): loss,
+    logits, the gradient entering layer1, every parameter gradient and the
+    BatchNorm running statistics.
+
+    The bound is bf16's own: the framework ops in bf16 (``PDO_OPS=torch`` +
+    autocast, MIOpen convolutions) run on the same batch, and every HIP error
+    against fp32 must stay within 1.5× the framework-bf16 error (+ 0.03).  BN
+    γ / β gradients carry ≈ 40 % bf16 noise either way at this batch
+    (tools/resnet_anchor_probe.py); a dropped, doubled or mis-masked gradient
+    is O(1) above it.  Batch 16 at 128 × 128: every stage's token count is a
+    multiple of 256, so the token-major GEMM paths run too.  BN γ / β re-drawn
+    (bn3's γ small, not zero: the residual branches carry gradient)."""
     import copy
+    import os
 
     from paddle_operator_amd.models.resnet import resnet50
     from paddle_operator_amd.parallel.flat import FlatParams
@@ -120,21 +128,31 @@ def test_resnet50_width_hip_vs_fp32(cuda):
         if isinstance(m, torch.nn.BatchNorm2d):
             torch.nn.init.uniform_(m.weight, 0.5, 1.5)
             torch.nn.init.uniform_(m.bias, -0.1, 0.1)
+        if hasattr(m, "bn3"):
+            torch.nn.init.uniform_(m.bn3.weight, 0.1, 0.3)
     hip = copy.deepcopy(ref).to(cuda).to(memory_format=torch.channels_last)
+    fw = copy.deepcopy(ref).to(cuda).to(memory_format=torch.channels_last)
     flat = FlatParams(hip, dtype=torch.float32, device=cuda, bucket_bytes=25 << 20)
     flat.enable_shadow(torch.bfloat16)
     g = torch.Generator().manual_seed(3)
     x = torch.randn(16, 3, 128, 128, generator=g)
     y = torch.randint(0, 1000, (16,), generator=g)
+    xh = x.to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     flat.zero_grad()
-    xh = x.to(cuda, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     with flat.shadow_scope(), torch.autocast("cuda", dtype=torch.bfloat16):
         logits_h, h_h = _resnet_fwd(hip, xh)
     loss_h = torch.nn.functional.cross_entropy(logits_h.float(), y.to(cuda))
     loss_h.backward()
+    os.environ["PDO_OPS"] = "torch"
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits_f, h_f = _resnet_fwd(fw, xh)
+        loss_f = torch.nn.functional.cross_entropy(logits_f.float(), y.to(cuda))
+        loss_f.backward()
+    finally:
+        os.environ["PDO_OPS"] = "hip"
     torch.cuda.synchronize()
-
     logits_r, h_r = _resnet_fwd(ref, x)  # CPU: the framework ops in fp32
     loss_r = torch.nn.functional.cross_entropy(logits_r, y)
     loss_r.backward()
@@ -143,14 +161,20 @@ def test_resnet50_width_hip_vs_fp32(cuda):
         a, b = a.detach().float().cpu(), b.detach().float().cpu()
         return float((a - b).norm() / (b.norm() + 1e-12))
 
-    assert abs(loss_h.item() - loss_r.item()) < 2e-2 * abs(loss_r.item()), (loss_h.item(), loss_r.item())
-    assert rel(logits_h, logits_r) < 5e-2
-    assert rel(h_h.grad, h_r.grad) < 6e-2
-    rp = dict(ref.named_parameters())
-    errs = {n: rel(p.grad, rp[n].grad) for n, p in hip.named_parameters()}
-    bad = {n: e for n, e in errs.items() if not e < 6e-2}
-    assert not bad, bad
-    rb = dict(ref.named_buffers())
-    stats = {n: rel(b, rb[n]) for n, b in hip.named_buffers() if "running" in n}
-    bad = {n: e for n, e in stats.items() if not e < 2e-2}
+    def within(name, hip_t, fw_t, ref_t, bad):
+        eh, ef = rel(hip_t, ref_t), rel(fw_t, ref_t)
+        if not eh <= 1.5 * ef + 0.03:
+            bad[name] = (round(eh, 4), round(ef, 4))
+
+    assert abs(loss_h.item() - loss_r.item()) < 1e-2 * abs(loss_r.item()), (loss_h.item(), loss_r.item())
+    bad = {}
+    within("logits", logits_h, logits_f, logits_r, bad)
+    within("d(stem out)", h_h.grad, h_f.grad, h_r.grad, bad)
+    rp, fp = dict(ref.named_parameters()), dict(fw.named_parameters())
+    for n, p in hip.named_parameters():
+        within(n, p.grad, fp[n].grad, rp[n].grad, bad)
+    rb, fb = dict(ref.named_buffers()), dict(fw.named_buffers())
+    for n, b in hip.named_buffers():
+        if "running" in n:
+            within(n, b, fb[n], rb[n], bad)
     assert not bad, bad
