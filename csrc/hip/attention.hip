@@ -165,6 +165,21 @@ __device__ __forceinline__ void stage_load(Stage& st, const bf16* base, size_t r
   }
 }
 
+// the same tile by buffer loads: per-thread byte offsets are loop-invariant
+// VGPRs, the tile's row offset a scalar soffset — no per-tile 64-bit address math
+__device__ __forceinline__ void stage_voff(unsigned (&vo)[2], size_t row_stride, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, r = c >> 3, ch = c & 7;
+    vo[i] = (unsigned)(((size_t)r * row_stride + ch * 8) * 2);
+  }
+}
+__device__ __forceinline__ void stage_load_buf(Stage& st, __amdgpu_buffer_rsrc_t rsrc, const unsigned (&vo)[2],
+                                               unsigned soff) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) st.v[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[i], soff, 0));
+}
+
 __device__ __forceinline__ void stage_store(const Stage& st, bf16* T, int tid) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -304,10 +319,52 @@ __device__ __forceinline__ bf16x8 tr_frag_v(const bf16* Tlane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// causal triangle of a 32x32 block whose first key and first query coincide:
+// element r of lane (li, hh) holds key c(r) + 4hh of query li, masked iff
+// c(r) + 4hh > li — a compile-time 64-bit lane mask per register, applied as
+// the SGPR condition of one v_cndmask (no per-element compares)
+__device__ __forceinline__ constexpr unsigned long long tri_mask(int r) {
+  const int c = (r & 3) + 8 * (r >> 2);
+  return ((unsigned long long)((1u << (c + 4)) - 1) << 32) | ((1u << c) - 1);
+}
+
+__device__ __forceinline__ unsigned cvt_pk(float a, float b) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// store_acc_rows with the scale applied to register pairs and packed by v_cvt_pk
+__device__ __forceinline__ void store_acc_rows_pk(bf16* dst_row, const f32x16& acc, int c0, int hh, float s) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint2 v;
+    v.x = cvt_pk(acc[4 * g] * s, acc[4 * g + 1] * s);
+    v.y = cvt_pk(acc[4 * g + 2] * s, acc[4 * g + 3] * s);
+    *reinterpret_cast<uint2*>(dst_row + c0 + 8 * g + 4 * hh) = v;
+  }
+}
+
+typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// l += Σ of the 8 bf16 P values of a B-operand fragment (the values P·V uses)
+__device__ __forceinline__ float rowsum8(bf16x8 p, float acc) {
+  const bf16x2 one = {(bf16)1.f, (bf16)1.f};
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(p, p, 0, 1), one, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(p, p, 2, 3), one, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(p, p, 4, 5), one, acc, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(p, p, 6, 7), one, acc, false);
+}
+
+// Variant bits (A/B in one build, PDO_ATTN_FWDV): 1 = diagonal mask by lane-mask
+// constants (and the fully masked half skipped as −inf), two v_max3 chains
+// for the tile max, packed epilogue; 2 = row sums by v_dot2 over the packed P.
+template <int V>
 __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                               float* __restrict__ lse, int B, int S, int H, float c2, int order) {
+  constexpr bool NEW = V & 1, DOT = V & 2;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, li = lane & 31;
+  const int w = NEW ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int nqb = S / 128;
   int bh, r_;
   attn_block(order, nqb, B * H, bh, r_);
@@ -335,8 +392,19 @@ __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
   Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
+  unsigned vo[2];
+  __amdgpu_buffer_rsrc_t rk, rv;
+  if constexpr (NEW) {
+    const int nbytes = (int)((size_t)S * rs * 2 - (size_t)H * HD * 2 * 2 - (size_t)h * HD * 2);
+    rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(kbase), 0, nbytes, 0x00020000);
+    rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(vbase), 0, nbytes, 0x00020000);
+    stage_voff(vo, rs, tid);
+    stage_load_buf(sk, rk, vo, 0);
+    stage_load_buf(sv, rv, vo, 0);
+  } else {
+    stage_load(sk, kbase, rs, 0, tid);
+    stage_load(sv, vbase, rs, 0, tid);
+  }
   stage_store(sk, smem, tid);
   stage_store_v(sv, smem + TROWS * HD, tid);
   __syncthreads();
@@ -346,8 +414,14 @@ __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16
     const bf16* Vt = Kt + TROWS * HD;
     const bool more = t + 1 < ntiles;
     if (more) {
-      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
-      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+      if constexpr (NEW) {
+        const unsigned so = (unsigned)((t + 1) * TROWS * rs * 2);
+        stage_load_buf(sk, rk, vo, so);
+        stage_load_buf(sv, rv, vo, so);
+      } else {
+        stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+        stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+      }
     }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
@@ -358,21 +432,45 @@ __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16
         s1 = mfma(row_frag(Kt, 32, ks, lane), qf[ks], s1);
       }
       if (key0 + TROWS - 1 > qb * 128 + w * 32) {  // diagonal tile (wave-uniform)
-        // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
-        const int d = q - key0 - 4 * hh;
+        if constexpr (NEW) {
+          // odd wave: keys of s0 precede every query, s1 is the triangle; even
+          // wave: s0 is the triangle, s1 follows every query
+          if (w & 1) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int c = (r & 3) + 8 * (r >> 2);
-          s0[r] = c > d ? -INFINITY : s0[r];
-          s1[r] = c + 32 > d ? -INFINITY : s1[r];
+            for (int r = 0; r < 16; ++r) s1[r] = __builtin_amdgcn_inverse_ballot_w64(tri_mask(r)) ? -INFINITY : s1[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s0[r] = __builtin_amdgcn_inverse_ballot_w64(tri_mask(r)) ? -INFINITY : s0[r];
+            s1 = bcast16(-INFINITY);
+          }
+        } else {
+          // element r holds key key0 + c(r) + 4hh (+32 in s1): masked iff c(r) > q - key0 - 4hh
+          const int d = q - key0 - 4 * hh;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = (r & 3) + 8 * (r >> 2);
+            s0[r] = c > d ? -INFINITY : s0[r];
+            s1[r] = c + 32 > d ? -INFINITY : s1[r];
+          }
         }
       }
       // tile max of s' (relative to m): only a growth past 2^8 rescales
       // (defer-max, cdna_hip_programming.md T13); the first tile sets m
-      float tmax = -INFINITY;
+      float tmax;
+      if constexpr (NEW) {
+        float ta = fmaxf(s0[0], s1[0]), tb = fmaxf(s0[1], s1[1]);
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-      tmax = xhalf_max(tmax);
+        for (int r = 2; r < 16; r += 2) {
+          ta = fmaxf(fmaxf(ta, s0[r]), s1[r]);
+          tb = fmaxf(fmaxf(tb, s0[r + 1]), s1[r + 1]);
+        }
+        tmax = xhalf_max(fmaxf(ta, tb));
+      } else {
+        tmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
+        tmax = xhalf_max(tmax);
+      }
       if (t == 0) {  // every query has key 0 unmasked here: tmax is finite
         m = tmax;
         s0 -= tmax;
@@ -389,20 +487,33 @@ __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16
         s1 -= d;
         nm16 = bcast16(-m);
       }
-      f32x2 ls2 = {0.f, 0.f};
+      if constexpr (DOT) {
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
-        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
-        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+        for (int r = 0; r < 16; ++r) {
+          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+        }
+      } else {
+        f32x2 ls2 = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+          s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+          s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+          ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
+        }
+        l += ls2[0] + ls2[1];
       }
-      l += ls2[0] + ls2[1];
       const bf16* V0 = Vt + vb0;
       const bf16* V1 = Vt + vb1;
+      float la = 0.f, lb = 0.f;
       {
         const bf16x8 p0 = pack8(s0, 0), p1 = pack8(s1, 0);
+        if constexpr (DOT) {
+          la = rowsum8(p0, la);
+          lb = rowsum8(p1, lb);
+        }
         o0 = mfma(tr_frag_v<0>(V0), p0, o0);
         o1 = mfma(tr_frag_v<0>(V1), p0, o1);
         o0 = mfma(tr_frag_v<32>(V0), p1, o0);
@@ -410,11 +521,16 @@ __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16
       }
       {
         const bf16x8 p0 = pack8(s0, 1), p1 = pack8(s1, 1);
+        if constexpr (DOT) {
+          la = rowsum8(p0, la);
+          lb = rowsum8(p1, lb);
+        }
         o0 = mfma(tr_frag_v<16>(V0), p0, o0);
         o1 = mfma(tr_frag_v<16>(V1), p0, o1);
         o0 = mfma(tr_frag_v<48>(V0), p1, o0);
         o1 = mfma(tr_frag_v<48>(V1), p1, o1);
       }
+      if constexpr (DOT) l += la + lb;
     }
     if (more) {
       bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
@@ -424,191 +540,33 @@ __device__ __forceinline__ void attn_fwd_body(const bf16* __restrict__ qkv, bf16
     __syncthreads();
   }
   const float lt = xhalf_sum(l);
-  const float inv = 1.f / lt;
   bf16* orow = out + ((size_t)(b * S + q) * H + h) * HD;
-  store_acc_rows(orow, o0, 0, hh, inv);
-  store_acc_rows(orow, o1, 32, hh, inv);
-  if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
+  if constexpr (NEW) {
+    // lt ≥ 1: the key that set m contributes exp2(0)
+    const float inv = __builtin_amdgcn_rcpf(lt);
+    store_acc_rows_pk(orow, o0, 0, hh, inv);
+    store_acc_rows_pk(orow, o1, 32, hh, inv);
+    if (hh == 0) lse[(size_t)bh * S + q] = (m + __builtin_amdgcn_logf(lt)) * LN2;
+  } else {
+    const float inv = 1.f / lt;
+    store_acc_rows(orow, o0, 0, hh, inv);
+    store_acc_rows(orow, o1, 32, hh, inv);
+    if (hh == 0) lse[(size_t)bh * S + q] = (m + log2f(lt)) * LN2;
+  }
 }
 
-__global__ __launch_bounds__(256) void attn_fwd_d64(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                     float* __restrict__ lse, int B, int S, int H, float c2,
-                                                     int order) {
-  attn_fwd_body(qkv, out, lse, B, S, H, c2, order);
-}
-// the same body capped at 168 registers for 3 waves per SIMD — the default:
-// 142.20 / 142.32 vs 142.49 / 142.61 ms per GPT-2-medium step for the
-// 2-wave build (PDO_ATTN_FWD3=0, its A/B alternative), no spills (165 VGPRs);
-// a 4-wave cap spills (29 VGPRs)
+// 168 registers for 3 waves per SIMD: 142.20 / 142.32 vs 142.49 / 142.61 ms per
+// GPT-2-medium step for the 2-wave build of the same body (since removed); a
+// 4-wave cap spills (29 VGPRs).  A 256-query workgroup (64 rows per wave: each
+// LDS K/V fragment feeds two sub-blocks, half the K/V traffic, LDS reads and
+// barriers per query) measured no faster (309.6 vs 312.5 µs, 301.5 vs 302.3)
+// and was removed: the forward is VALU-issue bound (rocprofv3 --pmc:
+// SQ_INSTS_VALU ≈ 12 per MFMA), not LDS- or barrier-bound.
+template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd3_d64(
     const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int S, int H, float c2,
     int order) {
-  attn_fwd_body(qkv, out, lse, B, S, H, c2, order);
-}
-
-// ----- forward, 64 query rows per wave -----
-// A workgroup = 4 waves = 256 queries of one (b, h); wave w owns two 32-row
-// sub-blocks, rows 32w + li (u = 0) and 128 + 32w + li (u = 1) of the block,
-// so every wave needs the same key tiles to within one (causal balance).  Each
-// K row fragment and V transposed fragment read from LDS feeds the MFMAs of
-// both sub-blocks, every staged K/V tile serves 256 queries instead of 128, and
-// the two sub-blocks' softmax chains interleave in one wave (ILP).  The score
-// MFMAs start from 0 and the row maximum is subtracted in the exponent (packed
-// fp32 subtract): no −m broadcast accumulators, which keeps the kernel at
-// 2 waves per SIMD.
-__device__ __forceinline__ void attn_fwd64_body(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                float* __restrict__ lse, int B, int S, int H, float c2, int order) {
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];  // [buf][K|V][64][64]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
-  const int nqb = S / 256;
-  int bh, r_;
-  attn_block(order, nqb, B * H, bh, r_);
-  const int qb = nqb - 1 - r_;  // heaviest query blocks first
-  const int b = bh / H, h = bh % H;
-  const size_t rs = (size_t)3 * H * HD;
-  const bf16* qbase = qkv + (size_t)b * S * rs + (size_t)h * HD;
-  const bf16* kbase = qbase + (size_t)H * HD;
-  const bf16* vbase = qbase + (size_t)2 * H * HD;
-
-  int q[2], qmin[2];
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    qmin[u] = qb * 256 + 128 * u + 32 * w;
-    q[u] = qmin[u] + li;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      qf[u][ks] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q[u] * rs + 16 * ks + 8 * hh);
-  }
-  retire(qf[0]);
-  retire(qf[1]);
-  prescale(qf[0], c2);
-  prescale(qf[1], c2);
-
-  const int vb0 = tr_base_v(0, lane), vb1 = tr_base_v(32, lane);
-  f32x16 o[2][2] = {{zero16(), zero16()}, {zero16(), zero16()}};
-  float m[2] = {0.f, 0.f}, l[2] = {0.f, 0.f};
-  const int ntiles = (qb * 256 + 256) / TROWS;
-
-  Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
-  stage_store(sk, smem, tid);
-  stage_store_v(sv, smem + TROWS * HD, tid);
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
-    const bf16* Vt = Kt + TROWS * HD;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
-      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
-    }
-    const int key0 = t * TROWS;
-    const bool act0 = key0 <= qmin[0] + 31;  // sub-block 0 still has keys (wave-uniform); u = 1 always
-    f32x16 sc[2][2];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 k0 = row_frag(Kt, 0, ks, lane), k1 = row_frag(Kt, 32, ks, lane);
-      if (ks == 0) {
-        sc[1][0] = mfma(k0, qf[1][0], zero16());
-        sc[1][1] = mfma(k1, qf[1][0], zero16());
-        if (act0) {
-          sc[0][0] = mfma(k0, qf[0][0], zero16());
-          sc[0][1] = mfma(k1, qf[0][0], zero16());
-        }
-      } else {
-        sc[1][0] = mfma(k0, qf[1][ks], sc[1][0]);
-        sc[1][1] = mfma(k1, qf[1][ks], sc[1][1]);
-        if (act0) {
-          sc[0][0] = mfma(k0, qf[0][ks], sc[0][0]);
-          sc[0][1] = mfma(k1, qf[0][ks], sc[0][1]);
-        }
-      }
-    }
-    // softmax of sub-block u: mask its diagonal tile, defer-max (T13), exponentiate, row sums
-    auto softmax = [&](int u) {
-      f32x16& s0 = sc[u][0];
-      f32x16& s1 = sc[u][1];
-      if (key0 + TROWS - 1 > qmin[u]) {  // diagonal tile (wave-uniform)
-        const int d = q[u] - key0 - 4 * hh;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int c = (r & 3) + 8 * (r >> 2);
-          s0[r] = c > d ? -INFINITY : s0[r];
-          s1[r] = c + 32 > d ? -INFINITY : s1[r];
-        }
-      }
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) tmax = fmaxf(fmaxf(tmax, fmaxf(s0[r], s1[r])), fmaxf(s0[r + 1], s1[r + 1]));
-      tmax = xhalf_max(tmax);
-      if (t == 0) {  // key 0 is unmasked for every query: finite
-        m[u] = tmax;
-      } else if (__any(tmax - m[u] > 8.f)) {
-        const float d = tmax - m[u] > 8.f ? tmax - m[u] : 0.f;
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-        m[u] += d;
-        l[u] *= alpha;
-        o[u][0] *= alpha;
-        o[u][1] *= alpha;
-      }
-      const f32x2 nm = {-m[u], -m[u]};
-      f32x2 ls2 = {0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f32x2 a0 = f32x2{s0[r], s0[r + 1]} + nm, a1 = f32x2{s1[r], s1[r + 1]} + nm;
-        s0[r] = __builtin_amdgcn_exp2f(a0[0]);
-        s0[r + 1] = __builtin_amdgcn_exp2f(a0[1]);
-        s1[r] = __builtin_amdgcn_exp2f(a1[0]);
-        s1[r + 1] = __builtin_amdgcn_exp2f(a1[1]);
-        ls2 += f32x2{s0[r], s0[r + 1]} + f32x2{s1[r], s1[r + 1]};
-      }
-      l[u] += ls2[0] + ls2[1];
-    };
-    softmax(1);
-    if (act0) softmax(0);
-    const bf16* V0 = Vt + vb0;
-    const bf16* V1 = Vt + vb1;
-    auto pv = [&](auto k_tag, int sst, int half) {
-      constexpr int K0 = decltype(k_tag)::value;
-      const bf16x8 va = tr_frag_v<K0>(V0), vbv = tr_frag_v<K0>(V1);
-      const bf16x8 p1 = pack8(sc[1][half], sst);
-      o[1][0] = mfma(va, p1, o[1][0]);
-      o[1][1] = mfma(vbv, p1, o[1][1]);
-      if (act0) {
-        const bf16x8 p0 = pack8(sc[0][half], sst);
-        o[0][0] = mfma(va, p0, o[0][0]);
-        o[0][1] = mfma(vbv, p0, o[0][1]);
-      }
-    };
-    pv(std::integral_constant<int, 0>{}, 0, 0);
-    pv(std::integral_constant<int, 32>{}, 0, 1);
-    pv(std::integral_constant<int, 16>{}, 1, 0);
-    pv(std::integral_constant<int, 48>{}, 1, 1);
-    if (more) {
-      bf16* Kn = smem + ((t + 1) & 1) * 2 * TROWS * HD;
-      stage_store(sk, Kn, tid);
-      stage_store_v(sv, Kn + TROWS * HD, tid);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const float lt = xhalf_sum(l[u]);
-    const float inv = 1.f / lt;
-    bf16* orow = out + ((size_t)(b * S + q[u]) * H + h) * HD;
-    store_acc_rows(orow, o[u][0], 0, hh, inv);
-    store_acc_rows(orow, o[u][1], 32, hh, inv);
-    if (hh == 0) lse[(size_t)bh * S + q[u]] = (m[u] + log2f(lt)) * LN2;
-  }
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd64_d64(
-    const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int S, int H, float c2,
-    int order) {
-  attn_fwd64_body(qkv, out, lse, B, S, H, c2, order);
+  attn_fwd_body<V>(qkv, out, lse, B, S, H, c2, order);
 }
 
 // ============================================================================
@@ -912,13 +870,17 @@ static int attn_order() {
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
-  static const int fwd3 = env_int("PDO_ATTN_FWD3", 1);
-  if (fwd3 == 2 && S % 256 == 0)
-    attn_fwd64_d64<<<B * H * (S / 256), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else if (fwd3)
-    attn_fwd3_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
-  else
-    attn_fwd_d64<<<B * H * (S / 128), 256, 0, st>>>(qkv, o, lse, B, S, H, scale * LOG2E, attn_order());
+  static const int v = env_int("PDO_ATTN_FWDV", 0);
+  const int grid = B * H * (S / 128);
+  const float c2 = scale * LOG2E;
+  // buffer-load variants address the (b, h) slice with 31-bit byte offsets
+  const bool fits = (size_t)S * 3 * H * HD * 2 < (1ull << 31);
+  switch (fits ? v : 0) {
+    case 1: attn_fwd3_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order()); break;
+    case 2: attn_fwd3_d64<2><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order()); break;
+    case 3: attn_fwd3_d64<3><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order()); break;
+    default: attn_fwd3_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order());
+  }
   return 0;
 }
 

@@ -333,6 +333,17 @@ void sumsq(at::Tensor g, at::Tensor out, double scale) {
   CHECK_RC(pdo::sumsq(bp(g), g.numel(), fp(part), cap, (float)scale, fp(out), cur_stream()), "sumsq");
 }
 
+void sumsq_chunks(at::Tensor g, at::Tensor part, int64_t chunk, int64_t k0, int64_t k1) {
+  CHECK_IN(g); CHECK_IN(part); CHECK_BF16(g); CHECK_F32(part);
+  TORCH_CHECK(k0 >= 0 && k1 <= part.numel() && (k1 - 1) * chunk < g.numel(), "sumsq_chunks: chunk range");
+  CHECK_RC(pdo::sumsq_chunks(bp(g), g.numel(), chunk, (int)k0, (int)k1, fp(part), cur_stream()), "sumsq_chunks");
+}
+
+void sumsq_total(at::Tensor part, at::Tensor out, double scale) {
+  CHECK_IN(part); CHECK_IN(out); CHECK_F32(part); CHECK_F32(out);
+  CHECK_RC(pdo::sumsq_total(fp(part), (int)part.numel(), (float)scale, fp(out), cur_stream()), "sumsq_total");
+}
+
 void adamw_flat(at::Tensor p, at::Tensor g, at::Tensor master, at::Tensor m1, at::Tensor m2, at::Tensor decay,
                 at::Tensor normsq, double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
                 double grad_scale, double clip) {
@@ -1145,6 +1156,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("embed_bwd_sorted", &embed_bwd_sorted);
   m.def("sumsq", &sumsq);
+  m.def("sumsq_chunks", &sumsq_chunks);
+  m.def("sumsq_total", &sumsq_total);
   m.def("adamw_flat", &adamw_flat);
   m.def("sgd_flat", &sgd_flat);
   m.def("splitk_add", &splitk_add);

@@ -195,6 +195,10 @@ int cast_f32_bf16(const float* in, bf16* out, long long n, hipStream_t st);
 
 // optim.hip
 int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, float* out, hipStream_t st);
+// Σ g² per fixed chunk (elements [k·chunk, (k+1)·chunk)) for chunks [k0, k1) → part[k]
+int sumsq_chunks(const bf16* g, long long n, long long chunk, int k0, int k1, float* part, hipStream_t st);
+// out[0] = scale² · Σ part[0..K), in a fixed order
+int sumsq_total(const float* part, int K, float scale, float* out, hipStream_t st);
 int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, const float* decay_chunks,
                const float* normsq, long long n, float lr, float b1, float b2, float eps, float wd, float bc1,
                float bc2, float grad_scale, float clip, hipStream_t st);

@@ -32,6 +32,24 @@ __global__ __launch_bounds__(1024) void sumsq_final_kernel(const float* __restri
   if (threadIdx.x == 0) out[0] = s * scale2;
 }
 
+// one block per fixed chunk of the gradient: part[k0 + b] = Σ g² over chunk k0 + b
+// (chunk boundaries independent of which call computes them, so partials taken
+// bucket by bucket as each all-reduce lands sum to the same bits as one pass)
+__global__ __launch_bounds__(256) void sumsq_chunk_kernel(const bf16* __restrict__ g, long long nvec, long long cvec,
+                                                          int k0, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int k = k0 + blockIdx.x;
+  const long long lo = (long long)k * cvec, hi = lo + cvec < nvec ? lo + cvec : nvec;
+  float s = 0.f;
+  for (long long i = lo + threadIdx.x; i < hi; i += 256) {
+    f32x8 v = to_f32(reinterpret_cast<const bf16x8*>(g)[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) part[k] = s;
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
                                                     float* __restrict__ master, float* __restrict__ m1,
                                                     float* __restrict__ m2, const float* __restrict__ decay_chunks,
@@ -170,6 +188,18 @@ int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, fl
   if (G > part_cap) G = part_cap;
   sumsq_part_kernel<<<G, 256, 0, st>>>(g, n / 8, part);
   sumsq_final_kernel<<<1, 1024, 0, st>>>(part, G, scale * scale, out);
+  return 0;
+}
+
+int sumsq_chunks(const bf16* g, long long n, long long chunk, int k0, int k1, float* part, hipStream_t st) {
+  if (k1 == k0) return 0;
+  if (n % 8 || chunk % 8 || k1 < k0) return -2;
+  sumsq_chunk_kernel<<<k1 - k0, 256, 0, st>>>(g, n / 8, chunk / 8, k0, part);
+  return 0;
+}
+
+int sumsq_total(const float* part, int K, float scale, float* out, hipStream_t st) {
+  sumsq_final_kernel<<<1, 1024, 0, st>>>(part, K, scale * scale, out);
   return 0;
 }
 

@@ -17,9 +17,12 @@ from .. import _native
 from . import use_hip
 
 
+NORM_CHUNK = 1 << 18  # elements per global-norm partial
+
+
 class FlatAdamW:
     def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
-                 max_grad_norm: float | None = 1.0):
+                 max_grad_norm: float | None = 1.0, norm_chunk: int = NORM_CHUNK):
         self.flat = flat
         self.lr = lr
         self.b1, self.b2 = betas
@@ -31,16 +34,42 @@ class FlatAdamW:
         self.m = torch.zeros_like(self.master)
         self.v = torch.zeros_like(self.master)
         self._norm_buf = torch.zeros(2, dtype=torch.float32, device=flat.device)
+        # global-norm partials per fixed chunk of the parameter range; BucketedDDP.finish
+        # computes those of each bucket as its all-reduce lands (norm_partial), the
+        # step the rest — the same chunks summed in the same order either way
+        n = flat.param_grads.numel()
+        self._chunk = norm_chunk
+        self._norm_part = torch.zeros((n + norm_chunk - 1) // norm_chunk, dtype=torch.float32, device=flat.device)
+        self._norm_next = 0
+
+    def norm_reset(self):
+        self._norm_next = 0
+
+    def norm_partial(self, upto: int):
+        """Σ g² of every chunk not yet summed this step that ends at or before
+        element ``upto`` of the parameter range (the whole range from its end on)."""
+        g = self.flat.param_grads
+        k1 = self._norm_part.numel() if upto >= g.numel() else upto // self._chunk
+        k0 = self._norm_next
+        if k1 <= k0:
+            return
+        if use_hip(g):
+            _native.require_hip().sumsq_chunks(g, self._norm_part, self._chunk, k0, k1)
+        else:
+            c = self._chunk
+            for k in range(k0, k1):
+                seg = g[k * c:(k + 1) * c].float()
+                self._norm_part[k] = (seg * seg).sum()
+        self._norm_next = k1
 
     def grad_norm_sq(self, grad_scale=1.0):
         """Device scalar of ||grad_scale * g||^2 (no sync)."""
-        g = self.flat.param_grads
-        if use_hip(g):
-            m = _native.require_hip()
-            m.sumsq(g, self._norm_buf, grad_scale)
-            return self._norm_buf[0]
-        gs = g.float() * grad_scale
-        self._norm_buf[0] = (gs * gs).sum()
+        self.norm_partial(self.flat.param_grads.numel())
+        self._norm_next = 0
+        if use_hip(self.flat.param_grads):
+            _native.require_hip().sumsq_total(self._norm_part, self._norm_buf, grad_scale)
+        else:
+            self._norm_buf[0] = self._norm_part.sum() * (grad_scale * grad_scale)
         return self._norm_buf[0]
 
     @torch.no_grad()

@@ -64,7 +64,11 @@ class BucketedDDP:
         self._pending = [0] * len(flat.buckets)
         self._sizes = [len(b.slots) for b in flat.buckets]
         self._works = []
+        self._work_bucket = []
         self._sync = True
+        # first arena element the post-drain fold of a split gradient rewrites
+        owners = {a.name[:-len("#head")] for a in flat.aux_slots}
+        self._fold_start = min([s.offset for s in flat.slots if s.name in owners], default=flat.numel)
         self._launched = [False] * len(flat.buckets)
         self._next = 0
         self._bucket_of = flat.bucket_of()
@@ -109,20 +113,36 @@ class BucketedDDP:
         self._pending = [0] * len(self.flat.buckets)
         self._launched = [False] * len(self.flat.buckets)
         self._works = []
+        self._work_bucket = []
         self._next = 0
         self._seen = set()
         self._staged = False
 
-    def finish(self):
+    def finish(self, opt=None):
         """Call after backward: launch stragglers, make the compute stream wait,
-        then fold split parameters' head-gradient slots into their gradients."""
+        then fold split parameters' head-gradient slots into their gradients.
+
+        ``opt`` (a FlatAdamW with clipping): its global-norm partials of each
+        parameter bucket are queued right behind that bucket's wait, so they run
+        while later buckets — the tied embedding's 105 MB tail last — are still
+        on the wire; only the ranges the fold or the fp32 cast-back rewrite after
+        the drain wait for the optimizer step."""
         _flush_reductions(buf_device=self.flat.device)
         if self.enabled and self._sync:
             while self._next < len(self.flat.buckets):
                 self._launch(self._next)
-            for w in self._works:
+            limit = 0 if self.stage is not None or opt is None else self._fold_start
+            if opt is not None:
+                opt.norm_reset()
+            # collectives on one communicator complete in issue order; parameter
+            # buckets are issued in ascending arena order
+            for i, w in zip(self._work_bucket, self._works):
                 w.wait()
+                b = self.flat.buckets[i]
+                if limit and b.start < self.flat.numel:
+                    opt.norm_partial(min(b.end, limit))
             self._works = []
+            self._work_bucket = []
             if self._staged:
                 self._cast_back()
         self.flat.fold_split()
@@ -179,6 +199,7 @@ class BucketedDDP:
             self._works[-1].wait()
         w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._works.append(w)
+        self._work_bucket.append(i)
 
     def _cast_back(self):
         g, st = self.flat.grads, self.stage

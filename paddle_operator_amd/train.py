@@ -131,7 +131,7 @@ class GPT2Trainer:
             with trace.range("backward"), deferred_reductions(self.device):
                 loss.backward()
         with trace.range("allreduce_drain"):
-            self.ddp.finish()
+            self.ddp.finish(self.opt if self.opt.max_grad_norm else None)
         with trace.range("optimizer"):
             self.opt.step(grad_scale=self.ddp.grad_scale)
         return loss

@@ -93,6 +93,59 @@ def test_bucketed_ddp_matches_full_batch(tmp_path, split):
         assert err < 1e-5, f"{n}: rel err {err}"
 
 
+def _norm_order_worker(rank, world, port, outdir, early):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PDO_OPS="torch")
+    torch.set_num_threads(1)
+    from paddle_operator_amd.models.gpt2 import GPT2, GPT2Config
+    from paddle_operator_amd.ops.optim import FlatAdamW
+    from paddle_operator_amd.parallel.ddp import BucketedDDP
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = GPT2Config.named("gpt2-tiny")
+    model = GPT2(cfg)
+    flat = FlatParams(model, dtype=torch.float32, device="cpu", bucket_bytes=64 << 10, late=("wte",), split=("wte",))
+    ddp = BucketedDDP(flat)
+    # a small clip so the coefficient is active; small chunks so buckets own many of them
+    opt = FlatAdamW(flat, lr=1e-3, max_grad_norm=0.05, norm_chunk=4096)
+    x, y = _batch(cfg, B=8)
+    per = x.shape[0] // world
+    sl = slice(rank * per, (rank + 1) * per)
+    early_chunks = []
+    for _ in range(3):
+        flat.zero_grad()
+        ddp.prepare()
+        model(x[sl], y[sl]).backward()
+        ddp.finish(opt if early else None)
+        early_chunks.append(opt._norm_next)
+        opt.step(grad_scale=ddp.grad_scale)
+    torch.save({"params": flat.params.clone(), "early_chunks": early_chunks, "nchunks": opt._norm_part.numel(),
+                "fold_chunk": ddp._fold_start // 4096}, os.path.join(outdir, f"p{rank}_{int(early)}.pt"))
+    dist.destroy_process_group()
+
+
+def test_norm_partials_per_bucket_bit_identical(tmp_path):
+    """BucketedDDP.finish(opt) sums each parameter bucket's global-norm chunks as
+    its all-reduce lands (only the tied embedding's tail range waits for the
+    step): 4 ranks, 3 clipped AdamW steps, parameters bit-identical to
+    finish() followed by the whole-range norm in the step."""
+    os.environ["PDO_OPS"] = "torch"
+    for early in (False, True):
+        mp.start_processes(_norm_order_worker, args=(4, _free_port(), str(tmp_path), early), nprocs=4,
+                           start_method="spawn")
+    for r in range(4):
+        a = torch.load(tmp_path / f"p{r}_0.pt", weights_only=True)
+        b = torch.load(tmp_path / f"p{r}_1.pt", weights_only=True)
+        assert torch.equal(a["params"], b["params"]), f"rank {r}: parameters differ"
+        assert a["early_chunks"] == [0, 0, 0]
+        # everything before the tied embedding's slot was summed before the step
+        assert all(c == b["fold_chunk"] for c in b["early_chunks"]), (b["early_chunks"], b["fold_chunk"])
+        assert 0 < b["fold_chunk"] < b["nchunks"]
+    a0 = torch.load(tmp_path / "p0_1.pt", weights_only=True)["params"]
+    for r in range(1, 4):
+        assert torch.equal(a0, torch.load(tmp_path / f"p{r}_1.pt", weights_only=True)["params"])
+
+
 def _bench_env():
     env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2", PDO_OPS="torch")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):

@@ -469,6 +469,27 @@ def test_attention_forced_rescale(cuda):
     assert rel_err(o, of) < 2e-2
 
 
+def test_grad_norm_chunks_order_independent(cuda):
+    """Global-norm partials per fixed chunk (csrc/hip/optim.hip sumsq_chunks):
+    taken in bucket-sized pieces or in one pass, the same bits; against fp64."""
+    from paddle_operator_amd.ops.optim import FlatAdamW
+    from paddle_operator_amd.parallel.flat import FlatParams
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(1024, 1000), torch.nn.Linear(1000, 700)).to(cuda).bfloat16()
+    fp_ = FlatParams(net, device=cuda)
+    opt = FlatAdamW(fp_, lr=1e-2, max_grad_norm=0.5, norm_chunk=1 << 16)
+    assert opt._norm_part.numel() > 20
+    fp_.grads.copy_(torch.randn_like(fp_.grads.float()).bfloat16())
+    one = opt.grad_norm_sq(0.5).clone()
+    opt.norm_reset()
+    for upto in (70_000, 70_001, 300_000, 900_000, 1_000_000):  # bucket ends, not chunk-aligned
+        opt.norm_partial(upto)
+    split = opt.grad_norm_sq(0.5).clone()
+    assert torch.equal(one, split)
+    ref = (fp_.param_grads.double() * 0.5).pow(2).sum()
+    assert abs(float(one) - float(ref)) / float(ref) < 1e-5
+
+
 def test_adamw_matches_reference(cuda):
     from paddle_operator_amd.ops.optim import FlatAdamW
     from paddle_operator_amd.parallel.flat import FlatParams
