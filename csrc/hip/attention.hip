@@ -100,6 +100,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* T, int k0, int cbase, int 
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// transposed fragment from two precomputed per-lane addresses (rows k0 and k0 + 8)
+__device__ __forceinline__ bf16x8 ld_tr(const bf16* lo_p, const bf16* hi_p) {
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)lo_p);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)hi_p);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // 8 accumulator registers [8s, 8s+8) → bf16 B-operand fragment
 __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
   bf16x8 r;
@@ -734,13 +741,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // ============================================================================
 // backward dQ: workgroup = 128 queries of one (b,h); loop over key tiles
 // ============================================================================
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                       const bf16* __restrict__ o, const float* __restrict__ lse,
-                                                       float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S,
-                                                       int H, float c2, float scale, float* __restrict__ dbias_part,
-                                                       int order) {
+// Variant bits (PDO_ATTN_DQV): 1 = K/V staging by buffer loads (scalar tile
+// offset), per-lane LDS fragment offsets computed once (rows advance in
+// multiples of 16, which the swizzle does not see: the tile loop adds only
+// immediates), the diagonal tile's triangle masked by lane-mask constants and
+// its fully masked 32-key half skipped.
+template <int V>
+__device__ __forceinline__ void dq_body(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                        const bf16* __restrict__ o, const float* __restrict__ lse,
+                                        float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S, int H,
+                                        float c2, float scale, float* __restrict__ dbias_part, int order) {
+  constexpr bool NEW = V & 1;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * TROWS * HD];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, li = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, li = lane & 31;
+  const int w = NEW ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int nqb = S / 128;
   int bh, r_;
   attn_block(order, nqb, B * H, bh, r_);
@@ -792,8 +806,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int wave_qmax = qb * 128 + w * 32 + 31;
 
   Stage sk, sv;
-  stage_load(sk, kbase, rs, 0, tid);
-  stage_load(sv, vbase, rs, 0, tid);
+  unsigned vo[2];
+  __amdgpu_buffer_rsrc_t rk, rv;
+  // per-lane fragment offsets (NEW): row reads roff[ks] = toff(li, 2ks + hh);
+  // transposed reads of V-columns half c: rows 4(g>>1) + q (lo) and + 8 (hi)
+  int roff[4], tlo[2], thi[2];
+  if constexpr (NEW) {
+    const int nbytes = (int)((size_t)S * rs * 2 - (size_t)H * HD * 2 * 2 - (size_t)h * HD * 2);
+    rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(kbase), 0, nbytes, 0x00020000);
+    rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(vbase), 0, nbytes, 0x00020000);
+    stage_voff(vo, rs, tid);
+    stage_load_buf(sk, rk, vo, 0);
+    stage_load_buf(sv, rv, vo, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) roff[ks] = toff(li, 2 * ks + hh);
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = 32 * c + 16 * (g & 1) + 4 * pp, r0 = 4 * (g >> 1) + qq;
+      tlo[c] = toff(r0, col >> 3) + (col & 7);
+      thi[c] = toff(r0 + 8, col >> 3) + (col & 7);
+    }
+  } else {
+    stage_load(sk, kbase, rs, 0, tid);
+    stage_load(sv, vbase, rs, 0, tid);
+  }
   stage_store(sk, smem, tid);
   stage_store(sv, smem + TROWS * HD, tid);
   __syncthreads();
@@ -802,40 +839,65 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const bf16* Kt = smem + (t & 1) * 2 * TROWS * HD;
     const bf16* Vt = Kt + TROWS * HD;
     if (more) {
-      stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
-      stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+      if constexpr (NEW) {
+        const unsigned so = (unsigned)((t + 1) * TROWS * rs * 2);
+        stage_load_buf(sk, rk, vo, so);
+        stage_load_buf(sv, rv, vo, so);
+      } else {
+        stage_load(sk, kbase, rs, (t + 1) * TROWS, tid);
+        stage_load(sv, vbase, rs, (t + 1) * TROWS, tid);
+      }
     }
     const int key0 = t * TROWS;
     if (key0 <= wave_qmax) {
       const bool diag = key0 + TROWS - 1 > qb * 128 + w * 32;
 #pragma unroll
       for (int ksub = 0; ksub < 2; ++ksub) {
+        // diagonal tile: an even wave's second 32 keys follow all its queries
+        if (NEW && ksub == 1 && diag && !(w & 1)) continue;
         f32x16 s = zero16(), dp = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
-          dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
+          if constexpr (NEW) {
+            s = mfma(*reinterpret_cast<const bf16x8*>(Kt + 32 * ksub * HD + roff[ks]), qf[ks], s);
+            dp = mfma(*reinterpret_cast<const bf16x8*>(Vt + 32 * ksub * HD + roff[ks]), df[ks], dp);
+          } else {
+            s = mfma(row_frag(Kt, 32 * ksub, ks, lane), qf[ks], s);
+            dp = mfma(row_frag(Vt, 32 * ksub, ks, lane), df[ks], dp);
+          }
         }
         auto softmax_grad = [&](auto masked) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[r], c2, -lq));
             if constexpr (decltype(masked)::value) {
-              const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              p = kr > q ? 0.f : p;
+              if constexpr (NEW) {
+                p = __builtin_amdgcn_inverse_ballot_w64(tri_mask(r)) ? 0.f : p;
+              } else {
+                const int kr = key0 + 32 * ksub + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                p = kr > q ? 0.f : p;
+              }
             }
             s[r] = p * (dp[r] - dq_delta);  // dS^T
           }
         };
-        if (diag)  // wave-uniform: only the diagonal tile pays for the mask
+        // wave-uniform: only the diagonal 32 × 32 block pays for the mask (NEW: the
+        // triangle — the even wave's first half, the odd wave's second)
+        if (NEW ? (diag && (w & 1) == ksub) : diag)
           softmax_grad(std::true_type{});
         else
           softmax_grad(std::false_type{});
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
           const bf16x8 dsb = pack8(s, sst);
-          a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
-          a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
+          if constexpr (NEW) {
+            const bf16* T = Kt + (32 * ksub + 16 * sst) * HD;
+            a0 = mfma(ld_tr(T + tlo[0], T + thi[0]), dsb, a0);
+            a1 = mfma(ld_tr(T + tlo[1], T + thi[1]), dsb, a1);
+          } else {
+            a0 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 0, lane), dsb, a0);
+            a1 = mfma(tr_frag(Kt, 32 * ksub + 16 * sst, 32, lane), dsb, a1);
+          }
         }
       }
     }
@@ -847,8 +909,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     __syncthreads();
   }
   bf16* qrow = dqkv + (size_t)(b * S + q) * rs + (size_t)h * HD;
-  store_acc_rows(qrow, a0, 0, hh, scale);
-  store_acc_rows(qrow, a1, 32, hh, scale);
+  if constexpr (NEW) {
+    store_acc_rows_pk(qrow, a0, 0, hh, scale);
+    store_acc_rows_pk(qrow, a1, 32, hh, scale);
+  } else {
+    store_acc_rows(qrow, a0, 0, hh, scale);
+    store_acc_rows(qrow, a1, 32, hh, scale);
+  }
   if (dbias_part) {  // q slot of the QKV bias-gradient partial row b·(S/128) + qb
     float* prow = dbias_part + (size_t)(b * (S / 128) + qb) * (3 * H * HD) + (size_t)h * HD;
     float* red = reinterpret_cast<float*>(smem);
@@ -857,6 +924,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     float* const out[1] = {prow};
     colsum_finish<1>(red, out, tid);
   }
+}
+
+template <int V>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dq_d64(
+    const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const bf16* __restrict__ o,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv, int B, int S, int H, float c2,
+    float scale, float* __restrict__ dbias_part, int order) {
+  dq_body<V>(qkv, dout, o, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 
 static int env_int(const char* k, int def) {
@@ -889,8 +964,14 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  attn_bwd_dq_d64<<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
-                                        attn_order());
+  static const int dqv = env_int("PDO_ATTN_DQV", 0);
+  const bool fits = (size_t)S * 3 * H * HD * 2 < (1ull << 31);
+  if (dqv == 1 && fits)
+    attn_bwd_dq_d64<1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                             dbias_part, attn_order());
+  else
+    attn_bwd_dq_d64<0><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                             dbias_part, attn_order());
   // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step;
   // PDO_ATTN_DKDV3=0 = the 2-waves-per-SIMD build of the same body (A/B alternative)
   static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 1);

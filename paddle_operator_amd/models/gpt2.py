@@ -15,8 +15,8 @@ MI355X-first rather than a transcription of any reference implementation:
   run in the fc1 / fc2 GEMM epilogues; embedding gather + position add is one
   kernel;
 * every dense projection (forward, input gradient, weight gradient, LM head)
-  runs on the hand-written gemm_nt4 / gemm_dw4 kernels; the library GEMMs are
-  only the PDO_NT_ALL=0 / PDO_HIP_DW=0 fallbacks.
+  runs on the hand-written gemm_nt4 / gemm_dw4 kernels; library GEMMs run
+  only for shapes outside their contracts.
 
 The reference operator has no model code at all; this workload
 is what a PaddleJob launches (``deploy/examples/resnet.yaml:14-19`` pattern).

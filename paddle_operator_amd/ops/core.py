@@ -153,8 +153,8 @@ _DX_TN = [True]
 # gemm_nt4 instead of hipBLASLt, where its shape contract holds (M, N % 256,
 # K % 128, or N % 256 = 128 like the 50304-column LM head).  Default since the
 # row-accumulator schedules (profiles/r3_gemm_nt4_rows.md): no hipBLASLt kernel
-# in the step.  PDO_NT_ALL=0 keeps the library for the GEMMs without a fused
-# epilogue, 1 routes all of them, any larger value routes those with K ≤ it.
+# in the step.  (Test hook: 0 keeps the library for the GEMMs without a fused
+# epilogue, 1 routes all of them, any larger value routes those with K ≤ it.)
 _NT_ALL = [1]
 
 

@@ -298,7 +298,7 @@ class _NTMLPFn(torch.autograd.Function):
 # interleaved rounds (tools/gpu.sh 'stepab:...', profiles/r3_gemm_nt4_sched.md):
 # 151.02 / 151.14 ms with hipBLASLt + bias_gelu_fwd, 150.76 / 150.79 fused.
 # (Round 2, on the one-barrier schedule, it was 0.5 ms slower: off then.)
-# PDO_NT_GELU=0 restores the library GEMM + the HIP bias-GELU kernel.
+# (Test hook: False restores the library GEMM + the HIP bias-GELU kernel.)
 _NT_GELU = [True]
 
 

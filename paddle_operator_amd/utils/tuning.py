@@ -2,7 +2,7 @@
 
 The flagship steps' GEMMs run on the hand-written gemm_nt4 / gemm_dw4 kernels;
 library GEMMs remain for shapes outside their contracts, the tiny classifier
-heads and the PDO_NT_ALL=0 / PDO_HIP_DW=0 fallbacks.  For those, instead of
+heads and the framework reference path (PDO_OPS=torch).  For those, instead of
 hipBLASLt's heuristic pick, every GEMM shape of the flagship step was benchmarked once on
 an MI355X (all hipBLASLt + rocBLAS solutions, TunableOp) and the winners are
 shipped in ``paddle_operator_amd/tuning/*.csv`` (validated against the

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Attention kernel variants A/B (GPT-2-medium shape, B=64): tools/attn_probe.py under
 # each env config (K=V[;K=V..]), 2 interleaved rounds.
-#   bash tools/attn_ab.sh 'PDO_ATTN_FWD=1' 'PDO_ATTN_FWD=5;PDO_ATTN_DQ_HOIST=1'
+#   bash tools/attn_ab.sh 'PDO_ATTN_FWDV=0;PDO_ATTN_DQV=0' 'PDO_ATTN_FWDV=3;PDO_ATTN_DQV=1'
 set -o pipefail
 for r in 1 2; do
   for cfg in "$@"; do

@@ -12,7 +12,7 @@ import torch
 import os
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tools.gemm_probe import bench  # noqa: E402
+from tools.attn_probe import bench  # noqa: E402
 from paddle_operator_amd import _native  # noqa: E402
 
 m = _native.require_hip()
