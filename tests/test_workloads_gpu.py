@@ -28,6 +28,31 @@ def test_resnet50_step_channels_last(cuda):
 
 
 @pytest.mark.gpu
+def test_resnet50_graph_replay_matches_eager(cuda, monkeypatch):
+    """The whole-step HIP graph (workloads/resnet.py _capture): 2 eager warm-up
+    steps, capture, 3 replays — same batches, same parameters, BN statistics
+    and losses as 5 eager steps (PDO_RESNET_GRAPH=0)."""
+    from paddle_operator_amd.workloads.resnet import ResNetTrainer
+
+    def run(graph):
+        monkeypatch.setenv("PDO_RESNET_GRAPH", "1" if graph else "0")
+        torch.manual_seed(0)
+        t = ResNetTrainer(16, "cuda:0")
+        assert t.graphed == graph
+        losses = [float(t.step()) for _ in range(5)]
+        torch.cuda.synchronize()
+        bufs = torch.cat([b.float().reshape(-1) for b in t.model.buffers()])
+        return t, losses, t.flat.params.clone(), bufs
+
+    te, le, pe, be = run(False)
+    tg, lg, pg, bg = run(True)
+    assert tg._graph is not None and tg.opt.step_count == te.opt.step_count == 5
+    assert all(abs(a - b) <= 2e-3 * abs(a) for a, b in zip(le, lg)), (le, lg)
+    assert float((pg - pe).norm() / pe.norm()) < 1e-4
+    assert float((bg - be).norm() / be.norm()) < 1e-4
+
+
+@pytest.mark.gpu
 def test_launcher_gpt2_single_gpu(cuda, tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, POD_IP="127.0.0.1", PADDLE_PORT="36500")
     out = subprocess.run([sys.executable, "-m", "paddle_operator_amd.launch", "--workload", "gpt2", "--tiny",
