@@ -348,9 +348,15 @@ class _ConvFn(torch.autograd.Function):
             m.conv_stride2_add(dx, cadd.contiguous(memory_format=torch.channels_last))
         if ctx.needs_input_grad[1]:
             p = ctx.wparam
+            g = None
             if ctx.one and _gemm_wgrad_1x1(C, K):
                 g = torch.empty(K, C, device=x.device, dtype=torch.bfloat16)
-                m.gemm_dw(dy.permute(0, 2, 3, 1).reshape(T, K), x.permute(0, 2, 3, 1).reshape(T, C), g, False)
+                # False: outside gemm_dw's contract (tokens not a multiple of its
+                # 64-token k-tile, e.g. 49·N at layer4 for N % 64 ≠ 0) — g unwritten
+                if not m.gemm_dw(dy.permute(0, 2, 3, 1).reshape(T, K), x.permute(0, 2, 3, 1).reshape(T, C), g,
+                                 False):
+                    g = None
+            if g is not None:
                 dw = g.view(K, C, 1, 1).to(p.dtype)
             elif (_direct_ok(p) and p.grad.dtype == torch.float32
                     and p.grad.is_contiguous(memory_format=torch.channels_last)):

@@ -160,6 +160,41 @@ def test_bottleneck_hip_conv_path_matches_framework_conv():
         assert _rel(pa.grad, pb.grad) < 3e-2, n
 
 
+def test_layer4_bottleneck_ragged_tokens_matches_framework_conv():
+    """A layer4 identity bottleneck (2048 → 512 → 2048 channels, 7×7) at 3
+    images: 147 tokens, not a multiple of gemm_dw's 64-token k-tile, so its 1×1
+    weight gradients must leave the token-major GEMM for the implicit-GEMM
+    weight gradient (the GEMM's False return was once ignored and an unwritten
+    buffer used as the gradient).  Every parameter gradient against the
+    framework's convolutions."""
+    import copy
+
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(0)
+    a = Bottleneck(2048, 512).cuda().to(memory_format=torch.channels_last)
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+    b = copy.deepcopy(a)
+    x = torch.randn(3, 2048, 7, 7, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    grads = []
+    for mod, hip_conv in ((a, True), (b, False)):
+        prev = ops._HIP_CONV[0]
+        ops._HIP_CONV[0] = hip_conv
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = mod(x)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        finally:
+            ops._HIP_CONV[0] = prev
+        grads.append({n: q.grad.clone() for n, q in mod.named_parameters()})
+    for n in grads[1]:
+        assert torch.isfinite(grads[0][n]).all(), n
+        assert _rel(grads[0][n], grads[1][n]) < 3e-2, n
+
+
 @pytest.mark.parametrize("N,C,H,K,stride", [(2, 64, 16, 64, 1), (3, 128, 7, 128, 2), (2, 128, 16, 128, 2)])
 def test_conv_dgrad_bn_partials(hip, N, C, H, K, stride):
     """The input gradient's epilogue BatchNorm partials, folded by
