@@ -945,17 +945,20 @@ static int attn_order() {
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
-  static const int v = env_int("PDO_ATTN_FWDV", 0);
+  // variant 3 (lane-mask diagonal, v_max3 chains, buffer-load staging, v_dot2
+  // row sums, packed epilogue) by default: 285.1 / 289.0 vs 302.6 / 303.1 µs
+  // for variant 0 (tools/attn_ab.sh, B64 H16 S1024, 2 interleaved rounds;
+  // variant 1 alone 290.2 / 290.3, variant 2 alone 298.2 / 300.1);
+  // PDO_ATTN_FWDV=0 is the A/B alternative
+  static const int v = env_int("PDO_ATTN_FWDV", 3);
   const int grid = B * H * (S / 128);
   const float c2 = scale * LOG2E;
   // buffer-load variants address the (b, h) slice with 31-bit byte offsets
   const bool fits = (size_t)S * 3 * H * HD * 2 < (1ull << 31);
-  switch (fits ? v : 0) {
-    case 1: attn_fwd3_d64<1><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order()); break;
-    case 2: attn_fwd3_d64<2><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order()); break;
-    case 3: attn_fwd3_d64<3><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order()); break;
-    default: attn_fwd3_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order());
-  }
+  if (fits && v == 3)
+    attn_fwd3_d64<3><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order());
+  else
+    attn_fwd3_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order());
   return 0;
 }
 
@@ -964,7 +967,9 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  static const int dqv = env_int("PDO_ATTN_DQV", 0);
+  // variant 1 by default: forward + backward 772.7 / 769.1 vs 786.9 / 784.3 µs
+  // with variant 0 (PDO_ATTN_DQV=0, the A/B alternative; tools/attn_ab.sh)
+  static const int dqv = env_int("PDO_ATTN_DQV", 1);
   const bool fits = (size_t)S * 3 * H * HD * 2 < (1ull << 31);
   if (dqv == 1 && fits)
     attn_bwd_dq_d64<1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,

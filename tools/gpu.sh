@@ -15,7 +15,8 @@
 #   'pmc:CTRS SCRIPT ARGS'  one rocprofv3 --pmc pass (CTRS joined by '+') over tools/SCRIPT
 #   step                prof of the GPT-2-medium training step (tools/train_probe.py)
 #   'stepab:C1 C2 ..'   in-process GPT-2-medium step under each env config Ci (K=V[;K=V..]),
-#                       2 interleaved rounds (STEPS, default 20)
+#                       ROUNDS (default 3) interleaved rounds of STEPS (default 20) steps
+#   'resab:C1 C2 ..'    the same for the ResNet-50 step (tools/bench_resnet.py)
 #   'soab:SCRIPT ARGS'  A/B built extensions: every ab/*.so in turn over the tree's
 #                       _pdo_hip.so, python tools/SCRIPT ARGS with each, 2 rounds; restored after
 #   env:K=V             export K=V for the following steps
@@ -73,12 +74,22 @@ run_step() {
       python3 tools/pmc_summary.py $(find "$p" -name "*.db") > "$p.md" 2>&1 && rm -rf "$p"; head -60 "$p.md" ;;
     stepab)
       local round cfg
-      for round in 1 2; do
+      for round in $(seq 1 "${ROUNDS:-3}"); do
         for cfg in "${A[@]}"; do
           ( IFS=';'; for kv in $cfg; do export "$kv"; done
             timeout -k 10 300 python tools/train_probe.py --dist --steps "${STEPS:-20}" --warmup 3 ) \
             > "$O/stepab.json" 2> "$O/stepab.err" || { tail -30 "$O/stepab.err"; return 1; }
           echo "$round [$cfg] $(tail -1 "$O/stepab.json")"
+        done
+      done ;;
+    resab)
+      local round cfg
+      for round in $(seq 1 "${ROUNDS:-3}"); do
+        for cfg in "${A[@]}"; do
+          ( IFS=';'; for kv in $cfg; do export "$kv"; done
+            timeout -k 10 300 python tools/bench_resnet.py --steps 20 --warmup 5 ) \
+            > "$O/resab.json" 2> "$O/resab.err" || { tail -30 "$O/resab.err"; return 1; }
+          echo "$round [$cfg] $(tail -1 "$O/resab.json")"
         done
       done ;;
     soab)
