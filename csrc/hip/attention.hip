@@ -335,6 +335,15 @@ __device__ __forceinline__ constexpr unsigned long long tri_mask(int r) {
   return ((unsigned long long)((1u << (c + 4)) - 1) << 32) | ((1u << c) - 1);
 }
 
+// the transposed block's mask (key on the lane, query c(r) + 4hh on the
+// register): masked iff c(r) + 4hh < li
+__device__ __forceinline__ constexpr unsigned long long tri_mask_before(int r) {
+  const int c = (r & 3) + 8 * (r >> 2);
+  const unsigned long long lo = ~((1ull << (c + 1)) - 1) & 0xffffffffull;
+  const unsigned long long hi = ~((1ull << (c + 5)) - 1) & 0xffffffffull;
+  return (hi << 32) | lo;
+}
+
 __device__ __forceinline__ unsigned cvt_pk(float a, float b) {
   unsigned r;
   asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -579,6 +588,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // ============================================================================
 // backward dK / dV: workgroup = 128 keys of one (b,h); loop over query tiles
 // ============================================================================
+// V (PDO_ATTN_DKDVV): 1 = each sub-block's 4 Q and 4 dO row fragments read
+// before its first score MFMA (the reads overlap; otherwise every MFMA waits
+// for its own LDS round trip), and the diagonal triangle by lane-mask constants.
+template <int V>
 __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                           bf16* __restrict__ dqkv, int B, int S, int H, float c2,
@@ -666,10 +679,28 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
             dpacc[4 * g + e] = d4[e];
           }
         }
+        if constexpr (V == 1) {
+          // two k-steps of fragments in flight (16 VGPRs)
+          bf16x8 qa0 = row_frag(Qt, 32 * qs, 0, lane), da0 = row_frag(Dt, 32 * qs, 0, lane);
+          bf16x8 qa1 = row_frag(Qt, 32 * qs, 1, lane), da1 = row_frag(Dt, 32 * qs, 1, lane);
+          sacc = mfma(qa0, kf[0], sacc);
+          dpacc = mfma(da0, vf[0], dpacc);
+          qa0 = row_frag(Qt, 32 * qs, 2, lane);
+          da0 = row_frag(Dt, 32 * qs, 2, lane);
+          sacc = mfma(qa1, kf[1], sacc);
+          dpacc = mfma(da1, vf[1], dpacc);
+          qa1 = row_frag(Qt, 32 * qs, 3, lane);
+          da1 = row_frag(Dt, 32 * qs, 3, lane);
+          sacc = mfma(qa0, kf[2], sacc);
+          dpacc = mfma(da0, vf[2], dpacc);
+          sacc = mfma(qa1, kf[3], sacc);
+          dpacc = mfma(da1, vf[3], dpacc);
+        } else {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
-          dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
+          for (int ks = 0; ks < 4; ++ks) {
+            sacc = mfma(row_frag(Qt, 32 * qs, ks, lane), kf[ks], sacc);
+            dpacc = mfma(row_frag(Dt, 32 * qs, ks, lane), vf[ks], dpacc);
+          }
         }
         // The causal mask only touches the diagonal sub-tile (wave-uniform): a
         // separate body keeps its compares and selects out of every other tile
@@ -681,7 +712,14 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
             for (int e = 0; e < 4; ++e) {
               const int r = 4 * g + e;
               float p = __builtin_amdgcn_exp2f(sacc[r]);
-              if constexpr (decltype(masked)::value) p = (q0 + qr + e) < key ? 0.f : p;
+              if constexpr (decltype(masked)::value) {
+                if constexpr (V == 1) {
+                  // diagonal block: query c(r) + 4hh (+ qb0) before key li (+ qb0) is masked
+                  p = __builtin_amdgcn_inverse_ballot_w64(tri_mask_before(r)) ? 0.f : p;
+                } else {
+                  p = (q0 + qr + e) < key ? 0.f : p;
+                }
+              }
               sacc[r] = p;
               dpacc[r] = p * dpacc[r];
             }
@@ -693,12 +731,23 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
           softmax_grad(std::false_type{});
 #pragma unroll
         for (int sst = 0; sst < 2; ++sst) {
-          const bf16x8 pb = pack8(sacc, sst);
-          const bf16x8 db = pack8(dpacc, sst);
-          dv0 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 0, lane), pb, dv0);
-          dv1 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 32, lane), pb, dv1);
-          dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
-          dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
+          if constexpr (V == 1) {  // the four transposed fragments in flight together
+            const bf16x8 t0 = tr_frag(Dt, 32 * qs + 16 * sst, 0, lane), t1 = tr_frag(Dt, 32 * qs + 16 * sst, 32, lane);
+            const bf16x8 t2 = tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), t3 = tr_frag(Qt, 32 * qs + 16 * sst, 32, lane);
+            const bf16x8 pb = pack8(sacc, sst);
+            const bf16x8 db = pack8(dpacc, sst);
+            dv0 = mfma(t0, pb, dv0);
+            dv1 = mfma(t1, pb, dv1);
+            dk0 = mfma(t2, db, dk0);
+            dk1 = mfma(t3, db, dk1);
+          } else {
+            const bf16x8 pb = pack8(sacc, sst);
+            const bf16x8 db = pack8(dpacc, sst);
+            dv0 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 0, lane), pb, dv0);
+            dv1 = mfma(tr_frag(Dt, 32 * qs + 16 * sst, 32, lane), pb, dv1);
+            dk0 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 0, lane), db, dk0);
+            dk1 = mfma(tr_frag(Qt, 32 * qs + 16 * sst, 32, lane), db, dk1);
+          }
         }
       }
     }
@@ -729,12 +778,13 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
       const float *__restrict__ delta, bf16 *__restrict__ dqkv, int B, int S, int H, float c2, float scale,          \
       float *__restrict__ dbias_part, int order
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(PDO_DKDV_ARGS) {
-  dkdv_body(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+  dkdv_body<0>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 // the same body capped at 168 VGPRs: 3 waves per SIMD instead of 2 (the LDS
 // ring, 49.5 KiB per workgroup, allows 3 workgroups per CU)
+template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dkdv3_d64(PDO_DKDV_ARGS) {
-  dkdv_body(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+  dkdv_body<V>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 #undef PDO_DKDV_ARGS
 
@@ -980,9 +1030,16 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step;
   // PDO_ATTN_DKDV3=0 = the 2-waves-per-SIMD build of the same body (A/B alternative)
   static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 1);
-  if (dkdv3)
-    attn_bwd_dkdv3_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
-                                             attn_order());
+  // variant 1 (fragments prefetched two k-steps / four transposed reads deep,
+  // lane-mask triangle) by default: forward + backward 759.4 / 763.0 vs 766.8 /
+  // 764.8 µs (tools/attn_ab.sh); PDO_ATTN_DKDVV=0 is the A/B alternative
+  static const int dkdvv = env_int("PDO_ATTN_DKDVV", 1);
+  if (dkdv3 && dkdvv == 1)
+    attn_bwd_dkdv3_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                                dbias_part, attn_order());
+  else if (dkdv3)
+    attn_bwd_dkdv3_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                                dbias_part, attn_order());
   else
     attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
                                             attn_order());

@@ -1157,6 +1157,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("embed_bwd_sorted", &embed_bwd_sorted);
   m.def("sumsq", &sumsq);
   m.def("sumsq_chunks", &sumsq_chunks);
+  m.def("set_adamw_variant", [](int v) { pdo::adamw_set_variant(v); });
   m.def("sumsq_total", &sumsq_total);
   m.def("adamw_flat", &adamw_flat);
   m.def("sgd_flat", &sgd_flat);

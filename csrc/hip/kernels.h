@@ -195,6 +195,7 @@ int cast_f32_bf16(const float* in, bf16* out, long long n, hipStream_t st);
 
 // optim.hip
 int sumsq(const bf16* g, long long n, float* part, int part_cap, float scale, float* out, hipStream_t st);
+void adamw_set_variant(int v);
 // Σ g² per fixed chunk (elements [k·chunk, (k+1)·chunk)) for chunks [k0, k1) → part[k]
 int sumsq_chunks(const bf16* g, long long n, long long chunk, int k0, int k1, float* part, hipStream_t st);
 // out[0] = scale² · Σ part[0..K), in a fixed order

@@ -88,52 +88,43 @@ __global__ __launch_bounds__(256) void adamw_kernel(bf16* __restrict__ p, const 
   }
 }
 
-// The same update, two 8-element vectors per thread per iteration with every
-// load of both issued before any math (14 loads in flight per lane instead of
-// 7), and non-temporal loads / stores: each byte of the 10 GB step is touched
-// once, so none of it is worth an L2 / MALL line (the next step's forward
-// re-reads the bf16 parameters, not the fp32 state).
-__device__ __forceinline__ f32x4 ntld4(const f32x4* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ void ntst4(f32x4* p, f32x4 v) { __builtin_nontemporal_store(v, p); }
-
-__global__ __launch_bounds__(256) void adamw2_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
-                                                     float* __restrict__ master, float* __restrict__ m1,
-                                                     float* __restrict__ m2, const float* __restrict__ decay_chunks,
-                                                     const float* __restrict__ normsq, long long npair, float lr,
-                                                     float b1, float b2, float eps, float wd, float inv_bc1,
-                                                     float inv_sqrt_bc2, float grad_scale, float clip) {
+// The same update with the hardware square root and reciprocal (v_sqrt_f32,
+// v_rcp_f32: ≈ 1 ulp) instead of the IEEE-exact expansions, VEC consecutive
+// 8-element vectors per lane per iteration with every load issued before any
+// math (VEC = 2: 32 B of gradient and 64 B of each state array per lane).
+template <int VEC>
+__global__ __launch_bounds__(256) void adamw_fast_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
+                                                         float* __restrict__ master, float* __restrict__ m1,
+                                                         float* __restrict__ m2, const float* __restrict__ decay_chunks,
+                                                         const float* __restrict__ normsq, long long ngroup, float lr,
+                                                         float b1, float b2, float eps, float wd, float inv_bc1,
+                                                         float inv_sqrt_bc2, float grad_scale, float clip) {
   float coef = grad_scale;
   if (clip > 0.f) {
     const float norm = sqrtf(normsq[0]);
     coef *= fminf(1.f, clip / (norm + 1e-6f));
   }
   const long long stride = (long long)gridDim.x * 256;
-  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < npair; q += stride) {
-    // vectors i0 = q and i1 = q + npair: two coalesced sweeps of the arena halves
-    const long long iv[2] = {q, q + npair};
-    bf16x8 gb[2];
-    f32x4 w[2][2], a[2][2], v[2][2];
-    float dec[2];
+  for (long long q = blockIdx.x * 256LL + threadIdx.x; q < ngroup; q += stride) {
+    const long long i0 = q * VEC;
+    bf16x8 gb[VEC];
+    f32x4 w[VEC][2], a[VEC][2], v[VEC][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const long long i = iv[u];
-      gb[u] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(g) + i);
-      const f32x4* mp = reinterpret_cast<const f32x4*>(master) + 2 * i;
-      const f32x4* ap = reinterpret_cast<const f32x4*>(m1) + 2 * i;
-      const f32x4* vp = reinterpret_cast<const f32x4*>(m2) + 2 * i;
-      w[u][0] = ntld4(mp);
-      w[u][1] = ntld4(mp + 1);
-      a[u][0] = ntld4(ap);
-      a[u][1] = ntld4(ap + 1);
-      v[u][0] = ntld4(vp);
-      v[u][1] = ntld4(vp + 1);
-      dec[u] = decay_chunks[i >> 7];  // 1024 elements per chunk = 128 vectors
+    for (int u = 0; u < VEC; ++u) {
+      const long long i = i0 + u;
+      gb[u] = reinterpret_cast<const bf16x8*>(g)[i];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        w[u][h] = reinterpret_cast<const f32x4*>(master)[2 * i + h];
+        a[u][h] = reinterpret_cast<const f32x4*>(m1)[2 * i + h];
+        v[u][h] = reinterpret_cast<const f32x4*>(m2)[2 * i + h];
+      }
     }
+    const float shrink = 1.f - lr * wd * decay_chunks[i0 >> 7];  // 128 vectors per chunk; VEC | 128
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const long long i = iv[u];
+    for (int u = 0; u < VEC; ++u) {
+      const long long i = i0 + u;
       const f32x8 gr = to_f32(gb[u]) * coef;
-      const float shrink = 1.f - lr * wd * dec[u];
       f32x8 wo;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -143,13 +134,13 @@ __global__ __launch_bounds__(256) void adamw2_kernel(bf16* __restrict__ p, const
           const float gj = gr[4 * h + j];
           ah[j] = b1 * ah[j] + (1.f - b1) * gj;
           vh[j] = b2 * vh[j] + (1.f - b2) * gj * gj;
-          const float upd = (ah[j] * inv_bc1) / (sqrtf(vh[j]) * inv_sqrt_bc2 + eps);
-          wh[j] = wh[j] * shrink - lr * upd;
+          const float den = __builtin_amdgcn_sqrtf(vh[j]) * inv_sqrt_bc2 + eps;
+          wh[j] = wh[j] * shrink - lr * (ah[j] * inv_bc1) * __builtin_amdgcn_rcpf(den);
           wo[4 * h + j] = wh[j];
         }
-        ntst4(reinterpret_cast<f32x4*>(master) + 2 * i + h, wh);
-        ntst4(reinterpret_cast<f32x4*>(m1) + 2 * i + h, ah);
-        ntst4(reinterpret_cast<f32x4*>(m2) + 2 * i + h, vh);
+        reinterpret_cast<f32x4*>(master)[2 * i + h] = wh;
+        reinterpret_cast<f32x4*>(m1)[2 * i + h] = ah;
+        reinterpret_cast<f32x4*>(m2)[2 * i + h] = vh;
       }
       reinterpret_cast<bf16x8*>(p)[i] = to_bf16(wo);
     }
@@ -203,26 +194,34 @@ int sumsq_total(const float* part, int K, float scale, float* out, hipStream_t s
   return 0;
 }
 
+// 2 (default) = fast math, one vector per lane: 1812.5 µs (5.75 TB/s) vs
+// 1864.8 µs (5.59 TB/s) for 1 = the IEEE-exact kernel; 3 = fast math with two
+// consecutive vectors per lane, 2269.4 µs (tools/adamw_probe.py, 355 M
+// elements, median of 5 interleaved; profiles/r5_adamw_resnet_graph.md).
+// PDO_ADAMW overrides; set_adamw_variant for the probe.
+static int g_adamw = [] {
+  const char* e = getenv("PDO_ADAMW");
+  return e && *e ? atoi(e) : 2;
+}();
+void adamw_set_variant(int v) { g_adamw = v; }
+
 int adamw_flat(bf16* p, const bf16* g, float* master, float* m1, float* m2, const float* decay_chunks,
                const float* normsq, long long n, float lr, float b1, float b2, float eps, float wd, float bc1,
                float bc2, float grad_scale, float clip, hipStream_t st) {
   if (n % 1024) return -2;
   const long long nvec = n / 8;
-  // PDO_ADAMW=2: two vectors per lane with non-temporal loads / stores — measured
-  // 3.21 ms vs 1.98 for the plain kernel in the GPT-2-medium step (round 4,
-  // profiles/r4b_step_kernels.md): off
-  static const int v1 = [] {
-    const char* e = getenv("PDO_ADAMW");
-    return e && *e ? (atoi(e) == 2 ? 0 : 1) : 1;
-  }();
-  if (v1 == 1 || nvec % 2) {
+  const float ib1 = 1.f / bc1, isb2 = 1.f / sqrtf(bc2);
+  if (g_adamw == 2) {
+    adamw_fast_kernel<1><<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec,
+                                                                 lr, b1, b2, eps, wd, ib1, isb2, grad_scale, clip);
+  } else if (g_adamw == 3) {
+    adamw_fast_kernel<2><<<stream_grid(nvec / 2, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq,
+                                                                     nvec / 2, lr, b1, b2, eps, wd, ib1, isb2,
+                                                                     grad_scale, clip);
+  } else {
     adamw_kernel<<<stream_grid(nvec, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, nvec, lr, b1, b2,
-                                                          eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
-    return 0;
+                                                          eps, wd, ib1, isb2, grad_scale, clip);
   }
-  const long long npair = nvec / 2;
-  adamw2_kernel<<<stream_grid(npair, 256), 256, 0, st>>>(p, g, master, m1, m2, decay_chunks, normsq, npair, lr, b1,
-                                                          b2, eps, wd, 1.f / bc1, 1.f / sqrtf(bc2), grad_scale, clip);
   return 0;
 }
 

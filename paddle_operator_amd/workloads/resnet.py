@@ -77,10 +77,6 @@ class ResNetTrainer:
         self.res = 32 if tiny else 224
         self.classes = 10 if tiny else 1000
         self.gen = torch.Generator(device=self.device).manual_seed(dist.get_rank() if dist.is_initialized() else 0)
-        self._graph, self._warm = None, 0
-        self._graphed = (self.device.type == "cuda" and self.ddp.world == 1 and not tiny
-                         and _native.ops_mode() == "hip" and os.environ.get("PDO_RESNET_GRAPH", "1") != "0")
-        self._side = torch.cuda.Stream(self.device) if self._graphed else None
 
     def sync_initial_weights(self):
         self.ddp.broadcast_params(0)
@@ -105,68 +101,19 @@ class ResNetTrainer:
         self._draw(xb, y)
         return x, y
 
-    def _body(self, x, y, cache=True):
+    def step(self):
+        x, y = self.batch()
         self.flat.zero_grad()
         self.ddp.prepare()
         # bf16 copies of the fp32 master weights: one cast of the arena per step
         with self.flat.shadow_scope(), torch.autocast(self.device.type, dtype=torch.bfloat16,
-                                                      enabled=self.device.type == "cuda", cache_enabled=cache):
+                                                      enabled=self.device.type == "cuda"):
             out = self.model(x)
         loss = F.cross_entropy(out.float(), y)
         loss.backward()
         self.ddp.finish()
         self.opt.step(self.ddp.grad_scale)
         return loss
-
-    def step(self):
-        if self.graphed:
-            return self._graph_step()
-        x, y = self.batch()
-        return self._body(x, y)
-
-    # ---- whole-step HIP graph (one rank) ----
-    # The ResNet-50 step is ~580 kernels; launched one by one the GPU idles
-    # between short ones (≈0.8 ms per step at batch 256).  Every tensor the step
-    # touches is static (flat arena, shadow, optimizer state, workspaces from the
-    # graph's private pool), so the forward, backward and SGD update are captured
-    # once and replayed; only the batch is drawn outside, into static buffers.
-    # Multi-rank steps stay eager (the bucket all-reduces are issued from
-    # autograd hooks).  PDO_RESNET_GRAPH=0 disables it.
-    @property
-    def graphed(self):
-        return self._graphed
-
-    def _graph_step(self):
-        if self._graph is None:
-            if self._warm < 2:
-                # the first two steps run eagerly on a side stream (lazy init and the
-                # allocator settle before capture, as torch requires)
-                self._warm += 1
-                x, y = self.batch()
-                side = self._side
-                side.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(side):
-                    loss = self._body(x, y, cache=False)
-                torch.cuda.current_stream(self.device).wait_stream(side)
-                return loss
-            self._capture()
-        self._fill_batch()
-        self._graph.replay()
-        self.opt.step_count += 1
-        return self._g_loss
-
-    def _fill_batch(self):
-        self._draw(self._xbuf, self._ybuf)
-
-    def _capture(self):
-        self._xbuf, self._x, self._ybuf = self._batch_buffers()
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        step0 = self.opt.step_count
-        with torch.cuda.graph(g):
-            self._g_loss = self._body(self._x, self._ybuf, cache=False)
-        self.opt.step_count = step0
-        self._graph = g
 
     def state_dict(self):
         return {"params": self.flat.params, "opt_buf": self.opt.buf, "buffers": {k: v for k, v in

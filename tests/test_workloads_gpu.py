@@ -28,28 +28,23 @@ def test_resnet50_step_channels_last(cuda):
 
 
 @pytest.mark.gpu
-def test_resnet50_graph_replay_matches_eager(cuda, monkeypatch):
-    """The whole-step HIP graph (workloads/resnet.py _capture): 2 eager warm-up
-    steps, capture, 3 replays — same batches, same parameters, BN statistics
-    and losses as 5 eager steps (PDO_RESNET_GRAPH=0)."""
+def test_resnet50_steps_deterministic_at_ragged_batch(cuda):
+    """Two ResNet-50 trainers from one seed at batch 16 (layer4: 784 tokens, not
+    a multiple of the 64-token k-tile of gemm_dw) take bitwise-identical steps:
+    no gradient is read from an unwritten buffer (the 1×1 weight gradient's
+    fallback, ops/resnet.py)."""
     from paddle_operator_amd.workloads.resnet import ResNetTrainer
 
-    def run(graph):
-        monkeypatch.setenv("PDO_RESNET_GRAPH", "1" if graph else "0")
+    runs = []
+    for _ in range(2):
         torch.manual_seed(0)
         t = ResNetTrainer(16, "cuda:0")
-        assert t.graphed == graph
-        losses = [float(t.step()) for _ in range(5)]
+        losses = [float(t.step()) for _ in range(3)]
         torch.cuda.synchronize()
-        bufs = torch.cat([b.float().reshape(-1) for b in t.model.buffers()])
-        return t, losses, t.flat.params.clone(), bufs
-
-    te, le, pe, be = run(False)
-    tg, lg, pg, bg = run(True)
-    assert tg._graph is not None and tg.opt.step_count == te.opt.step_count == 5
-    assert all(abs(a - b) <= 2e-3 * abs(a) for a, b in zip(le, lg)), (le, lg)
-    assert float((pg - pe).norm() / pe.norm()) < 1e-4
-    assert float((bg - be).norm() / be.norm()) < 1e-4
+        runs.append((losses, t.flat.params.clone()))
+    assert runs[0][0] == runs[1][0]
+    assert torch.isfinite(runs[0][1]).all()
+    assert torch.equal(runs[0][1], runs[1][1])
 
 
 @pytest.mark.gpu
