@@ -988,6 +988,12 @@ static int env_int(const char* k, int def) {
   const char* e = getenv(k);
   return e && *e ? atoi(e) : def;
 }
+// Heaviest-first order by default.  The XCD-grouped order cuts the kernels'
+// L2 misses 2-3× (forward TCC_EA0_RDREQ 3.1e6 vs 1.05e7 per call) and wins
+// the isolated microbenchmark (backward 761 / 754 vs 775 / 777 µs), but loses
+// in the GPT-2-medium step: 144.20 / 144.02 / 144.19 vs 143.88 / 143.78 /
+// 143.81 ms (stepab, round 5) — its last workgroups end unevenly.  4-wave-
+// per-SIMD builds of the forward and dQ spilled and ran 401 / 1068 µs (removed).
 static int attn_order() {
   static const int o = env_int("PDO_ATTN_ORDER", 0);
   return o;
