@@ -10,6 +10,8 @@
 // registers, dlogits written in the forward — 4.6 ms vs these two passes'
 // 3.6 ms at [65536, 50304]: with ≤ 1 resident 50k-column row per CU the load,
 // reduce and store phases serialise.)
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -221,6 +223,77 @@ __global__ __launch_bounds__(256) void xent_fused_kernel(bf16* __restrict__ logi
   for (; i < nv; i += 256) grad(lv[i], i);
 }
 
+// The same row pass with the row held in registers: 512 threads × RV vectors
+// of 8 (RV = 13: rows of up to 53,248 columns, GPT-2's 50,304) — the logits
+// are read from HBM once instead of twice (statistics pass, then the dlogits
+// pass re-reading them), and the row max comes first so each element takes one
+// exp for the sum and one for its gradient (no running rescale).
+template <int RV>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void xent_fused_reg_kernel(bf16* __restrict__ logits,
+                                                             const int64_t* __restrict__ tgt,
+                                                             const float* __restrict__ inv_cnt,
+                                                             float* __restrict__ row_loss, int Vp, int V) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  bf16x8* lv = reinterpret_cast<bf16x8*>(logits + (size_t)row * Vp);
+  const int nv = Vp >> 3;
+  bf16x8 r[RV];
+#pragma unroll
+  for (int k = 0; k < RV; ++k) {
+    const int i = threadIdx.x + 512 * k;
+    if (i < nv) r[k] = lv[i];
+  }
+  const int64_t t = tgt[row];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < RV; ++k) {
+    const int i = threadIdx.x + 512 * k;
+    if (i < nv) {
+      const f32x8 v = to_f32(r[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (8 * i + j < V) m = fmaxf(m, v[j]);
+    }
+  }
+  const float M = block_max<8>(m, red);
+  float s = 0.f, tl = 0.f;
+#pragma unroll
+  for (int k = 0; k < RV; ++k) {
+    const int i = threadIdx.x + 512 * k;
+    if (i < nv) {
+      const f32x8 v = to_f32(r[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * i + j;
+        if (c < V) s += __expf(v[j] - M);
+        if (c == t) tl = v[j];
+      }
+    }
+  }
+  const float S = block_sum<8>(s, red);
+  const float T = block_sum<8>(tl, red);  // the target logit (one lane holds it)
+  const float L = M + __logf(S);
+  const bool valid = t >= 0 && t < V;
+  if (threadIdx.x == 0) row_loss[row] = valid ? L - T : 0.f;
+  const float scale = valid ? inv_cnt[0] : 0.f;
+#pragma unroll
+  for (int k = 0; k < RV; ++k) {
+    const int i = threadIdx.x + 512 * k;
+    if (i < nv) {
+      const f32x8 v = to_f32(r[k]);
+      f32x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * i + j;
+        float p = c < V ? __expf(v[j] - L) : 0.f;
+        if (c == t) p -= 1.f;
+        o[j] = p * scale;
+      }
+      lv[i] = to_bf16(o);
+    }
+  }
+}
+
 // loss = Σ row_loss · inv_cnt
 __global__ __launch_bounds__(1024) void xent_sum_kernel(const float* __restrict__ row_loss, int N,
                                                         const float* __restrict__ inv_cnt, float* __restrict__ loss) {
@@ -234,7 +307,15 @@ __global__ __launch_bounds__(1024) void xent_sum_kernel(const float* __restrict_
 int xent_fused(bf16* logits, const int64_t* tgt, const float* inv_cnt, float* row_loss, float* loss, int N, int Vp,
                int V, hipStream_t st) {
   if (Vp % 8) return -2;
-  xent_fused_kernel<<<N, 256, 0, st>>>(logits, tgt, inv_cnt, row_loss, Vp, V);
+  // register-resident rows where they fit (PDO_XENT_REG=0: the two-read kernel, A/B)
+  static const bool reg = [] {
+    const char* e = getenv("PDO_XENT_REG");
+    return !(e && *e == '0');
+  }();
+  if (reg && Vp / 8 <= 512 * 13)
+    xent_fused_reg_kernel<13><<<N, 512, 0, st>>>(logits, tgt, inv_cnt, row_loss, Vp, V);
+  else
+    xent_fused_kernel<<<N, 256, 0, st>>>(logits, tgt, inv_cnt, row_loss, Vp, V);
   xent_sum_kernel<<<1, 1024, 0, st>>>(row_loss, N, inv_cnt, loss);
   return 0;
 }
