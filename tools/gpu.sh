@@ -64,7 +64,8 @@ run_step() {
         > "$O/$tag.log" 2>&1 || { tail -30 "$O/$tag.log"; return 1; }
       local db; db=$(find "$d" -name '*.db' | head -1)
       local steps=0; [[ $kind == step ]] && steps=9  # 2 warmup + 7 timed steps are all traced; 0 = count AdamW dispatches
-      python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/$tag.md" && rm -rf "$d"
+      python3 tools/prof_summary.py "$db" --steps $steps --top 40 > "$O/$tag.md" &&
+        { [[ $kind != step ]] || python3 tools/prof_sequence.py "$db" --last 800 --list > "$O/$tag.seq.md"; } && rm -rf "$d"
       tail -5 "$O/$tag.log"; head -45 "$O/$tag.md" ;;
     pmc)
       PMC_PASS=$((PMC_PASS + 1))
