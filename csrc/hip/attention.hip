@@ -777,8 +777,9 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
   const bf16 *__restrict__ qkv, const bf16 *__restrict__ dout, const float *__restrict__ lse,                        \
       const float *__restrict__ delta, bf16 *__restrict__ dqkv, int B, int S, int H, float c2, float scale,          \
       float *__restrict__ dbias_part, int order
+template <int V>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(PDO_DKDV_ARGS) {
-  dkdv_body<0>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
+  dkdv_body<V>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 // the same body capped at 168 VGPRs: 3 waves per SIMD instead of 2 (the LDS
 // ring, 49.5 KiB per workgroup, allows 3 workgroups per CU)
@@ -1046,9 +1047,12 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   else if (dkdv3)
     attn_bwd_dkdv3_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                                 dbias_part, attn_order());
+  else if (dkdvv == 1)
+    attn_bwd_dkdv_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                               dbias_part, attn_order());
   else
-    attn_bwd_dkdv_d64<<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale, dbias_part,
-                                            attn_order());
+    attn_bwd_dkdv_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                               dbias_part, attn_order());
   return 0;
 }
 
