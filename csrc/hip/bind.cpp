@@ -476,22 +476,26 @@ at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r, c10::optional<a
   return c;
 }
 
-// (pre, y): pre = a·bᵀ, y = gelu(pre + bias)
-std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias) {
+// (pre, y): pre = a·bᵀ, y = gelu(pre + bias); saved_grad: pre = gelu'(a·bᵀ + bias)
+// instead (EPI 7, for gemm_nt_dgelu(..., saved_grad=true))
+std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias, bool saved_grad) {
   nt_check(a, b);
   CHECK_IN(bias); CHECK_BF16(bias);
   const int M = a.size(0), N = b.size(0), K = a.size(1);
   TORCH_CHECK(bias.numel() == N);
   auto pre = at::empty({M, N}, a.options());
   auto y = at::empty({M, N}, a.options());
-  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(pre), N, 2, bp(bias), bp(y), N, nullptr, cur_stream()),
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(pre), N, saved_grad ? 7 : 2, bp(bias), bp(y), N, nullptr,
+                        cur_stream()),
            "gemm_nt_gelu");
   return {pre, y};
 }
 
-// dx = (a·bᵀ) ⊙ gelu'(pre + bias); db = colsum(dx) (accumulated into db_out when given)
+// dx = (a·bᵀ) ⊙ gelu'(pre + bias); db = colsum(dx) (accumulated into db_out when given).
+// saved_grad: pre is gemm_nt_gelu(..., saved_grad=true)'s gelu' and dx = (a·bᵀ) ⊙ pre
+// (EPI 8; bias unused)
 std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre, at::Tensor bias,
-                                      c10::optional<at::Tensor> db_out) {
+                                      c10::optional<at::Tensor> db_out, bool saved_grad) {
   nt_check(a, b);
   CHECK_IN(pre); CHECK_IN(bias); CHECK_BF16(pre); CHECK_BF16(bias);
   const int M = a.size(0), N = b.size(0), K = a.size(1);
@@ -499,7 +503,8 @@ std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre
   auto dx = at::empty({M, N}, a.options());
   const int G = pdo::gemm_nt_dbias_rows(M);
   auto part = at::empty({(int64_t)G * N + pdo::colsum_scratch_floats(G, N)}, a.options().dtype(at::kFloat));
-  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(dx), N, 3, bp(bias), bp(pre), N, fp(part), cur_stream()),
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(dx), N, saved_grad ? 8 : 3, bp(bias), bp(pre), N, fp(part),
+                        cur_stream()),
            "gemm_nt_dgelu");
   at::Tensor db;
   pdo::ColOut co;
@@ -1183,9 +1188,9 @@ PYBIND11_MODULE(_pdo_hip, m) {
     return prev;
   }, py::arg("impl") = -1, "select gemm_nt's mainloop (0 = 8-wave ring, 1 = 4-wave); returns the previous");
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("out") = py::none());
-  m.def("gemm_nt_gelu", &gemm_nt_gelu);
+  m.def("gemm_nt_gelu", &gemm_nt_gelu, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("saved_grad") = false);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),
-        py::arg("db_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("saved_grad") = false);
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_fwd_tiles", &bn_act_fwd_tiles);
   m.def("conv_ok", &conv_ok);

@@ -129,6 +129,18 @@ __device__ __forceinline__ f32x2 gelu_sig_grad2(f32x2 x, f32x2 m1) {
   return pk_fma(sg, q, sg);
 }
 
+// gelu(x) and gelu'(x) together (the shared t, z, s computed once): the fc1
+// forward epilogue stores gelu' for fc2's input-gradient epilogue, which then
+// needs one multiply per element instead of the whole derivative
+__device__ __forceinline__ void gelu_and_grad2(f32x2 x, f32x2 m1, f32x2& y, f32x2& g) {
+  const f32x2 t = x * x;
+  const f32x2 z = x * pk_fma(t, f32x2(-2.f * GK0 * GK1 * GL2E), f32x2(-2.f * GK0 * GL2E));
+  const f32x2 sg = rcp_2(exp2_2(z) + 1.f);
+  y = x * sg;
+  const f32x2 w = pk_fma(t, f32x2(6.f * GK0 * GK1), f32x2(2.f * GK0));
+  g = pk_fma(y * w, pk_fma(sg, m1, -m1), sg);  // s + y·2u'·(1 - s), y = x·s
+}
+
 // number of workgroups for a grid-stride memory-bound kernel (256 CUs × 8)
 inline int stream_grid(long long work_items, int per_block) {
   long long g = (work_items + per_block - 1) / per_block;

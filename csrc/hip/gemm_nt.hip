@@ -27,7 +27,12 @@
 //              GEMM with the bias-GELU backward pass fused
 //   EPI_ADD    C = A·Bᵀ + Y (EPI 5: + bias too — a projection writing the residual
 //              stream x + proj(a) + b) — or an input gradient that joins another branch's
-//              (ResNet's block input: conv1 dX + the identity / downsample dX)
+//              (ResNet's block input: conv1 dX + the identity / downsample dX);
+//              EPI 6: + Y ⊙ keep bits (a ReLU mask)
+//   EPI 7 / 8  (4-wave mainloop only) the GELU pair with the derivative saved:
+//              fc1 writes C = gelu'(A·Bᵀ + bias), Y = gelu(A·Bᵀ + bias); fc2's
+//              input gradient is then C = (A·Bᵀ) ⊙ Y plus the bias-gradient
+//              partials — one multiply per element instead of the derivative
 // Rounding matches the unfused path bit for bit: the GEMM result is rounded to
 // bf16 before the activation math, as when it made an HBM round trip.
 #include <stdlib.h>
@@ -266,10 +271,11 @@ int gemm_nt_get_impl() { return g_impl; }
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st) {
   if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
-  if (((epi >= 1 && epi <= 3) || epi >= 5) && !bias) return -3;  // EPI 6: bias = the addend's keep mask
+  if (((epi >= 1 && epi <= 3) || (epi >= 5 && epi <= 7)) && !bias) return -3;  // EPI 6: bias = the addend's keep mask
   if (epi == 6 && ldy % 8) return -3;
   if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
-  if (epi == 3 && !dbias_part) return -3;
+  if ((epi == 3 || epi == 8) && !dbias_part) return -3;
+  if (epi >= 7 && !nt4_path(K)) return -4;  // the saved-GELU' pair exists on the 4-wave mainloop only
   if (nt4_path(K))
     return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st);
   const long long grid = (long long)(M / BM) * (N / BN);

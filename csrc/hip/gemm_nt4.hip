@@ -217,9 +217,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const int g4 = lane >> 4;
     const int nb = n0 + wn * 128 + 8 * (lane & 15);
     const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
-    bf16x8 pre[EPI >= 3 ? 32 : 1];  // EPI 3: the GELU pre-activation; EPI 4 / 5 / 6: the addend
+    // EPI 3: the GELU pre-activation; EPI 4 / 5 / 6: the addend; EPI 8: the saved GELU'
+    constexpr bool PRE = EPI >= 3 && EPI != 7;
+    bf16x8 pre[PRE ? 32 : 1];
     unsigned char mk[EPI == 6 ? 32 : 1];  // EPI 6: the addend's keep bits (8 columns per byte)
-    if constexpr (EPI >= 3) {
+    if constexpr (PRE) {
 #pragma unroll
       for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
     }
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       for (int u = 0; u < 32; ++u) mk[u] = mask[((mr + 16 * (u >> 2) + (u & 3)) * ldy + nb) >> 3];
     }
     f32x8 bv8 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if constexpr ((EPI >= 1 && EPI <= 3) || EPI == 5) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
+    if constexpr ((EPI >= 1 && EPI <= 3) || EPI == 5 || EPI == 7) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + nb));
     f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     f32x2 m1 = {-1.f, -1.f};
     asm volatile("" : "+v"(m1));
@@ -260,6 +262,27 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
             y[q + 1] = gg[1];
           }
           st16(Y + m * ldy + nb, to_bf16(y));
+        } else if constexpr (EPI == 7) {
+          // fc1 with the derivative saved instead of the pre-activation: C =
+          // gelu'(x), Y = gelu(x), x = the fp32 product + bias
+          const f32x8 x = v + bv8;
+          f32x8 y, g;
+#pragma unroll
+          for (int q = 0; q < 8; q += 2) {
+            f32x2 yy, gg;
+            gelu_and_grad2(f32x2{x[q], x[q + 1]}, m1, yy, gg);
+            y[q] = yy[0];
+            y[q + 1] = yy[1];
+            g[q] = gg[0];
+            g[q + 1] = gg[1];
+          }
+          st16(crow, to_bf16(g));
+          st16(Y + m * ldy + nb, to_bf16(y));
+        } else if constexpr (EPI == 8) {
+          // fc2's input gradient against the saved GELU': C = (A·Bᵀ) ⊙ Y, + bias-gradient partials
+          const f32x8 d = v * to_f32(pre[4 * i + e]);
+          colp += d;
+          st16(crow, to_bf16(d));
         } else if constexpr (EPI == 4) {
           st16(crow, to_bf16(v + to_f32(pre[4 * i + e])));  // C = A·Bᵀ + Y, one rounding
         } else if constexpr (EPI == 5) {
@@ -286,7 +309,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         }
       }
     }
-    if constexpr (EPI == 3) {
+    if constexpr (EPI == 3 || EPI == 8) {
       // partial row 4·wm + (l >> 4) of this M-tile's 8: the rows 16i + 4(l >> 4) + e
       float* prow = dbias_part + (size_t)(8 * tm + 4 * wm + g4) * N + nb;
       *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
@@ -472,6 +495,8 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
       case 4: return go(gemm_nt4_kernel<4, MI>);
       case 5: return go(gemm_nt4_kernel<5, MI>);
       case 6: return go(gemm_nt4_kernel<6, MI>);
+      case 7: return go(gemm_nt4_kernel<7, MI>);
+      case 8: return go(gemm_nt4_kernel<8, MI>);
       default: return -4;
     }
   };

@@ -14,8 +14,8 @@ from .core import (  # noqa: F401
     _weight_grad_lib, _workspace, deferred_reductions, flush_deferred, linear, ref_attention, ref_bias_gelu,
     ref_cross_entropy, ref_layer_norm, transpose, use_hip)
 from .gpt2 import (  # noqa: F401
-    _LMHeadXentFn, _LM_CHUNK, _QKV_FUSED, _RES_EPI, _XENT_FUSED, _NT_GELU, _NT_DGELU, add_layer_norm, attention, bias_gelu,
-    cross_entropy, embedding, layer_norm, linear_add_layer_norm, lm_head_xent, mlp, mlp_add_layer_norm,
+    _LMHeadXentFn, _LM_CHUNK, _QKV_FUSED, _RES_EPI, _XENT_FUSED, _NT_GELU, _NT_DGELU, _NT_GD, add_layer_norm,
+    attention, bias_gelu, cross_entropy, embedding, layer_norm, linear_add_layer_norm, lm_head_xent, mlp, mlp_add_layer_norm,
     qkv_attention)
 from .resnet import (  # noqa: F401
     _BNLink, _BNReluPoolFn, _CompactGradLink, _ResMaskLink, _StemFn, _BN_FUSED, _BN_LINK, _BN_LINK_USED, _DS_COMPACT, _DS_COMPACT_USED, _HIP_CONV, _HIP_STEM, _RES_MASK,

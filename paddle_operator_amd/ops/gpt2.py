@@ -256,6 +256,11 @@ class _NTMLPFn(torch.autograd.Function):
     1×MI355X: 598.7 µs vs 644.5 µs for hipBLASLt + bias_gelu_fwd
     (tools/nt4_probe.py fc1_fwd, profiles/r2_gemm_nt4.md).
 
+    With ``_NT_GD`` (default) the fc1 epilogue stores gelu'(hp + b1) instead of
+    hp (EPI 7: the derivative shares the GELU's exp2 / rcp) and fc2's input
+    gradient is one multiply per element (EPI 8) instead of recomputing the
+    derivative with the matrix pipe idle.
+
     ``res``/``b2`` (optional): the fc2 GEMM also adds its bias and the residual
     stream in the epilogue (gemm_nt4 EPI 5), returning x_res + m + b2 for a
     one-input LayerNorm (_LNResFn, which takes b2's gradient); the residual's
@@ -265,7 +270,8 @@ class _NTMLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2=None, res=None):
         m = _native.require_hip()
         x2 = x.reshape(-1, x.shape[-1])
-        hp, h = m.gemm_nt_gelu(x2, w1, b1)
+        ctx.saved_grad = _NT_GD[0]
+        hp, h = m.gemm_nt_gelu(x2, w1, b1, saved_grad=ctx.saved_grad)  # hp = gelu'(x·W1ᵀ + b1) when saved_grad
         ctx.save_for_backward(x2, w1, hp, h, w2)
         ctx.b1 = b1
         ctx.shape = x.shape
@@ -283,11 +289,11 @@ class _NTMLPFn(torch.autograd.Function):
         dw2 = _weight_grad(w2, dy2, h) if ctx.needs_input_grad[3] else None
         gd = _arena_grads((b1,))
         if gd is not None:
-            (dhp,) = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1, db_out=gd[0])
+            (dhp,) = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1, db_out=gd[0], saved_grad=ctx.saved_grad)
             _signal_ready((b1,))
             db1 = None
         else:
-            dhp, db1 = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1)
+            dhp, db1 = m.gemm_nt_dgelu(dy2, transpose(w2), hp, b1, saved_grad=ctx.saved_grad)
         dw1 = _weight_grad(w1, dhp, x2) if ctx.needs_input_grad[1] else None  # its bucket can go first
         dx = _input_grad(dhp, w1).view(ctx.shape) if ctx.needs_input_grad[0] else None
         return dx, dw1, db1, dw2, None, (dy if ctx.res else None)
@@ -305,6 +311,10 @@ _NT_GELU = [True]
 # fc2 input gradient with the fused GELU' epilogue (gemm_nt) where its shape
 # contract holds; PDO_NT_DGELU=0 restores hipBLASLt + the bias-GELU kernel.
 _NT_DGELU = [True]
+
+# _NTMLPFn saves gelu' from the fc1 epilogue (EPI 7 / 8) instead of the
+# pre-activation; PDO_NT_GD=0 = the recomputing pair (EPI 2 / 3), the A/B alternative
+_NT_GD = [os.environ.get("PDO_NT_GD", "1") != "0"]
 
 
 def _nt_dgelu_ok(hp, w2) -> bool:

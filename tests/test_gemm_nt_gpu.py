@@ -205,3 +205,32 @@ def test_nt4_fused_epilogues_many_tiles_vs_fp32(hip, impl, M, N):
     # per-row differences of 2^-9 |dy| add up like √M over the column
     torch.testing.assert_close(db.float(), xp.grad.sum(0), rtol=2e-2, atol=0.5 * (M / 16384) ** 0.5)
 
+
+
+@pytest.mark.parametrize("M,N,K", [(65536, 4096, 1024), (4352, 2048, 1024), (768, 640, 512)])
+def test_nt4_saved_gelu_grad_pair_vs_fp32(hip, M, N, K):
+    """EPI 7 / 8: fc1 stores gelu'(x) (x = A·Bᵀ + bias in fp32) next to gelu(x);
+    fc2's input gradient multiplies its fp32 product by the saved bf16 gelu' and
+    sums the bias gradient.  Against fp32 (autograd of F.gelu on the exact
+    pre-activation), at the GPT-2-medium shape, an uneven persistent grid and a
+    half-width last tile column."""
+    g = torch.Generator(device="cuda").manual_seed(31)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    w1 = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
+    b1 = torch.empty(N, device="cuda", dtype=torch.bfloat16).uniform_(-0.1, 0.1, generator=g)
+    dy = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    w2t = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
+    gd, y = hip.gemm_nt_gelu(a, w1, b1, saved_grad=True)
+    x = (a.float() @ w1.float().t() + b1.float()).requires_grad_(True)
+    gl = F.gelu(x, approximate="tanh")
+    (gref,) = torch.autograd.grad(gl.sum(), x)
+    assert bool(((y.float() - gl).abs() <= 1e-2 + 8e-3 * gl.abs()).all())
+    assert bool(((gd.float() - gref).abs() <= 1e-2 + 8e-3 * gref.abs()).all())
+    dx, db = hip.gemm_nt_dgelu(dy, w2t, gd, b1, saved_grad=True)
+    ref = (dy.float() @ w2t.float().t()) * gref
+    assert bool(((dx.float() - ref).abs() <= 2e-2 + 1.6e-2 * ref.abs()).all())
+    torch.testing.assert_close(db.float(), ref.sum(0), rtol=2e-2, atol=0.5 * (M / 16384) ** 0.5)
+    acc = torch.ones(N, device="cuda", dtype=torch.bfloat16)
+    (dx2,) = hip.gemm_nt_dgelu(dy, w2t, gd, b1, db_out=acc, saved_grad=True)
+    assert torch.equal(dx2, dx)
+    torch.testing.assert_close(acc.float(), 1.0 + ref.sum(0), rtol=2e-2, atol=0.5 * (M / 16384) ** 0.5 + 0.01)

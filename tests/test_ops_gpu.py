@@ -613,11 +613,13 @@ def test_qkv_attention_fused_bias_grad(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nt_gelu", [True, False])
-def test_mlp_nt_dgelu_matches_unfused(cuda, nt_gelu):
-    """gemm_nt epilogues in the MLP — fc1 GELU forward (_NTMLPFn) and/or fc2's input
-    gradient ⊙ GELU' — == hipBLASLt + the bias-GELU kernels (output and every gradient)."""
+@pytest.mark.parametrize("nt_gelu,saved_grad", [(True, True), (True, False), (False, False)])
+def test_mlp_nt_dgelu_matches_unfused(cuda, nt_gelu, saved_grad):
+    """gemm_nt epilogues in the MLP — fc1 GELU forward (_NTMLPFn, saving gelu' or
+    the pre-activation) and/or fc2's input gradient ⊙ GELU' — == hipBLASLt + the
+    bias-GELU kernels (output and every gradient)."""
     ops = _ops()
+    ops._NT_GD[0] = saved_grad
     T, C = 4096, 512
     g = torch.Generator(device=cuda).manual_seed(5)
     base = [(0.05 * torch.randn(T, C, device=cuda, generator=g)).bfloat16() * 20,
@@ -636,6 +638,7 @@ def test_mlp_nt_dgelu_matches_unfused(cuda, nt_gelu):
         finally:
             ops._NT_DGELU[0] = True
             ops._NT_GELU[0] = True
+            ops._NT_GD[0] = True
         outs.append(y.detach().float())
         grads.append([t.grad.float() for t in ts])
     assert rel_err(outs[0], outs[1]) < 1e-2, "y"

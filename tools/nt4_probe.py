@@ -50,7 +50,8 @@ def main():
     shapes = [("qkv_fwd", 3 * C, C, "bias"), ("proj_fwd", C, C, "plain"), ("fc1_fwd", 4 * C, C, "gelu"),
               ("fc2_fwd", C, 4 * C, "plain"), ("qkv_dx", C, 3 * C, "plain"), ("proj_dx", C, C, "plain"),
               ("fc1_dx", C, 4 * C, "plain"), ("fc2_dx", 4 * C, C, "dgelu"), ("lm_dx", C, 50304, "plain"),
-              ("wide_plain", 4 * C, C, "plain")]  # fc1_fwd / fc2_dx GEMM without an epilogue
+              ("wide_plain", 4 * C, C, "plain"),  # fc1_fwd / fc2_dx GEMM without an epilogue
+              ("fc1_gd", 4 * C, C, "gelu_gd"), ("fc2_dx_gd", 4 * C, C, "dgelu_gd")]  # the saved-GELU' pair
     if a.shapes:
         keep = set(a.shapes.split(","))
         shapes = [s for s in shapes if s[0] in keep]
@@ -65,6 +66,12 @@ def main():
         elif epi == "gelu":
             ours = lambda: m.gemm_nt_gelu(x, w, b)  # noqa: E731
             lib = lambda: m.bias_gelu_fwd(F.linear(x, w), b)  # noqa: E731
+        elif epi == "gelu_gd":
+            ours = lambda: m.gemm_nt_gelu(x, w, b, saved_grad=True)  # noqa: E731
+            lib = lambda: m.bias_gelu_fwd(F.linear(x, w), b)  # noqa: E731
+        elif epi == "dgelu_gd":
+            ours = lambda: m.gemm_nt_dgelu(x, w, pre, b, saved_grad=True)  # noqa: E731
+            lib = lambda: F.linear(x, w) * pre  # noqa: E731
         else:
             ours = lambda: m.gemm_nt_dgelu(x, w, pre, b)  # noqa: E731
             lib = lambda: m.bias_gelu_bwd(F.linear(x, w), pre, b)  # noqa: E731
