@@ -334,16 +334,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
 // block per 8 channels, 256 tile lanes each reading the 8 channels as one
 // 32-B vector (G = 3 136 tiles at ResNet's 56 × 56 × 64: 13 per lane).  Two
 // plain reductions (no sequential merge): mean = Σ sum_i / M, then
-// M2 = Σ (M2_i + n_i·(mean_i − mean)²); both through an in-order LDS tree.
-__device__ __forceinline__ f32x8 tree_sum256(f32x8 v, f32x8* red) {
-  red[threadIdx.x] = v;
-  __syncthreads();
+// M2 = Σ (M2_i + n_i·(mean_i − mean)²); both by wave butterflies + one LDS
+// exchange (block_sum256) instead of an 8-level LDS tree.
+// a block-wide f32x8 sum by wave butterflies and one LDS exchange of the 4 wave totals
+// (fixed order: deterministic); red = 4 vectors of LDS
+__device__ __forceinline__ f32x8 block_sum256(f32x8 v, f32x8* red) {
 #pragma unroll
-  for (int h = 128; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-    __syncthreads();
-  }
-  const f32x8 t = red[0];
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += __shfl_xor(v[k], o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const f32x8 t = (red[0] + red[1]) + (red[2] + red[3]);
   __syncthreads();
   return t;
 }
@@ -357,18 +359,27 @@ __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __r
                                                                 float* __restrict__ invstd_out,
                                                                 float* __restrict__ ss) {
   const int c = blockIdx.x * 8;
-  __shared__ f32x8 red[256];
-  f32x8 s = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int i = threadIdx.x; i < G; i += 256) s += *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + c);
-  const f32x8 mean = tree_sum256(s, red) * (1.f / (float)M);
-  f32x8 q = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int i = threadIdx.x; i < G; i += 256) {
+  __shared__ f32x8 red[4];
+  const f32x8 z = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // 4 partial rows in flight per lane (the loop is latency-bound: G / 256 ≈
+  // 1-13 rows per lane at ResNet-50's shapes)
+  auto row = [&](int i, int off) { return i < G ? *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + off + c) : z; };
+  f32x8 s = z;
+  for (int i = threadIdx.x; i < G; i += 1024) {
+    const f32x8 a0 = row(i, 0), a1 = row(i + 256, 0), a2 = row(i + 512, 0), a3 = row(i + 768, 0);
+    s += (a0 + a1) + (a2 + a3);
+  }
+  const f32x8 mean = block_sum256(s, red) * (1.f / (float)M);
+  auto dev = [&](int i) {  // M2_i + n_i·(mean_i − mean)² of partial row i (0 past G)
+    if (i >= G) return z;
     const long long r0 = (long long)i * tile_rows;
     const float n = (float)(M - r0 < tile_rows ? M - r0 : tile_rows);
-    const f32x8 d = *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + c) * (1.f / n) - mean;
-    q += *reinterpret_cast<const f32x8*>(part + (size_t)i * 2 * C + C + c) + n * d * d;
-  }
-  q = tree_sum256(q, red);
+    const f32x8 d = row(i, 0) * (1.f / n) - mean;
+    return row(i, C) + n * d * d;
+  };
+  f32x8 q = z;
+  for (int i = threadIdx.x; i < G; i += 1024) q += (dev(i) + dev(i + 256)) + (dev(i + 512) + dev(i + 768));
+  q = block_sum256(q, red);
   if (threadIdx.x != 0) return;
   f32x8 var, inv;
 #pragma unroll

@@ -476,6 +476,20 @@ at::Tensor gemm_nt_add(at::Tensor a, at::Tensor b, at::Tensor r, c10::optional<a
   return c;
 }
 
+// (c, part): c = a·bᵀ and the BatchNorm statistics of its bf16 columns per
+// row group of gemm_nt_stats_rows(K) rows, part [M / rows, 2, N] = (Σ, Σ(x − x̄)²)
+// — bn_act_fwd_tiles' input
+std::vector<at::Tensor> gemm_nt_stats(at::Tensor a, at::Tensor b) {
+  nt_check(a, b);
+  const int M = a.size(0), N = b.size(0), K = a.size(1);
+  TORCH_CHECK(N % 256 == 0 || pdo::gemm_nt_epi_ok(M, N, K), "gemm_nt_stats: N % 256 = 0 on the 8-wave ring");
+  auto c = at::empty({M, N}, a.options());
+  auto part = at::empty({M / pdo::gemm_nt_stats_rows(K), 2, N}, a.options().dtype(at::kFloat));
+  CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(c), N, 9, nullptr, nullptr, 0, fp(part), cur_stream()),
+           "gemm_nt_stats");
+  return {c, part};
+}
+
 // (pre, y): pre = a·bᵀ, y = gelu(pre + bias); saved_grad: pre = gelu'(a·bᵀ + bias)
 // instead (EPI 7, for gemm_nt_dgelu(..., saved_grad=true))
 std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias, bool saved_grad) {
@@ -1177,6 +1191,8 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("splits") = 0);
   m.def("gemm_dw_splits", &pdo::gemm_dw_splits);
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_stats", &gemm_nt_stats);
+  m.def("gemm_nt_stats_rows", [](int64_t K) { return pdo::gemm_nt_stats_rows((int)K); });
   m.def("gemm_dw_impl", [](int impl) {
     const int prev = pdo::gemm_dw_get_impl();
     if (impl >= 0) pdo::gemm_dw_set_impl(impl);

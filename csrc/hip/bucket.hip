@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256) void cast_scale_bf16_f32_kernel(const bf16* __
 // x *= *s (an fp32 device scalar: the loss gradient, no host sync), fp32 math
 __global__ __launch_bounds__(256) void scale_dev_kernel(bf16* __restrict__ x, long long nvec, const float* __restrict__ s) {
   const float f = *s;
+  if (f == 1.f) return;  // bf16(f32(x) · 1) = x: the LM head's dloss of a plain loss.backward()
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
     bf16x8* p = reinterpret_cast<bf16x8*>(x) + i;
     *p = to_bf16(to_f32(*p) * f);

@@ -141,6 +141,14 @@ __device__ __forceinline__ void gelu_and_grad2(f32x2 x, f32x2 m1, f32x2& y, f32x
   g = pk_fma(y * w, pk_fma(sg, m1, -m1), sg);  // s + y·2u'·(1 - s), y = x·s
 }
 
+// BatchNorm partials (Σx, Σ(x − x̄)²) of two groups of n rows each, merged
+// (Chan: the means differ by (sa − sb)/n, weight n·n / 2n)
+__device__ __forceinline__ void chan_merge_equal(f32x8& s, f32x8& q, const f32x8& s2, const f32x8& q2, float n) {
+  const f32x8 d = s - s2;
+  q = q + q2 + d * d * (0.5f / n);
+  s = s + s2;
+}
+
 // number of workgroups for a grid-stride memory-bound kernel (256 CUs × 8)
 inline int stream_grid(long long work_items, int per_block) {
   long long g = (work_items + per_block - 1) / per_block;

@@ -33,6 +33,10 @@
 //              fc1 writes C = gelu'(A·Bᵀ + bias), Y = gelu(A·Bᵀ + bias); fc2's
 //              input gradient is then C = (A·Bᵀ) ⊙ Y plus the bias-gradient
 //              partials — one multiply per element instead of the derivative
+//   EPI 9      C = A·Bᵀ and the BatchNorm statistics of the bf16 outputs per
+//              row group: [groups][2][N] (Σ, Σ(x − x̄)²), gemm_nt_stats_rows
+//              rows each, merged by batchnorm.hip bn_fwd_tiles — a 1×1
+//              convolution's forward without a statistics pass over its output
 // Rounding matches the unfused path bit for bit: the GEMM result is rounded to
 // bf16 before the activation math, as when it made an HBM round trip.
 #include <stdlib.h>
@@ -197,6 +201,9 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
   f32x8 bv8;
   if constexpr (EPI == 2 || EPI == 3) bv8 = to_f32(*reinterpret_cast<const bf16x8*>(bias + n));
   f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // EPI 9: statistics of this thread's 16 rows, shifted by its first row
+  f32x8 x0 = colp, ssq = colp;
+  if constexpr (EPI == 9) x0 = to_f32(*reinterpret_cast<const bf16x8*>(lds + r0 * 512 + ((c ^ (r0 & 31)) << 4)));
 #pragma unroll 4
   for (int it = 0; it < 16; ++it) {
     const int r = 16 * it + r0;
@@ -204,6 +211,11 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
     const size_t m = (size_t)(m0 + r);
     if constexpr (EPI <= 1) {
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+    } else if constexpr (EPI == 9) {
+      *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
+      const f32x8 d = to_f32(v) - x0;
+      colp += d;
+      ssq += d * d;
     } else if constexpr (EPI == 2) {
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = v;
       const f32x8 x = to_f32(v) + bv8;
@@ -230,6 +242,37 @@ __global__ __launch_bounds__(NTHR) void gemm_nt_kernel(const bf16* __restrict__ 
       for (int e = 0; e < 8; ++e) d[e] = dy[e] * gelu_sig_grad(x[e]);
       colp += d;
       *reinterpret_cast<bf16x8*>(C + m * ldc + n) = to_bf16(d);
+    }
+  }
+  if constexpr (EPI == 9) {
+    // 16 rows per thread → lanes l, l + 32 (rows r0 = 2w, 2w + 1) → the 8 waves
+    // through LDS (the staged tile is dead after this barrier): one 256-row
+    // group per M-tile, partial row tm of [M/256][2][N]
+    f32x8 sum = colp + 16.f * x0, m2 = ssq - colp * colp * (1.f / 16.f), s2, q2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s2[k] = __shfl_xor(sum[k], 32, 64);
+      q2[k] = __shfl_xor(m2[k], 32, 64);
+    }
+    chan_merge_equal(sum, m2, s2, q2, 16.f);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [8 waves][2][256]
+    if (lane < 32) {
+      *reinterpret_cast<f32x8*>(red + w * 512 + 8 * c) = sum;
+      *reinterpret_cast<f32x8*>(red + w * 512 + 256 + 8 * c) = m2;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      float s = red[tid], q = red[256 + tid];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {  // (32k rows) + (32 rows)
+        const float sb = red[k * 512 + tid], qb = red[k * 512 + 256 + tid];
+        const float d = sb * (1.f / 32.f) - s * (1.f / (32.f * k));
+        q += qb + d * d * (32.f * k * 32.f / (32.f * (k + 1)));
+        s += sb;
+      }
+      dbias_part[(size_t)tm * 2 * N + n0 + tid] = s;
+      dbias_part[(size_t)tm * 2 * N + N + n0 + tid] = q;
     }
   }
   if constexpr (EPI == 3) {
@@ -264,6 +307,9 @@ int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
 }
 
 int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
+int gemm_nt_epi_ok(int M, int N, int K) { return gemm_nt_ok(M, N, K, K, K, N) && nt4_path(K); }
+// rows per BatchNorm partial of EPI 9: a (tile, wm) half on the 4-wave mainloop, the tile on the ring
+int gemm_nt_stats_rows(int K) { return nt4_path(K) ? BM / 2 : BM; }
 void gemm_nt_set_impl(int impl) { g_impl = impl; }
 
 int gemm_nt_get_impl() { return g_impl; }
@@ -273,9 +319,9 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
   if (!gemm_nt_ok(M, N, K, lda, ldb, ldc)) return -2;
   if (((epi >= 1 && epi <= 3) || (epi >= 5 && epi <= 7)) && !bias) return -3;  // EPI 6: bias = the addend's keep mask
   if (epi == 6 && ldy % 8) return -3;
-  if ((epi >= 2) && (!Y || ldy % 4 || ldy < N)) return -3;
-  if ((epi == 3 || epi == 8) && !dbias_part) return -3;
-  if (epi >= 7 && !nt4_path(K)) return -4;  // the saved-GELU' pair exists on the 4-wave mainloop only
+  if (epi >= 2 && epi != 9 && (!Y || ldy % 4 || ldy < N)) return -3;
+  if ((epi == 3 || epi == 8 || epi == 9) && !dbias_part) return -3;
+  if ((epi == 7 || epi == 8) && !nt4_path(K)) return -4;  // the saved-GELU' pair: 4-wave mainloop only
   if (nt4_path(K))
     return gemm_nt4(A, B, M, N, K, lda, ldb, C, ldc, epi, bias, Y, ldy, dbias_part, st);
   const long long grid = (long long)(M / BM) * (N / BN);
@@ -289,6 +335,7 @@ int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb,
     case 4: gemm_nt_kernel<4><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 5: gemm_nt_kernel<5><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     case 6: gemm_nt_kernel<6><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
+    case 9: gemm_nt_kernel<9><<<(int)grid, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part); break;
     default: return -4;
   }
   return 0;

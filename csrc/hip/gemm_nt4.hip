@@ -218,7 +218,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     const int nb = n0 + wn * 128 + 8 * (lane & 15);
     const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
     // EPI 3: the GELU pre-activation; EPI 4 / 5 / 6: the addend; EPI 8: the saved GELU'
-    constexpr bool PRE = EPI >= 3 && EPI != 7;
+    constexpr bool PRE = EPI >= 3 && EPI != 7 && EPI != 9;
     bf16x8 pre[PRE ? 32 : 1];
     unsigned char mk[EPI == 6 ? 32 : 1];  // EPI 6: the addend's keep bits (8 columns per byte)
     if constexpr (PRE) {
@@ -235,6 +235,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     f32x8 colp = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     f32x2 m1 = {-1.f, -1.f};
     asm volatile("" : "+v"(m1));
+    // EPI 9: BatchNorm statistics of the bf16 outputs — per lane its 8 columns
+    // over the 32 rows it holds (16i + 4(l >> 4) + e), shifted by the first row
+    // (x0) so Σd² − (Σd)²/32 does not cancel when |mean| ≫ std
+    f32x8 x0 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssum = x0, ssq = x0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       f32x4 a[8];
@@ -247,6 +251,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         bf16* crow = C + m * ldc + nb;
         if constexpr (EPI <= 1) {
           st16(crow, to_bf16(v + bv8));
+        } else if constexpr (EPI == 9) {
+          const bf16x8 o = to_bf16(v);
+          st16(crow, o);
+          const f32x8 r = to_f32(o);
+          if (i == 0 && e == 0) x0 = r;
+          const f32x8 d = r - x0;
+          ssum += d;
+          ssq += d * d;
         } else if constexpr (EPI == 2) {
           // GELU of the fp32 pre-activation (the bf16 copy is stored for the
           // backward, as hipBLASLt's GELU_AUX epilogue does); no bf16 round trip:
@@ -307,6 +319,31 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
           colp += d;
           st16(crow, to_bf16(d));
         }
+      }
+    }
+    if constexpr (EPI == 9) {
+      // this lane's 32 rows, then the four lane groups (same columns, rows
+      // 4·g4 + …) merged by xor-16 / xor-32 exchanges: one 128-row group per
+      // (M-tile, wm), partial row 2·tm + wm of [M/128][2][N]
+      f32x8 sum = ssum + 32.f * x0, m2 = ssq - ssum * ssum * (1.f / 32.f);
+      float n = 32.f;
+#pragma unroll
+      for (int x = 16; x <= 32; x *= 2) {
+        f32x8 s2, q2;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          s2[k] = __shfl_xor(sum[k], x, 64);
+          q2[k] = __shfl_xor(m2[k], x, 64);
+        }
+        chan_merge_equal(sum, m2, s2, q2, n);
+        n *= 2.f;
+      }
+      if (g4 == 0) {
+        float* prow = dbias_part + (size_t)(2 * tm + wm) * 2 * N + nb;
+        *reinterpret_cast<f32x4*>(prow) = f32x4{sum[0], sum[1], sum[2], sum[3]};
+        *reinterpret_cast<f32x4*>(prow + 4) = f32x4{sum[4], sum[5], sum[6], sum[7]};
+        *reinterpret_cast<f32x4*>(prow + N) = f32x4{m2[0], m2[1], m2[2], m2[3]};
+        *reinterpret_cast<f32x4*>(prow + N + 4) = f32x4{m2[4], m2[5], m2[6], m2[7]};
       }
     }
     if constexpr (EPI == 3 || EPI == 8) {
@@ -497,6 +534,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
       case 6: return go(gemm_nt4_kernel<6, MI>);
       case 7: return go(gemm_nt4_kernel<7, MI>);
       case 8: return go(gemm_nt4_kernel<8, MI>);
+      case 9: return go(gemm_nt4_kernel<9, MI>);
       default: return -4;
     }
   };

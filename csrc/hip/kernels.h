@@ -148,6 +148,10 @@ int gemm_dw_get_impl();
 // (0 plain, 1 +bias, 2 C = pre-activation & Y = gelu(C + bias),
 //  3 C = (A·Bᵀ)⊙gelu'(Y + bias) & fp32 column partials [gemm_nt_dbias_rows(M)][N])
 int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc);
+// EPI 7 / 8 / 9 (the 4-wave mainloop's epilogues) apply to this product
+int gemm_nt_epi_ok(int M, int N, int K);
+// rows per BatchNorm partial row of EPI 9 (gemm_nt with the statistics epilogue)
+int gemm_nt_stats_rows(int K);
 int gemm_nt_dbias_rows(int M);
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);

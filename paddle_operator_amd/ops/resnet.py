@@ -224,6 +224,20 @@ def _gemm_fwd_1x1(m, T, C, K) -> bool:
     return K > 128 and bool(m.gemm_nt_supported(T, K, C))
 
 
+# the 1×1 forward on gemm_nt takes the BatchNorm statistics in its epilogue
+# (gemm_nt4 EPI 9) where the 4-wave mainloop runs it; PDO_GEMM_BN_STATS=0 = a
+# separate statistics pass over the output (the A/B alternative)
+_GEMM_BN_STATS = [os.environ.get("PDO_GEMM_BN_STATS", "1") != "0"]
+
+
+def _fwd_stats_rows(m, conv: torch.nn.Conv2d, x) -> int:
+    """Rows per partial of the statistics _ConvFn returns for conv(x)."""
+    N, C, H, W = x.shape
+    if conv.kernel_size[0] == 1 and conv.stride[0] == 1 and _gemm_fwd_1x1(m, N * H * W, C, conv.out_channels):
+        return m.gemm_nt_stats_rows(C)
+    return m.conv_tile_rows(conv.out_channels)
+
+
 def _gemm_dgrad_1x1(m, T, C, K) -> bool:
     """1×1 stride-1 input gradient on gemm_nt: faster at C > 128 input channels
     (profiles/r4d_conv_probe.jsonl)."""
@@ -268,7 +282,12 @@ class _ConvFn(torch.autograd.Function):
         ctx.one = R == 1 and stride == 1
         st = None
         if ctx.one and _gemm_fwd_1x1(m, N * H * W_, C, K):
-            y = m.gemm_nt(x.permute(0, 2, 3, 1).reshape(-1, C), wb.view(K, C)).view(N, H, W_, K).permute(0, 3, 1, 2)
+            x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+            if want_stats and _GEMM_BN_STATS[0]:
+                y, st = m.gemm_nt_stats(x2, wb.view(K, C))  # + BatchNorm partials (EPI 9, _fwd_stats_rows)
+            else:
+                y = m.gemm_nt(x2, wb.view(K, C))
+            y = y.view(N, H, W_, K).permute(0, 3, 1, 2)
         else:
             y, st = m.conv_fwd(x, wb, stride, pad, want_stats)
         ctx.save_for_backward(x, wb)
@@ -491,7 +510,7 @@ def _conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool 
         else:
             mom = bn.momentum if bn.momentum is not None else 0.1
             m = _native.require_hip()
-            rows = m.stem_tile_rows() if stem else m.conv_tile_rows(conv.out_channels)
+            rows = m.stem_tile_rows() if stem else _fwd_stats_rows(m, conv, x)
             link = _BNLink() if residual is None and _BN_LINK[0] and torch.is_grad_enabled() else None
             out = _BNActFn.apply(y, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, mom,
                                  relu, st, rows, link, rres, ml)

@@ -234,3 +234,33 @@ def test_nt4_saved_gelu_grad_pair_vs_fp32(hip, M, N, K):
     (dx2,) = hip.gemm_nt_dgelu(dy, w2t, gd, b1, db_out=acc, saved_grad=True)
     assert torch.equal(dx2, dx)
     torch.testing.assert_close(acc.float(), 1.0 + ref.sum(0), rtol=2e-2, atol=0.5 * (M / 16384) ** 0.5 + 0.01)
+
+
+@pytest.mark.parametrize("M,N,K", [(12544, 1024, 256), (50176, 256, 1024), (3328, 2048, 512), (768, 640, 512),
+                                   (802816 // 4, 256, 64), (12544, 512, 128)])
+def test_nt_bn_stats_epilogue_vs_fp32(hip, M, N, K):
+    """EPI 9 (gemm_nt_stats): C = A·Bᵀ plus BatchNorm partials (Σ, Σ(x − x̄)²)
+    of the bf16 outputs per row group — on the 4-wave mainloop a (256-row tile,
+    wm) half: rows 256·tile + 128·wm + …, 128 rows; on the 8-wave ring (K < 256)
+    the whole 256-row tile.  Checked per group against fp32 sums of the
+    kernel's own bf16 output, and the merged column mean / variance against the
+    fp32 product (ResNet-50 1×1 shapes, a half-width last tile column)."""
+    g = torch.Generator(device="cuda").manual_seed(41)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-0.05, 0.05, generator=g)
+    a[:, 0] = 8.0  # a column offset: |mean| ≫ std in some channels
+    rows = hip.gemm_nt_stats_rows(K)
+    assert rows == (128 if K >= 256 else 256)
+    c, part = hip.gemm_nt_stats(a, b)
+    ref = a.float() @ b.float().t()
+    assert bool(((c.float() - ref).abs() <= 1e-2 + 8e-3 * ref.abs()).all())
+    assert part.shape == (M // rows, 2, N)
+    yg = c.float().view(M // rows, rows, N)
+    s_ref = yg.sum(1)
+    m2_ref = ((yg - yg.mean(1, keepdim=True)) ** 2).sum(1)
+    torch.testing.assert_close(part[:, 0], s_ref, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(part[:, 1], m2_ref, rtol=2e-3, atol=2e-3)
+    mean = part[:, 0].sum(0) / M
+    var = (part[:, 1].sum(0) + (rows * (part[:, 0] / rows - mean) ** 2).sum(0)) / M
+    torch.testing.assert_close(mean, ref.mean(0), rtol=1e-2, atol=2e-3)
+    torch.testing.assert_close(var, ref.var(0, unbiased=False), rtol=2e-2, atol=1e-4)
