@@ -1193,6 +1193,10 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_stats", &gemm_nt_stats);
   m.def("gemm_nt_stats_rows", [](int64_t K) { return pdo::gemm_nt_stats_rows((int)K); });
+  // EPI 7 / 8 (the saved-GELU' pair) run on the 4-wave mainloop only
+  m.def("gemm_nt_epi_ok", [](int64_t M, int64_t N, int64_t K) {
+    return M < (1LL << 31) && N < (1LL << 31) && pdo::gemm_nt_epi_ok((int)M, (int)N, (int)K) != 0;
+  });
   m.def("gemm_dw_impl", [](int impl) {
     const int prev = pdo::gemm_dw_get_impl();
     if (impl >= 0) pdo::gemm_dw_set_impl(impl);

@@ -270,7 +270,7 @@ class _NTMLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2=None, res=None):
         m = _native.require_hip()
         x2 = x.reshape(-1, x.shape[-1])
-        ctx.saved_grad = _NT_GD[0]
+        ctx.saved_grad = _NT_GD[0] and bool(m.gemm_nt_epi_ok(x2.shape[0], w1.shape[0], w1.shape[1]))
         hp, h = m.gemm_nt_gelu(x2, w1, b1, saved_grad=ctx.saved_grad)  # hp = gelu'(x·W1ᵀ + b1) when saved_grad
         ctx.save_for_backward(x2, w1, hp, h, w2)
         ctx.b1 = b1
