@@ -163,27 +163,34 @@ __global__ __launch_bounds__(FIN_THREADS) void bn_finalize_kernel(const float* _
 // a lane's channel chunk never changes along the grid-stride loop.
 // mask (optional): bit j of byte i = [y[8i + j] > 0], the ReLU mask the backward
 // reads instead of y (1/16 of the bytes; relu = 2 there)
+// rss (optional, with res): the residual is itself a BatchNorm's input — res·rscale
+// + rshift is added (ResNet's downsample branch: its normalised output never
+// exists in memory)
 template <bool HOIST>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                        const float* __restrict__ ss, long long n8, int C, int relu,
-                                                       bf16* __restrict__ y, unsigned char* __restrict__ mask) {
+                                                       bf16* __restrict__ y, unsigned char* __restrict__ mask,
+                                                       const float* __restrict__ rss) {
   const int C8 = C / 8;
   const long long i0 = blockIdx.x * 256LL + threadIdx.x;
   const long long stride = (long long)gridDim.x * 256;
-  Affine a;
-  if (HOIST) {
-    const int c = (int)(i0 % C8) * 8;
+  Affine a, ra;
+  auto load_aff = [&](int c) {
     a.sc = *reinterpret_cast<const f32x8*>(ss + c);
     a.sh = *reinterpret_cast<const f32x8*>(ss + C + c);
-  }
-  for (long long i = i0; i < n8; i += stride) {
-    if (!HOIST) {
-      const int c = (int)(i % C8) * 8;
-      a.sc = *reinterpret_cast<const f32x8*>(ss + c);
-      a.sh = *reinterpret_cast<const f32x8*>(ss + C + c);
+    if (rss) {
+      ra.sc = *reinterpret_cast<const f32x8*>(rss + c);
+      ra.sh = *reinterpret_cast<const f32x8*>(rss + C + c);
     }
+  };
+  if (HOIST) load_aff((int)(i0 % C8) * 8);
+  for (long long i = i0; i < n8; i += stride) {
+    if (!HOIST) load_aff((int)(i % C8) * 8);
     f32x8 v = preact(to_f32(reinterpret_cast<const bf16x8*>(x)[i]), a);
-    if (res) v += to_f32(reinterpret_cast<const bf16x8*>(res)[i]);
+    if (res) {
+      const f32x8 r = to_f32(reinterpret_cast<const bf16x8*>(res)[i]);
+      v += rss ? preact(r, ra) : r;
+    }
     if (relu) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -596,8 +603,8 @@ int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float
                                              invstd, ss);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
-  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
-  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
+  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask, nullptr);
+  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask, nullptr);
   return 0;
 }
 
@@ -612,8 +619,29 @@ int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, co
                                                   running_var, mean, invstd, ss);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
-  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
-  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask);
+  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask, nullptr);
+  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask, nullptr);
+  return 0;
+}
+
+// y = act(BN(x) + BN_r(r)) with both BatchNorms' statistics from their
+// producing convolutions: two finalizes, one apply pass (the residual
+// BatchNorm's output is never written)
+int bn_fwd_tiles_bnres(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
+                       float* running_mean, float* running_var, float eps, float momentum, float* mean, float* invstd,
+                       float* ss, const float* rtile_part, int rG, int rtile_rows, const bf16* r, const float* rw,
+                       const float* rb, float* rrunning_mean, float* rrunning_var, float reps, float rmomentum,
+                       float* rmean, float* rinvstd, float* rss, long long M, int C, int relu, bf16* y,
+                       unsigned char* mask, hipStream_t st) {
+  if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1 || rG < 1) return -2;
+  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
+                                                  running_var, mean, invstd, ss);
+  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(rtile_part, rG, rtile_rows, M, C, rw, rb, reps, rmomentum,
+                                                  rrunning_mean, rrunning_var, rmean, rinvstd, rss);
+  const long long n8 = M * C / 8;
+  const unsigned g = apply_grid(n8);
+  if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, r, ss, n8, C, relu, y, mask, rss);
+  else bn_apply_kernel<false><<<g, 256, 0, st>>>(x, r, ss, n8, C, relu, y, mask, rss);
   return 0;
 }
 

@@ -863,6 +863,44 @@ std::vector<at::Tensor> bn_act_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t
   return {y, mean, invstd, mask};
 }
 
+// y = act(BN(x) + BN_r(r)) from both convolutions' tile statistics (ResNet's
+// downsample block: r = the downsample conv's output, never normalised in memory):
+// [y, mean, invstd, mask (ReLU bits), rmean, rinvstd]
+std::vector<at::Tensor> bn_act_fwd_tiles_bnres(at::Tensor x, at::Tensor stats, int64_t tile_rows, at::Tensor w,
+                                               at::Tensor b, c10::optional<at::Tensor> rm,
+                                               c10::optional<at::Tensor> rv, double eps, double momentum,
+                                               at::Tensor r, at::Tensor rstats, int64_t rtile_rows, at::Tensor rw,
+                                               at::Tensor rb, c10::optional<at::Tensor> rrm,
+                                               c10::optional<at::Tensor> rrv, double reps, double rmomentum,
+                                               bool relu) {
+  CHECK_BF16(x); CHECK_BF16(r); CHECK_F32(w); CHECK_F32(b); CHECK_F32(rw); CHECK_F32(rb);
+  CHECK_F32(stats); CHECK_F32(rstats);
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              r.sizes() == x.sizes() && r.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_act_fwd_tiles_bnres: channels_last bf16 x and r of one shape");
+  const long long C = x.size(1), M = x.numel() / C;
+  TORCH_CHECK(stats.dim() == 3 && stats.size(1) == 2 && stats.size(2) == C &&
+              stats.size(0) == (M + tile_rows - 1) / tile_rows, "bn_act_fwd_tiles_bnres: stats [tiles, 2, C]");
+  TORCH_CHECK(rstats.dim() == 3 && rstats.size(1) == 2 && rstats.size(2) == C &&
+              rstats.size(0) == (M + rtile_rows - 1) / rtile_rows, "bn_act_fwd_tiles_bnres: rstats [tiles, 2, C]");
+  TORCH_CHECK(w.numel() == C && b.numel() == C && rw.numel() == C && rb.numel() == C);
+  auto y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  auto mean = at::empty({C}, w.options()), invstd = at::empty({C}, w.options());
+  auto rmean = at::empty({C}, w.options()), rinvstd = at::empty({C}, w.options());
+  auto ss = at::empty({2 * C}, w.options()), rss = at::empty({2 * C}, w.options());
+  at::Tensor mask;
+  if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  auto opt = [](c10::optional<at::Tensor>& t) { return t && t->defined() ? fp(*t) : nullptr; };
+  CHECK_RC(pdo::bn_fwd_tiles_bnres(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), fp(w), fp(b), opt(rm), opt(rv),
+                                   (float)eps, (float)momentum, fp(mean), fp(invstd), fp(ss), fp(rstats),
+                                   (int)rstats.size(0), (int)rtile_rows, bp(r), fp(rw), fp(rb), opt(rrm), opt(rrv),
+                                   (float)reps, (float)rmomentum, fp(rmean), fp(rinvstd), fp(rss), M, (int)C,
+                                   relu ? 1 : 0, bp(y), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
+                                   cur_stream()),
+           "bn_fwd_tiles_bnres");
+  return {y, mean, invstd, mask, rmean, rinvstd};
+}
+
 // ResNet stem BatchNorm + ReLU + max-pool 3×3/2 from the stem conv's tile statistics:
 // [pooled y, window positions (uint8), xsel (the BatchNorm input at each maximum), mean, invstd]
 std::vector<at::Tensor> bn_relu_pool_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t tile_rows, at::Tensor w,
@@ -1212,6 +1250,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),
         py::arg("db_out") = py::none(), py::arg("saved_grad") = false);
   m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_fwd_tiles_bnres", &bn_act_fwd_tiles_bnres);
   m.def("bn_act_fwd_tiles", &bn_act_fwd_tiles);
   m.def("conv_ok", &conv_ok);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),

@@ -109,6 +109,13 @@ int stem_wgrad(const bf16* dy, const bf16* z, int N, int IH, int IW, int Kout, f
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
                  float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st, unsigned char* mask = nullptr);
+// act(BN(x) + BN_r(r)): both from their convolutions' tile statistics, one apply pass
+int bn_fwd_tiles_bnres(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
+                       float* running_mean, float* running_var, float eps, float momentum, float* mean, float* invstd,
+                       float* ss, const float* rtile_part, int rG, int rtile_rows, const bf16* r, const float* rw,
+                       const float* rb, float* rrunning_mean, float* rrunning_var, float reps, float rmomentum,
+                       float* rmean, float* rinvstd, float* rss, long long M, int C, int relu, bf16* y,
+                       unsigned char* mask, hipStream_t st);
 int bn_fwd_scratch_floats(long long M, int C);
 // ResNet stem BatchNorm + ReLU + 3×3/2 max-pool fused (batchnorm.hip): forward from
 // the conv's tile statistics → pooled y and window positions; backward → dx of the

@@ -46,10 +46,10 @@ class Bottleneck(nn.Module):
         # gradient joins conv1's dX in the dX kernel's epilogue.
         out, xa = ops.conv_bn_act(self.conv1, self.bn1, x, fork=True)
         out = ops.conv_bn_act(self.conv2, self.bn2, out)
-        idt = xa
         if self.downsample is not None:
-            idt = ops.conv_bn_act(self.downsample[0], self.downsample[1], xa, relu=False, as_residual=True)
-        return ops.conv_bn_act(self.conv3, self.bn3, out, relu=True, residual=idt)
+            # bn3 and the downsample BatchNorm in one apply pass where fused
+            return ops.conv_bn_ds_act(self.conv3, self.bn3, out, self.downsample[0], self.downsample[1], xa)
+        return ops.conv_bn_act(self.conv3, self.bn3, out, relu=True, residual=xa)
 
 
 class ResNet(nn.Module):

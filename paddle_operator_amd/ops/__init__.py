@@ -18,13 +18,15 @@ from .gpt2 import (  # noqa: F401
     attention, bias_gelu, cross_entropy, embedding, layer_norm, linear_add_layer_norm, lm_head_xent, mlp, mlp_add_layer_norm,
     qkv_attention)
 from .resnet import (  # noqa: F401
-    _BNLink, _BNReluPoolFn, _CompactGradLink, _ResMaskLink, _StemFn, _BN_FUSED, _GEMM_BN_STATS, _BN_LINK, _BN_LINK_USED, _DS_COMPACT, _DS_COMPACT_USED, _HIP_CONV, _HIP_STEM, _RES_MASK,
-    _RES_MASK_USED, _STEM_POOL, _apply_bitmask, _stem_ok, bn_act, conv1x1, conv_bn_act, conv_bn_relu_maxpool,
+    _BNActBNResFn, _BNLink, _BNReluPoolFn, _CompactGradLink, _ResMaskLink, _StemFn, _BN_FUSED, _DS_FUSED,
+    _GEMM_BN_STATS, _BN_LINK, _BN_LINK_USED, _DS_COMPACT, _DS_COMPACT_USED, _HIP_CONV, _HIP_STEM, _RES_MASK,
+    _RES_MASK_USED, _STEM_POOL, _apply_bitmask, _stem_ok, bn_act, conv1x1, conv_bn_act, conv_bn_ds_act,
+    conv_bn_relu_maxpool,
     max_pool_3x3s2)
 
 __all__ = [
     "layer_norm", "add_layer_norm", "bias_gelu", "attention", "cross_entropy",
     "embedding", "ref_layer_norm", "ref_bias_gelu", "ref_attention",
     "ref_cross_entropy", "use_hip", "linear", "mlp", "qkv_attention", "lm_head_xent",
-    "conv_bn_act", "bn_act", "deferred_reductions",
+    "conv_bn_act", "conv_bn_ds_act", "bn_act", "deferred_reductions",
 ]

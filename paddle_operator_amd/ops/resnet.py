@@ -523,6 +523,75 @@ def _conv_bn_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, relu: bool 
     return (out, x) if fork else out
 
 
+class _BNActBNResFn(torch.autograd.Function):
+    """y = ReLU(BN(x) + BN_r(r)) — ResNet's downsample block tail: bn3 over
+    conv3's output x and the downsample BatchNorm over the downsample conv's
+    output r, both from their convolutions' tile statistics, in ONE apply pass
+    (``bn_act_fwd_tiles_bnres``): the downsample branch's normalised activation
+    is never written or re-read.  Backward: each BatchNorm's backward from the
+    shared output gradient and ReLU bitmask (what the unfused pair did through
+    the residual-mask hand-off)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, r, rw, rb, rm, rv, eps, mom, rrm, rrv, reps, rmom, stats, rows, rstats, rrows):
+        m = _native.require_hip()
+        y, mean, invstd, mask, rmean, rinvstd = m.bn_act_fwd_tiles_bnres(
+            x, stats, rows, w, b, rm, rv, eps, mom, r, rstats, rrows, rw, rb, rrm, rrv, reps, rmom, True)
+        ctx.save_for_backward(x, r, mask, mean, invstd, w, b, rmean, rinvstd, rw, rb)
+        ctx.params = (w, b, rw, rb)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        m = _native.require_hip()
+        x, r, mask, mean, invstd, w, b, rmean, rinvstd, rw, rb = ctx.saved_tensors
+        grads = []
+        for (xi, mu, inv, wi, bi), (pw, pb) in (((x, mean, invstd, w, b), ctx.params[:2]),
+                                                ((r, rmean, rinvstd, rw, rb), ctx.params[2:])):
+            direct = _direct_ok(pw) and _direct_ok(pb) and pw.grad.dtype == torch.float32
+            dwi, dbi = (pw.grad, pb.grad) if direct else (None, None)
+            dxi, _, dw, db = m.bn_act_bwd(dy, mask, xi, mu, inv, wi, bi, True, False, dwi, dbi)
+            if direct:
+                pw._pdo_ready(pw)
+                pb._pdo_ready(pb)
+                dw = db = None
+            grads.append((dxi, dw, db))
+        (dx, dw, db), (dr, drw, drb) = grads
+        return dx, dw, db, dr, drw, drb, None, None, None, None, None, None, None, None, None, None, None, None
+
+
+# ResNet's downsample block: bn3 and the downsample BatchNorm in one apply pass
+# (_BNActBNResFn); False = the downsample BatchNorm's own apply pass (A/B, tests)
+_DS_FUSED = [os.environ.get("PDO_DS_BN_FUSED", "1") != "0"]
+
+
+def conv_bn_ds_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, dconv: torch.nn.Conv2d,
+                   dbn: torch.nn.BatchNorm2d, xa):
+    """ReLU(BN(conv(x)) + BN_d(dconv(xa))) — a downsample bottleneck's tail.
+    Both convolutions on the hand-written kernels with BatchNorm statistics in
+    their epilogues, then one apply pass (_BNActBNResFn); otherwise the
+    downsample branch through conv_bn_act(as_residual=True) and bn3 with it as
+    the residual."""
+    m = _native.require_hip() if use_hip(x) else None
+    if (m is not None and _DS_FUSED[0] and torch.is_grad_enabled() and _hip_conv_ok(conv, x)
+            and _hip_conv_ok(dconv, xa) and _bn_fused_ok(bn, None) and _bn_fused_ok(dbn, None)):
+        # the downsample conv first (as the unfused order): its compact input
+        # gradient goes to the conv that forked xa (_CompactGradLink)
+        cl = getattr(xa, "_pdo_slink", None)
+        yd, std, _ = _ConvFn.apply(xa, dconv.weight, dconv.stride[0], dconv.padding[0], True, False, None, None, cl)
+        y, st, _ = _ConvFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], True)
+        if st is not None and std is not None:
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            dmom = dbn.momentum if dbn.momentum is not None else 0.1
+            return _BNActBNResFn.apply(y, bn.weight, bn.bias, yd, dbn.weight, dbn.bias, bn.running_mean,
+                                       bn.running_var, bn.eps, mom, dbn.running_mean, dbn.running_var, dbn.eps, dmom,
+                                       st, _fwd_stats_rows(m, conv, x), std, _fwd_stats_rows(m, dconv, xa))
+        idt = bn_act(dbn, yd, relu=False)
+        return bn_act(bn, y, relu=True, residual=idt)
+    idt = conv_bn_act(dconv, dbn, xa, relu=False, as_residual=True)
+    return conv_bn_act(conv, bn, x, relu=True, residual=idt)
+
+
 class _BNReluPoolFn(torch.autograd.Function):
     """max_pool_3x3s2(ReLU(BN(x))) for ResNet's stem in one forward pass (from the
     stem convolution's tile statistics) and a two-pass backward

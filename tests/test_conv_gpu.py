@@ -488,8 +488,10 @@ def test_identity_bottleneck_residual_mask_in_dx_epilogue(downsample):
     x = torch.randn(4, 256, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     outs = []
     for mod, on in ((a, True), (b, False)):
-        prev = ops._RES_MASK[0]
-        ops._RES_MASK[0] = on
+        prev = ops._RES_MASK[0], ops._DS_FUSED[0]
+        # (the downsample case exercises the two-pass tail's hand-off: the fused
+        # tail, _BNActBNResFn, needs none — test_downsample_block_bn_pair_in_one_apply)
+        ops._RES_MASK[0], ops._DS_FUSED[0] = on, False
         used = ops._RES_MASK_USED[0]
         try:
             xx = x.clone().requires_grad_()
@@ -497,7 +499,7 @@ def test_identity_bottleneck_residual_mask_in_dx_epilogue(downsample):
                 y = mod(xx)
             (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
         finally:
-            ops._RES_MASK[0] = prev
+            ops._RES_MASK[0], ops._DS_FUSED[0] = prev
         assert (ops._RES_MASK_USED[0] - used) == (1 if on else 0)
         outs.append((y, xx.grad))
     assert torch.equal(outs[0][0], outs[1][0])
@@ -556,3 +558,64 @@ def test_downsample_compact_input_gradient():
     assert _rel(outs[0][1], outs[1][1]) < 1e-2
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         assert _rel(pa.grad, pb.grad) < 1e-2, n
+
+
+@pytest.mark.parametrize("cin,width,stride,hw", [(256, 128, 2, 16), (64, 64, 1, 16), (1024, 512, 2, 14)])
+def test_downsample_block_bn_pair_in_one_apply(cin, width, stride, hw):
+    """A downsample bottleneck's tail ReLU(bn3(conv3) + bn_ds(conv_ds)) in one
+    apply pass (ops._BNActBNResFn: the downsample BatchNorm's output never
+    materialised) — same output, input / parameter gradients and running
+    statistics as the two-pass path (PDO_DS_BN_FUSED=0); also against an fp32
+    copy of the block on the framework ops."""
+    import copy
+
+    from paddle_operator_amd import ops
+    from paddle_operator_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(13)
+    ds = torch.nn.Sequential(torch.nn.Conv2d(cin, width * 4, 1, stride=stride, bias=False),
+                             torch.nn.BatchNorm2d(width * 4))
+    a = Bottleneck(cin, width, stride=stride, downsample=ds).cuda().to(memory_format=torch.channels_last)
+    for mod in a.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(mod.weight, 0.5, 1.5)
+            torch.nn.init.uniform_(mod.bias, -0.2, 0.2)
+    b = copy.deepcopy(a)
+    f = copy.deepcopy(a).float()
+    x = torch.randn(4, cin, hw, hw, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    wgt = None
+    outs = []
+    for mod, on in ((a, True), (b, False)):
+        prev = ops._DS_FUSED[0]
+        ops._DS_FUSED[0] = on
+        try:
+            xx = x.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = mod(xx)
+            wgt = torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)
+            (y.float() * wgt).sum().backward()
+        finally:
+            ops._DS_FUSED[0] = prev
+        outs.append((y, xx.grad))
+    # the residual enters the apply in fp32 instead of rounded to bf16 first: the
+    # two paths differ by bf16 rounding, so each is held against an fp32 copy of
+    # the block on the framework ops and the fused one may not be the worse
+    assert _rel(outs[0][0], outs[1][0]) < 1e-2
+    for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
+        if ba.dtype.is_floating_point:
+            torch.testing.assert_close(ba, bb, rtol=1e-3, atol=1e-4, msg=n)
+    prev = ops._HIP_CONV[0], ops._BN_FUSED[0]
+    ops._HIP_CONV[0], ops._BN_FUSED[0] = False, False
+    try:
+        xf = x.float().requires_grad_()
+        yf = f(xf)
+        (yf * wgt).sum().backward()
+    finally:
+        ops._HIP_CONV[0], ops._BN_FUSED[0] = prev
+    e_fused, e_two = _rel(outs[0][0].float(), yf), _rel(outs[1][0].float(), yf)
+    assert e_fused < 3e-2 and e_fused <= 1.25 * e_two + 1e-3, (e_fused, e_two)
+    e_fused, e_two = _rel(outs[0][1].float(), xf.grad), _rel(outs[1][1].float(), xf.grad)
+    assert e_fused < 0.15 and e_fused <= 1.25 * e_two + 1e-3, ("dx", e_fused, e_two)
+    for (n, pa), (_, pb), (_, pf) in zip(a.named_parameters(), b.named_parameters(), f.named_parameters()):
+        e_fused, e_two = _rel(pa.grad.float(), pf.grad), _rel(pb.grad.float(), pf.grad)
+        assert e_fused < 0.15 and e_fused <= 1.25 * e_two + 1e-3, (n, e_fused, e_two)
