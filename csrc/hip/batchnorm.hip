@@ -280,6 +280,61 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_kernel(const bf16* __
   }
 }
 
+// the same for two BatchNorms fed one output gradient through one ReLU bitmask
+// (ResNet's downsample block tail: bn3 over x, the downsample BatchNorm over r):
+// g = dy ⊙ mask is read once, partials (Σg, Σg·(x−μ)) and (Σg, Σg·(r−μr))
+template <int TX>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_stats_pair_kernel(
+    const bf16* __restrict__ dy, const unsigned char* __restrict__ mask, const bf16* __restrict__ x,
+    const float* __restrict__ mean, const bf16* __restrict__ r, const float* __restrict__ rmean, long long M, int C,
+    long long rows_per_group, float* __restrict__ part, float* __restrict__ rpart) {
+  constexpr int TY = BN_THREADS / TX;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const int c8 = blockIdx.x * TX + tx;
+  const long long r0 = (long long)blockIdx.y * rows_per_group;
+  const long long r1 = r0 + rows_per_group < M ? r0 + rows_per_group : M;
+  f32x8 s1 = {0, 0, 0, 0, 0, 0, 0, 0}, s2 = s1, s3 = s1;
+  const bool live = c8 * 8 < C;
+  if (live) {
+    const f32x8 mu = *reinterpret_cast<const f32x8*>(mean + c8 * 8);
+    const f32x8 rmu = *reinterpret_cast<const f32x8*>(rmean + c8 * 8);
+    const int C8 = C / 8;
+    const Affine unused{};
+#pragma unroll 4
+    for (long long rr = r0 + ty; rr < r1; rr += TY) {
+      const long long i = rr * C8 + c8;
+      const f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(x)[i]);
+      const f32x8 rv = to_f32(reinterpret_cast<const bf16x8*>(r)[i]);
+      const f32x8 g = relu_grad(dy, reinterpret_cast<const bf16*>(mask), xv, unused, i, 2);
+      s1 += g;
+      s2 += g * (xv - mu);
+      s3 += g * (rv - rmu);
+    }
+  }
+  __shared__ f32x8 l1[BN_THREADS], l2[BN_THREADS], l3[BN_THREADS];
+  l1[threadIdx.x] = s1;
+  l2[threadIdx.x] = s2;
+  l3[threadIdx.x] = s3;
+  __syncthreads();
+#pragma unroll
+  for (int h = TY / 2; h > 0; h >>= 1) {
+    if (ty < h) {
+      l1[threadIdx.x] += l1[threadIdx.x + h * TX];
+      l2[threadIdx.x] += l2[threadIdx.x + h * TX];
+      l3[threadIdx.x] += l3[threadIdx.x + h * TX];
+    }
+    __syncthreads();
+  }
+  if (ty == 0 && live) {
+    float* p = part + (size_t)blockIdx.y * 2 * C + c8 * 8;
+    float* q = rpart + (size_t)blockIdx.y * 2 * C + c8 * 8;
+    *reinterpret_cast<f32x8*>(p) = l1[tx];
+    *reinterpret_cast<f32x8*>(p + C) = l2[tx];
+    *reinterpret_cast<f32x8*>(q) = l1[tx];
+    *reinterpret_cast<f32x8*>(q + C) = l3[tx];
+  }
+}
+
 // backward finalize: one block per 8-channel chunk → dgamma = Σg·x̂, dbeta = Σg
 // and the dx coefficients [3][C]: k = w·invstd, k1 = k·Σg/M,
 // k2 = k·invstd·(Σg·x̂)/M with Σg·x̂ = invstd·Σg(x−μ)
@@ -333,6 +388,39 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     const f32x8 g = relu_grad(dy, y, xv, a, i, relu);
     if (dres) reinterpret_cast<bf16x8*>(dres)[i] = to_bf16(g);
     reinterpret_cast<bf16x8*>(dx)[i] = to_bf16(k * g - k1 - k2 * (xv - mu));
+  }
+}
+
+// backward apply of the pair: dx = k·g − k1 − k2·(x−μ), dr likewise, g read once
+template <bool HOIST>
+__global__ __launch_bounds__(256) void bn_bwd_apply_pair_kernel(
+    const bf16* __restrict__ dy, const unsigned char* __restrict__ mask, const bf16* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ coef, const bf16* __restrict__ r,
+    const float* __restrict__ rmean, const float* __restrict__ rcoef, long long n8, int C, bf16* __restrict__ dx,
+    bf16* __restrict__ dr) {
+  const int C8 = C / 8;
+  const long long i0 = blockIdx.x * 256LL + threadIdx.x;
+  const long long stride = (long long)gridDim.x * 256;
+  f32x8 mu, k, k1, k2, rmu, rk, rk1, rk2;
+  auto load = [&](int c) {
+    mu = *reinterpret_cast<const f32x8*>(mean + c);
+    k = *reinterpret_cast<const f32x8*>(coef + c);
+    k1 = *reinterpret_cast<const f32x8*>(coef + C + c);
+    k2 = *reinterpret_cast<const f32x8*>(coef + 2 * C + c);
+    rmu = *reinterpret_cast<const f32x8*>(rmean + c);
+    rk = *reinterpret_cast<const f32x8*>(rcoef + c);
+    rk1 = *reinterpret_cast<const f32x8*>(rcoef + C + c);
+    rk2 = *reinterpret_cast<const f32x8*>(rcoef + 2 * C + c);
+  };
+  if (HOIST) load((int)(i0 % C8) * 8);
+  const Affine unused{};
+  for (long long i = i0; i < n8; i += stride) {
+    if (!HOIST) load((int)(i % C8) * 8);
+    const f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(x)[i]);
+    const f32x8 rv = to_f32(reinterpret_cast<const bf16x8*>(r)[i]);
+    const f32x8 g = relu_grad(dy, reinterpret_cast<const bf16*>(mask), xv, unused, i, 2);
+    reinterpret_cast<bf16x8*>(dx)[i] = to_bf16(k * g - k1 - k2 * (xv - mu));
+    reinterpret_cast<bf16x8*>(dr)[i] = to_bf16(rk * g - rk1 - rk2 * (rv - rmu));
   }
 }
 
@@ -692,6 +780,42 @@ int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, cons
     bn_bwd_apply_kernel<true><<<g, 256, 0, st>>>(dy, y, x, mean, invstd, w, b, coef, n8, C, relu, dx, dres);
   else
     bn_bwd_apply_kernel<false><<<g, 256, 0, st>>>(dy, y, x, mean, invstd, w, b, coef, n8, C, relu, dx, dres);
+  return 0;
+}
+
+// the backward of two BatchNorms whose outputs were summed under one ReLU (the
+// forward of bn_fwd_tiles_bnres): one statistics pass and one apply pass over
+// (dy, mask, x, r) instead of two of each
+int bn_bwd_scratch_pair_floats(long long M, int C) { return 2 * bn_bwd_scratch_floats(M, C); }
+
+int bn_bwd_pair(const bf16* dy, const unsigned char* mask, const bf16* x, const float* mean, const float* invstd,
+                const float* w, float* dw, float* db, int accumulate, const bf16* r, const float* rmean,
+                const float* rinvstd, const float* rw, float* rdw, float* rdb, int raccumulate, long long M, int C,
+                bf16* dx, bf16* dr, float* scratch, hipStream_t st) {
+  if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32)) return -2;
+  const int TX = pick_tx(C);
+  int gx, gy;
+  long long rpg;
+  stats_grid(M, C, TX, &gx, &gy, &rpg);
+  float* part = scratch;
+  float* rpart = part + (size_t)gy * 2 * C;
+  float* coef = rpart + (size_t)gy * 2 * C;
+  float* rcoef = coef + 3 * C;
+  const dim3 grid(gx, gy);
+  if (TX == 32)
+    bn_bwd_stats_pair_kernel<32><<<grid, BN_THREADS, 0, st>>>(dy, mask, x, mean, r, rmean, M, C, rpg, part, rpart);
+  else if (TX == 16)
+    bn_bwd_stats_pair_kernel<16><<<grid, BN_THREADS, 0, st>>>(dy, mask, x, mean, r, rmean, M, C, rpg, part, rpart);
+  else
+    bn_bwd_stats_pair_kernel<8><<<grid, BN_THREADS, 0, st>>>(dy, mask, x, mean, r, rmean, M, C, rpg, part, rpart);
+  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, gy, M, C, w, invstd, dw, db, accumulate, coef);
+  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(rpart, gy, M, C, rw, rinvstd, rdw, rdb, raccumulate, rcoef);
+  const long long n8 = M * C / 8;
+  const unsigned g = apply_grid(n8);
+  if (256 % (C / 8) == 0)
+    bn_bwd_apply_pair_kernel<true><<<g, 256, 0, st>>>(dy, mask, x, mean, coef, r, rmean, rcoef, n8, C, dx, dr);
+  else
+    bn_bwd_apply_pair_kernel<false><<<g, 256, 0, st>>>(dy, mask, x, mean, coef, r, rmean, rcoef, n8, C, dx, dr);
   return 0;
 }
 

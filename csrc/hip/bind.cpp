@@ -901,6 +901,45 @@ std::vector<at::Tensor> bn_act_fwd_tiles_bnres(at::Tensor x, at::Tensor stats, i
   return {y, mean, invstd, mask, rmean, rinvstd};
 }
 
+// backward of bn_act_fwd_tiles_bnres: [dx, dr, dw, db, drw, drb] from dy and the
+// ReLU bitmask; parameter gradients accumulated into the *_into fp32 tensors when given
+std::vector<at::Tensor> bn_act_bwd_pair(at::Tensor dy, at::Tensor mask, at::Tensor x, at::Tensor mean,
+                                        at::Tensor invstd, at::Tensor w, at::Tensor r, at::Tensor rmean,
+                                        at::Tensor rinvstd, at::Tensor rw, c10::optional<at::Tensor> dw_into,
+                                        c10::optional<at::Tensor> db_into, c10::optional<at::Tensor> rdw_into,
+                                        c10::optional<at::Tensor> rdb_into) {
+  CHECK_BF16(dy); CHECK_BF16(x); CHECK_BF16(r);
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && r.sizes() == x.sizes() &&
+              r.is_contiguous(at::MemoryFormat::ChannelsLast), "bn_act_bwd_pair: channels_last x, r of one shape");
+  const long long C = x.size(1), M = x.numel() / C;
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.numel() == M * C / 8 && mask.is_contiguous(),
+              "bn_act_bwd_pair: mask [M·C/8] uint8");
+  auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  auto dx = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  auto dr = at::empty_like(r, r.options(), at::MemoryFormat::ChannelsLast);
+  auto grads = [&](c10::optional<at::Tensor>& wi, c10::optional<at::Tensor>& bi, at::Tensor& dw, at::Tensor& db) {
+    const bool into = wi && wi->defined() && bi && bi->defined();
+    if (into) {
+      CHECK_F32((*wi)); CHECK_F32((*bi));
+      TORCH_CHECK(wi->numel() == C && bi->numel() == C && wi->is_contiguous() && bi->is_contiguous());
+      dw = *wi;
+      db = *bi;
+    } else {
+      dw = at::empty({C}, w.options());
+      db = at::empty({C}, w.options());
+    }
+    return into ? 1 : 0;
+  };
+  at::Tensor dw, db, rdw, rdb;
+  const int acc = grads(dw_into, db_into, dw, db), racc = grads(rdw_into, rdb_into, rdw, rdb);
+  auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_pair_floats(M, C)}, w.options());
+  CHECK_RC(pdo::bn_bwd_pair(bp(dyc), mask.data_ptr<uint8_t>(), bp(x), fp(mean), fp(invstd), fp(w), fp(dw), fp(db), acc,
+                            bp(r), fp(rmean), fp(rinvstd), fp(rw), fp(rdw), fp(rdb), racc, M, (int)C, bp(dx), bp(dr),
+                            fp(scratch), cur_stream()),
+           "bn_bwd_pair");
+  return {dx, dr, dw, db, rdw, rdb};
+}
+
 // ResNet stem BatchNorm + ReLU + max-pool 3×3/2 from the stem conv's tile statistics:
 // [pooled y, window positions (uint8), xsel (the BatchNorm input at each maximum), mean, invstd]
 std::vector<at::Tensor> bn_relu_pool_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t tile_rows, at::Tensor w,
@@ -1250,6 +1289,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),
         py::arg("db_out") = py::none(), py::arg("saved_grad") = false);
   m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_bwd_pair", &bn_act_bwd_pair);
   m.def("bn_act_fwd_tiles_bnres", &bn_act_fwd_tiles_bnres);
   m.def("bn_act_fwd_tiles", &bn_act_fwd_tiles);
   m.def("conv_ok", &conv_ok);

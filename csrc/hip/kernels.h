@@ -117,6 +117,13 @@ int bn_fwd_tiles_bnres(const float* tile_part, int G, int tile_rows, const bf16*
                        float* rmean, float* rinvstd, float* rss, long long M, int C, int relu, bf16* y,
                        unsigned char* mask, hipStream_t st);
 int bn_fwd_scratch_floats(long long M, int C);
+// backward of bn_fwd_tiles_bnres's pair (ReLU bitmask `mask`): dx, dr and both
+// BatchNorms' dgamma / dbeta, one statistics and one apply pass
+int bn_bwd_scratch_pair_floats(long long M, int C);
+int bn_bwd_pair(const bf16* dy, const unsigned char* mask, const bf16* x, const float* mean, const float* invstd,
+                const float* w, float* dw, float* db, int accumulate, const bf16* r, const float* rmean,
+                const float* rinvstd, const float* rw, float* rdw, float* rdb, int raccumulate, long long M, int C,
+                bf16* dx, bf16* dr, float* scratch, hipStream_t st);
 // ResNet stem BatchNorm + ReLU + 3×3/2 max-pool fused (batchnorm.hip): forward from
 // the conv's tile statistics → pooled y and window positions; backward → dx of the
 // BatchNorm input and dgamma / dbeta (scratch: pool_bn_bwd_scratch_floats)

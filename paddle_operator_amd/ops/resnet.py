@@ -530,7 +530,8 @@ class _BNActBNResFn(torch.autograd.Function):
     (``bn_act_fwd_tiles_bnres``): the downsample branch's normalised activation
     is never written or re-read.  Backward: each BatchNorm's backward from the
     shared output gradient and ReLU bitmask (what the unfused pair did through
-    the residual-mask hand-off)."""
+    the residual-mask hand-off) in one statistics and one apply pass over
+    (dy, mask, x, r): the shared gradient and mask are read once."""
 
     @staticmethod
     def forward(ctx, x, w, b, r, rw, rb, rm, rv, eps, mom, rrm, rrv, reps, rmom, stats, rows, rstats, rrows):
@@ -545,18 +546,21 @@ class _BNActBNResFn(torch.autograd.Function):
     def backward(ctx, dy):
         m = _native.require_hip()
         x, r, mask, mean, invstd, w, b, rmean, rinvstd, rw, rb = ctx.saved_tensors
-        grads = []
-        for (xi, mu, inv, wi, bi), (pw, pb) in (((x, mean, invstd, w, b), ctx.params[:2]),
-                                                ((r, rmean, rinvstd, rw, rb), ctx.params[2:])):
+        into = []
+        for pw, pb in (ctx.params[:2], ctx.params[2:]):
             direct = _direct_ok(pw) and _direct_ok(pb) and pw.grad.dtype == torch.float32
-            dwi, dbi = (pw.grad, pb.grad) if direct else (None, None)
-            dxi, _, dw, db = m.bn_act_bwd(dy, mask, xi, mu, inv, wi, bi, True, False, dwi, dbi)
-            if direct:
+            into.append((pw.grad, pb.grad) if direct else (None, None))
+        # one statistics pass and one apply pass over (dy, mask, x, r) for both
+        dx, dr, dw, db, drw, drb = m.bn_act_bwd_pair(dy, mask, x, mean, invstd, w, r, rmean, rinvstd, rw,
+                                                     *into[0], *into[1])
+        out = []
+        for (pw, pb), (dwi, _), (gw, gb) in zip((ctx.params[:2], ctx.params[2:]), into, ((dw, db), (drw, drb))):
+            if dwi is not None:
                 pw._pdo_ready(pw)
                 pb._pdo_ready(pb)
-                dw = db = None
-            grads.append((dxi, dw, db))
-        (dx, dw, db), (dr, drw, drb) = grads
+                gw = gb = None
+            out.append((gw, gb))
+        (dw, db), (drw, drb) = out
         return dx, dw, db, dr, drw, drb, None, None, None, None, None, None, None, None, None, None, None, None
 
 
