@@ -1017,6 +1017,16 @@ std::vector<at::Tensor> maxpool3s2_fwd(at::Tensor x) {
   return {y, arg};
 }
 
+// dx = the global average pool's input gradient, channels_last [N, C, H, W], from dy [N, C]
+at::Tensor gap_bwd(at::Tensor dy, int64_t H, int64_t W) {
+  CHECK_BF16(dy);
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 2 && dy.is_contiguous() && dy.size(1) % 8 == 0, "gap_bwd: dy [N, C], C % 8 == 0");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  CHECK_RC(pdo::gap_bwd(bp(dy), (int)N, (int)(H * W), (int)C, bp(dx), cur_stream()), "gap_bwd");
+  return dx;
+}
+
 at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W) {
   CHECK_BF16(dy);
   auto dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -1320,6 +1330,7 @@ PYBIND11_MODULE(_pdo_hip, m) {
         py::arg("mean"), py::arg("invstd"),
         py::arg("w"), py::arg("b"), py::arg("dw_into") = py::none(), py::arg("db_into") = py::none());
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.def("gap_bwd", &gap_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("n_head"),
         py::arg("with_bias_grad") = false, py::arg("db_out") = py::none());

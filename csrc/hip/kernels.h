@@ -146,6 +146,8 @@ int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, cons
 // ResNet stem max-pool 3×3/2 pad 1, NHWC bf16 (pool.hip); arg = uint8 window position
 int maxpool3s2_fwd(const bf16* x, int N, int H, int W, int C, bf16* y, uint8_t* arg, hipStream_t st);
 int maxpool3s2_bwd(const bf16* dy, const uint8_t* arg, int N, int H, int W, int C, bf16* dx, hipStream_t st);
+// global average pool backward: dy [N][C] → dx NHWC [N][HW][C] = dy / HW
+int gap_bwd(const bf16* dy, int N, int HW, int C, bf16* dx, hipStream_t st);
 // gemm_dw.hip: C[M][N] (+)= Aᵀ·B for token-major A [T][M], B [T][N] (weight gradients)
 // splits: 0 = shape unsupported; ws: splits·M·N bf16 when splits > 1
 int gemm_dw_splits(long long T, int M, int N);

@@ -89,7 +89,27 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16* __restr
   }
 }
 
+// global average pool backward: dx[n][p][c] = dy[n][c] / HW for every pixel p of
+// an NHWC activation — a pure 16-B-per-lane write stream (the framework's
+// expand + channels_last copy of the broadcast gradient ran at ≈ 1.3 TB/s)
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16* __restrict__ dy, long long n8, int HW, int C8,
+                                                      float inv, bf16* __restrict__ dx) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    const long long n = i / ((long long)HW * C8);
+    const int c8 = (int)(i % C8);
+    const f32x8 g = to_f32(reinterpret_cast<const bf16x8*>(dy)[n * C8 + c8]) * inv;
+    reinterpret_cast<bf16x8*>(dx)[i] = to_bf16(g);
+  }
+}
+
 }  // namespace
+
+int gap_bwd(const bf16* dy, int N, int HW, int C, bf16* dx, hipStream_t st) {
+  if (C % 8 != 0 || N < 1 || HW < 1) return -2;
+  const long long n8 = (long long)N * HW * (C / 8);
+  gap_bwd_kernel<<<stream_grid(n8, 256), 256, 0, st>>>(dy, n8, HW, C / 8, 1.f / (float)HW, dx);
+  return 0;
+}
 
 int maxpool3s2_fwd(const bf16* x, int N, int H, int W, int C, bf16* y, uint8_t* arg, hipStream_t st) {
   if (C % 8 != 0) return -2;

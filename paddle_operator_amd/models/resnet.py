@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import ops
 
@@ -87,7 +86,7 @@ class ResNet(nn.Module):
         # the space-to-depth stem with BatchNorm + ReLU + max-pool fused on the HIP path
         x = ops.conv_bn_relu_maxpool(self.conv1, self.bn1, x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        x = ops.global_avg_pool(x)  # its backward writes the channels_last gradient directly (HIP path)
         return self.fc(x)
 
 

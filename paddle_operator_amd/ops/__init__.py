@@ -21,7 +21,7 @@ from .resnet import (  # noqa: F401
     _BNActBNResFn, _BNLink, _BNReluPoolFn, _CompactGradLink, _ResMaskLink, _StemFn, _BN_FUSED, _DS_FUSED,
     _GEMM_BN_STATS, _BN_LINK, _BN_LINK_USED, _DS_COMPACT, _DS_COMPACT_USED, _HIP_CONV, _HIP_STEM, _RES_MASK,
     _RES_MASK_USED, _STEM_POOL, _apply_bitmask, _stem_ok, bn_act, conv1x1, conv_bn_act, conv_bn_ds_act,
-    conv_bn_relu_maxpool,
+    conv_bn_relu_maxpool, global_avg_pool,
     max_pool_3x3s2)
 
 __all__ = [

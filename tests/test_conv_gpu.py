@@ -619,3 +619,22 @@ def test_downsample_block_bn_pair_in_one_apply(cin, width, stride, hw):
     for (n, pa), (_, pb), (_, pf) in zip(a.named_parameters(), b.named_parameters(), f.named_parameters()):
         e_fused, e_two = _rel(pa.grad.float(), pf.grad), _rel(pb.grad.float(), pf.grad)
         assert e_fused < 0.15 and e_fused <= 1.25 * e_two + 1e-3, (n, e_fused, e_two)
+
+
+@pytest.mark.parametrize("N,C,HW", [(256, 2048, 7), (4, 64, 5)])
+def test_global_avg_pool_channels_last_grad(N, C, HW):
+    """ops.global_avg_pool (HIP backward: dy / HW written straight into a
+    channels_last gradient) against the framework's adaptive_avg_pool2d in fp32."""
+    from paddle_operator_amd import ops
+
+    x = torch.randn(N, C, HW, HW, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_()
+    y = ops.global_avg_pool(xa)
+    dy = torch.randn(N, C, device="cuda").bfloat16()
+    y.backward(dy)
+    xr = x.float().requires_grad_()
+    yr = torch.flatten(torch.nn.functional.adaptive_avg_pool2d(xr, 1), 1)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=8e-3, atol=1e-6)

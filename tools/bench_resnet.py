@@ -19,6 +19,11 @@ def main():
     a = ap.parse_args()
     import torch
     from paddle_operator_amd.workloads.resnet import ResNetTrainer
+    if os.environ.get("BENCH_GAP_FRAMEWORK") == "1":  # A/B: the framework's average pool (and its backward copies)
+        import torch.nn.functional as F
+
+        from paddle_operator_amd import ops
+        ops.global_avg_pool = lambda x: torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
     t0 = time.time()
     tr = ResNetTrainer(a.batch, "cuda:0")
     for _ in range(a.warmup):
