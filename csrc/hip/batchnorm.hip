@@ -445,6 +445,35 @@ __device__ __forceinline__ f32x8 block_sum256(f32x8 v, f32x8* red) {
   return t;
 }
 
+// Large partial counts (G > 512: layer 1's 56 × 56 convolutions, the stem) are
+// first merged per 256 partial rows by a 2-D grid — (Σ, M2 about the chunk
+// mean) of 256·tile_rows rows — so the finalize's one block per 8 channels
+// walks G / 256 rows instead of G (its serial per-lane loads dominated: 20-74
+// µs per call at those G)
+constexpr int MERGE_MIN_G = 512, MERGE_CHUNK = 256;
+__device__ __forceinline__ f32x8 block_sum256(f32x8 v, f32x8* red);
+
+__global__ __launch_bounds__(256) void bn_merge_tiles_kernel(const float* __restrict__ part, int G, int tile_rows,
+                                                             long long M, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * 8, sidx = blockIdx.y;
+  const int g0 = sidx * MERGE_CHUNK, g = g0 + threadIdx.x;
+  __shared__ f32x8 red[4];
+  const f32x8 z = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool live = g < G;
+  const f32x8 sum = live ? *reinterpret_cast<const f32x8*>(part + (size_t)g * 2 * C + c) : z;
+  const f32x8 m2 = live ? *reinterpret_cast<const f32x8*>(part + (size_t)g * 2 * C + C + c) : z;
+  const long long r0 = (long long)g * tile_rows, cr0 = (long long)g0 * tile_rows;
+  const float n = live ? (float)(M - r0 < tile_rows ? M - r0 : tile_rows) : 1.f;
+  const long long cn = M - cr0 < (long long)MERGE_CHUNK * tile_rows ? M - cr0 : (long long)MERGE_CHUNK * tile_rows;
+  const f32x8 S = block_sum256(sum, red);
+  const f32x8 d = sum * (1.f / n) - S * (1.f / (float)cn);
+  const f32x8 Q = block_sum256(live ? m2 + n * d * d : z, red);
+  if (threadIdx.x == 0) {
+    *reinterpret_cast<f32x8*>(out + (size_t)sidx * 2 * C + c) = S;
+    *reinterpret_cast<f32x8*>(out + (size_t)sidx * 2 * C + C + c) = Q;
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_tiles_kernel(const float* __restrict__ part, int G, int tile_rows,
                                                                 long long M, int C, const float* __restrict__ w,
                                                                 const float* __restrict__ b, float eps,
@@ -698,13 +727,33 @@ int bn_fwd(const bf16* x, const bf16* res, const float* w, const float* b, float
 
 // BatchNorm forward whose statistics came with the producing convolution
 // (conv.hip tile partials): finalize + apply, no statistics pass over x
+int bn_tiles_merge_floats(int G, int C) {
+  return G > MERGE_MIN_G ? (G + MERGE_CHUNK - 1) / MERGE_CHUNK * 2 * C : 0;
+}
+
+// finalize from [G][2][C] tile partials, pre-merged through `merge`
+// (bn_tiles_merge_floats floats, or nullptr) when G is large
+static void finalize_tiles(const float* part, int G, int tile_rows, long long M, int C, const float* w, const float* b,
+                           float eps, float momentum, float* rm, float* rv, float* mean, float* invstd, float* ss,
+                           float* merge, hipStream_t st) {
+  if (merge && G > MERGE_MIN_G) {
+    const int S = (G + MERGE_CHUNK - 1) / MERGE_CHUNK;
+    bn_merge_tiles_kernel<<<dim3(C / 8, S), 256, 0, st>>>(part, G, tile_rows, M, C, merge);
+    part = merge;
+    G = S;
+    tile_rows *= MERGE_CHUNK;
+  }
+  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(part, G, tile_rows, M, C, w, b, eps, momentum, rm, rv, mean, invstd,
+                                                  ss);
+}
+
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
                  float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st,
-                 unsigned char* mask) {
+                 unsigned char* mask, float* merge) {
   if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1) return -2;
-  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
-                                                  running_var, mean, invstd, ss);
+  finalize_tiles(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean, running_var, mean, invstd, ss, merge,
+                 st);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
   if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, res, ss, n8, C, relu, y, mask, nullptr);
@@ -720,12 +769,13 @@ int bn_fwd_tiles_bnres(const float* tile_part, int G, int tile_rows, const bf16*
                        float* ss, const float* rtile_part, int rG, int rtile_rows, const bf16* r, const float* rw,
                        const float* rb, float* rrunning_mean, float* rrunning_var, float reps, float rmomentum,
                        float* rmean, float* rinvstd, float* rss, long long M, int C, int relu, bf16* y,
-                       unsigned char* mask, hipStream_t st) {
+                       unsigned char* mask, hipStream_t st, float* merge) {
   if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1 || rG < 1) return -2;
-  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
-                                                  running_var, mean, invstd, ss);
-  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(rtile_part, rG, rtile_rows, M, C, rw, rb, reps, rmomentum,
-                                                  rrunning_mean, rrunning_var, rmean, rinvstd, rss);
+  // (one merge buffer serves both: the second merge is stream-ordered after the first finalize)
+  finalize_tiles(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean, running_var, mean, invstd, ss, merge,
+                 st);
+  finalize_tiles(rtile_part, rG, rtile_rows, M, C, rw, rb, reps, rmomentum, rrunning_mean, rrunning_var, rmean, rinvstd,
+                 rss, merge, st);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
   if (256 % (C / 8) == 0) bn_apply_kernel<true><<<g, 256, 0, st>>>(x, r, ss, n8, C, relu, y, mask, rss);
@@ -827,11 +877,11 @@ static bool pool_bn_ok(int N, int H, int W, int C) {
 int bn_relu_pool_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
                            float* running_mean, float* running_var, int N, int H, int W, int C, float eps,
                            float momentum, bf16* y, uint8_t* arg, bf16* xsel, float* mean, float* invstd, float* ss,
-                           hipStream_t st) {
+                           hipStream_t st, float* merge) {
   if (!pool_bn_ok(N, H, W, C) || G < 1) return -2;
   const long long M = (long long)N * H * W;
-  bn_finalize_tiles_kernel<<<C / 8, 256, 0, st>>>(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean,
-                                                  running_var, mean, invstd, ss);
+  finalize_tiles(tile_part, G, tile_rows, M, C, w, b, eps, momentum, running_mean, running_var, mean, invstd, ss, merge,
+                 st);
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   const int tot = N * OH * OW * (C / 8);
   bn_relu_pool_fwd_kernel<<<(unsigned)min((tot + 255) / 256, 8192), 256, 0, st>>>(x, ss, N, H, W, C, OH, OW, y, arg,

@@ -857,9 +857,13 @@ std::vector<at::Tensor> bn_act_fwd_tiles(at::Tensor x, at::Tensor stats, int64_t
   float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
   at::Tensor mask;
   if (relu && rp) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  const int mf = pdo::bn_tiles_merge_floats((int)stats.size(0), (int)C);
+  at::Tensor merge;
+  if (mf) merge = at::empty({mf}, w.options());
   CHECK_RC(pdo::bn_fwd_tiles(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), rp, fp(w), fp(b), rmp, rvp, M,
                              (int)C, (float)eps, (float)momentum, relu ? 1 : 0, bp(y), fp(mean), fp(invstd), fp(ss),
-                             cur_stream(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr), "bn_fwd_tiles");
+                             cur_stream(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
+                             mf ? fp(merge) : nullptr), "bn_fwd_tiles");
   return {y, mean, invstd, mask};
 }
 
@@ -891,12 +895,16 @@ std::vector<at::Tensor> bn_act_fwd_tiles_bnres(at::Tensor x, at::Tensor stats, i
   at::Tensor mask;
   if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   auto opt = [](c10::optional<at::Tensor>& t) { return t && t->defined() ? fp(*t) : nullptr; };
+  const int mf = std::max(pdo::bn_tiles_merge_floats((int)stats.size(0), (int)C),
+                          pdo::bn_tiles_merge_floats((int)rstats.size(0), (int)C));
+  at::Tensor merge;
+  if (mf) merge = at::empty({mf}, w.options());
   CHECK_RC(pdo::bn_fwd_tiles_bnres(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), fp(w), fp(b), opt(rm), opt(rv),
                                    (float)eps, (float)momentum, fp(mean), fp(invstd), fp(ss), fp(rstats),
                                    (int)rstats.size(0), (int)rtile_rows, bp(r), fp(rw), fp(rb), opt(rrm), opt(rrv),
                                    (float)reps, (float)rmomentum, fp(rmean), fp(rinvstd), fp(rss), M, (int)C,
                                    relu ? 1 : 0, bp(y), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr,
-                                   cur_stream()),
+                                   cur_stream(), mf ? fp(merge) : nullptr),
            "bn_fwd_tiles_bnres");
   return {y, mean, invstd, mask, rmean, rinvstd};
 }
@@ -960,9 +968,13 @@ std::vector<at::Tensor> bn_relu_pool_fwd_tiles(at::Tensor x, at::Tensor stats, i
   auto ss = at::empty({2 * C}, w.options());
   float* rmp = rm && rm->defined() ? fp(*rm) : nullptr;
   float* rvp = rv && rv->defined() ? fp(*rv) : nullptr;
+  const int mf = pdo::bn_tiles_merge_floats((int)stats.size(0), (int)C);
+  at::Tensor merge;
+  if (mf) merge = at::empty({mf}, w.options());
   CHECK_RC(pdo::bn_relu_pool_fwd_tiles(fp(stats), (int)stats.size(0), (int)tile_rows, bp(x), fp(w), fp(b), rmp, rvp,
                                        (int)N, (int)H, (int)W, (int)C, (float)eps, (float)momentum, bp(y),
-                                       arg.data_ptr<uint8_t>(), bp(xsel), fp(mean), fp(invstd), fp(ss), cur_stream()),
+                                       arg.data_ptr<uint8_t>(), bp(xsel), fp(mean), fp(invstd), fp(ss), cur_stream(),
+                                       mf ? fp(merge) : nullptr),
            "bn_relu_pool_fwd_tiles");
   return {y, arg, xsel, mean, invstd};
 }

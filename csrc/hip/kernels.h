@@ -108,14 +108,17 @@ int stem_wgrad(const bf16* dy, const bf16* z, int N, int IH, int IW, int Kout, f
                float* scratch, hipStream_t st);
 int bn_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const bf16* res, const float* w,
                  const float* b, float* running_mean, float* running_var, long long M, int C, float eps,
-                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st, unsigned char* mask = nullptr);
+                 float momentum, int relu, bf16* y, float* mean, float* invstd, float* ss, hipStream_t st, unsigned char* mask = nullptr,
+                 float* merge = nullptr);
+// floats of the pre-merge buffer the *_tiles BatchNorm forwards take for G partial rows (0: none needed)
+int bn_tiles_merge_floats(int G, int C);
 // act(BN(x) + BN_r(r)): both from their convolutions' tile statistics, one apply pass
 int bn_fwd_tiles_bnres(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
                        float* running_mean, float* running_var, float eps, float momentum, float* mean, float* invstd,
                        float* ss, const float* rtile_part, int rG, int rtile_rows, const bf16* r, const float* rw,
                        const float* rb, float* rrunning_mean, float* rrunning_var, float reps, float rmomentum,
                        float* rmean, float* rinvstd, float* rss, long long M, int C, int relu, bf16* y,
-                       unsigned char* mask, hipStream_t st);
+                       unsigned char* mask, hipStream_t st, float* merge = nullptr);
 int bn_fwd_scratch_floats(long long M, int C);
 // backward of bn_fwd_tiles_bnres's pair (ReLU bitmask `mask`): dx, dr and both
 // BatchNorms' dgamma / dbeta, one statistics and one apply pass
@@ -130,7 +133,7 @@ int bn_bwd_pair(const bf16* dy, const unsigned char* mask, const bf16* x, const 
 int bn_relu_pool_fwd_tiles(const float* tile_part, int G, int tile_rows, const bf16* x, const float* w, const float* b,
                            float* running_mean, float* running_var, int N, int H, int W, int C, float eps,
                            float momentum, bf16* y, uint8_t* arg, bf16* xsel, float* mean, float* invstd, float* ss,
-                           hipStream_t st);
+                           hipStream_t st, float* merge = nullptr);
 int pool_bn_bwd_scratch_floats(int N, int H, int W, int C);
 int pool_bn_bwd(const bf16* dy, const bf16* y, const bf16* xsel, const uint8_t* arg, const bf16* x, const float* mean,
                 const float* invstd, const float* w, const float* b, int N, int H, int W, int C, bf16* dx, float* dw,
