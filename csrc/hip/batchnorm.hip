@@ -785,11 +785,38 @@ int bn_fwd_tiles_bnres(const float* tile_part, int G, int tile_rows, const bf16*
 
 // BatchNorm backward whose statistics (Σg, Σg·(x − mean) partials [G][2][C])
 // came with the input gradient that produced dy (conv.hip): finalize + apply
+// backward partials [G][2][C] pre-summed per 256 rows (the same large-G
+// serial-load problem as the forward finalize; plain sums, no merge formula)
+__global__ __launch_bounds__(256) void bn_sum_rows_kernel(const float* __restrict__ part, int G, int C,
+                                                          float* __restrict__ out) {
+  const int c = blockIdx.x * 8, sidx = blockIdx.y, g = sidx * MERGE_CHUNK + threadIdx.x;
+  __shared__ f32x8 red[4];
+  const f32x8 z = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool live = g < G;
+  const f32x8 a = block_sum256(live ? *reinterpret_cast<const f32x8*>(part + (size_t)g * 2 * C + c) : z, red);
+  const f32x8 b = block_sum256(live ? *reinterpret_cast<const f32x8*>(part + (size_t)g * 2 * C + C + c) : z, red);
+  if (threadIdx.x == 0) {
+    *reinterpret_cast<f32x8*>(out + (size_t)sidx * 2 * C + c) = a;
+    *reinterpret_cast<f32x8*>(out + (size_t)sidx * 2 * C + C + c) = b;
+  }
+}
+
+static void bwd_finalize(const float* part, int G, long long M, int C, const float* w, const float* invstd, float* dw,
+                         float* db, int accumulate, float* coef, float* merge, hipStream_t st) {
+  if (merge && G > MERGE_MIN_G) {
+    const int S = (G + MERGE_CHUNK - 1) / MERGE_CHUNK;
+    bn_sum_rows_kernel<<<dim3(C / 8, S), 256, 0, st>>>(part, G, C, merge);
+    part = merge;
+    G = S;
+  }
+  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, G, M, C, w, invstd, dw, db, accumulate, coef);
+}
+
 int bn_bwd_part(const float* part, int G, const bf16* dy, const bf16* y, const bf16* x, const float* mean,
                 const float* invstd, const float* w, const float* b, long long M, int C, int relu, bf16* dx,
-                bf16* dres, float* dw, float* db, int accumulate, float* coef, hipStream_t st) {
+                bf16* dres, float* dw, float* db, int accumulate, float* coef, hipStream_t st, float* merge) {
   if (C % 8 != 0 || M < 1 || M * C / 8 >= (1ll << 32) || G < 1) return -2;
-  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, G, M, C, w, invstd, dw, db, accumulate, coef);
+  bwd_finalize(part, G, M, C, w, invstd, dw, db, accumulate, coef, merge, st);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
   if (256 % (C / 8) == 0)
@@ -803,7 +830,7 @@ int bn_bwd_scratch_floats(long long M, int C) {
   int gx, gy;
   long long rpg;
   stats_grid(M, C, pick_tx(C), &gx, &gy, &rpg);
-  return gy * 2 * C + 3 * C;
+  return gy * 2 * C + 3 * C + bn_tiles_merge_floats(gy, C);
 }
 
 int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, const float* invstd, const float* w,
@@ -823,7 +850,7 @@ int bn_bwd(const bf16* dy, const bf16* y, const bf16* x, const float* mean, cons
     bn_bwd_stats_kernel<16><<<grid, BN_THREADS, 0, st>>>(dy, y, x, mean, invstd, w, b, M, C, rpg, relu, part);
   else
     bn_bwd_stats_kernel<8><<<grid, BN_THREADS, 0, st>>>(dy, y, x, mean, invstd, w, b, M, C, rpg, relu, part);
-  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, gy, M, C, w, invstd, dw, db, accumulate, coef);
+  bwd_finalize(part, gy, M, C, w, invstd, dw, db, accumulate, coef, coef + 3 * C, st);  // merge region follows coef
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
   if (256 % (C / 8) == 0)
@@ -858,8 +885,9 @@ int bn_bwd_pair(const bf16* dy, const unsigned char* mask, const bf16* x, const 
     bn_bwd_stats_pair_kernel<16><<<grid, BN_THREADS, 0, st>>>(dy, mask, x, mean, r, rmean, M, C, rpg, part, rpart);
   else
     bn_bwd_stats_pair_kernel<8><<<grid, BN_THREADS, 0, st>>>(dy, mask, x, mean, r, rmean, M, C, rpg, part, rpart);
-  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, gy, M, C, w, invstd, dw, db, accumulate, coef);
-  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(rpart, gy, M, C, rw, rinvstd, rdw, rdb, raccumulate, rcoef);
+  // (scratch = 2 × bn_bwd_scratch_floats: a merge region follows rcoef; stream order lets both use it)
+  bwd_finalize(part, gy, M, C, w, invstd, dw, db, accumulate, coef, rcoef + 3 * C, st);
+  bwd_finalize(rpart, gy, M, C, rw, rinvstd, rdw, rdb, raccumulate, rcoef, rcoef + 3 * C, st);
   const long long n8 = M * C / 8;
   const unsigned g = apply_grid(n8);
   if (256 % (C / 8) == 0)
@@ -894,7 +922,7 @@ int pool_bn_bwd_scratch_floats(int N, int H, int W, int C) {
   int gx, gy;
   long long rpg;
   stats_grid(Mp, C, pick_tx(C), &gx, &gy, &rpg);
-  return gy * 2 * C + 3 * C;
+  return gy * 2 * C + 3 * C + bn_tiles_merge_floats(gy, C);
 }
 
 int pool_bn_bwd(const bf16* dy, const bf16* y, const bf16* xsel, const uint8_t* arg, const bf16* x, const float* mean,
@@ -915,8 +943,7 @@ int pool_bn_bwd(const bf16* dy, const bf16* y, const bf16* xsel, const uint8_t* 
   else if (TX == 16) bn_bwd_stats_kernel<16><<<grid, BN_THREADS, 0, st>>>(dy, y, xsel, mean, invstd, w, b, Mp, C, rpg, 1, part);
   else bn_bwd_stats_kernel<8><<<grid, BN_THREADS, 0, st>>>(dy, y, xsel, mean, invstd, w, b, Mp, C, rpg, 1, part);
   // ... normalised by the BatchNorm's full-resolution count
-  bn_bwd_finalize_kernel<<<C / 8, FIN_THREADS, 0, st>>>(part, gy, (long long)N * H * W, C, w, invstd, dw, db,
-                                                        accumulate, coef);
+  bwd_finalize(part, gy, (long long)N * H * W, C, w, invstd, dw, db, accumulate, coef, coef + 3 * C, st);
   const int tot = N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
   pool_bn_bwd_apply_kernel<<<(unsigned)min((tot + 255) / 256, 8192), 256, 0, st>>>(dy, arg, x, mean, invstd, w, b,
                                                                                   coef, N, H, W, C, OH, OW, dx);

@@ -622,10 +622,11 @@ static std::vector<at::Tensor> bn_act_bwd_impl(at::Tensor dy, c10::optional<at::
     CHECK_F32((*part));
     TORCH_CHECK(part->dim() == 3 && part->size(1) == 2 && part->size(2) == C && part->is_contiguous(),
                 "bn_act_bwd_part: partials [G, 2, C]");
-    auto coef = at::empty({3 * C}, w.options());
+    const int mf = pdo::bn_tiles_merge_floats((int)part->size(0), (int)C);
+    auto coef = at::empty({3 * C + mf}, w.options());  // + the merge region for a large partial count
     CHECK_RC(pdo::bn_bwd_part(fp(*part), (int)part->size(0), bp(dyc), yp, bp(x), fp(mean), fp(invstd), fp(w), fp(b), M,
                               (int)C, rmode, bp(dx), want_dres ? bp(dres) : nullptr, fp(dw), fp(db),
-                              into ? 1 : 0, fp(coef), cur_stream()),
+                              into ? 1 : 0, fp(coef), cur_stream(), mf ? fp(coef) + 3 * C : nullptr),
              "bn_bwd_part");
   } else {
     auto scratch = at::empty({(long long)pdo::bn_bwd_scratch_floats(M, C)}, w.options());

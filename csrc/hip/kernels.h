@@ -88,7 +88,8 @@ int conv_dgrad_nhwc(const bf16* dy, int N, int H, int W, int C, const bf16* wt, 
                     int pad, bf16* dx, hipStream_t st, const ConvBnBwd* bn = nullptr, const bf16* add = nullptr);
 int bn_bwd_part(const float* part, int G, const bf16* dy, const bf16* y, const bf16* x, const float* mean,
                 const float* invstd, const float* w, const float* b, long long M, int C, int relu, bf16* dx,
-                bf16* dres, float* dw, float* db, int accumulate, float* coef, hipStream_t st);
+                bf16* dres, float* dw, float* db, int accumulate, float* coef, hipStream_t st,
+                float* merge = nullptr);  // merge: bn_tiles_merge_floats(G, C) floats for a large G
 long long conv_wgrad_scratch_floats(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad);
 int conv_wgrad_nhwc(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Kout, int R, int S, int stride,
                     int pad, float* dw, int accumulate, float* scratch, hipStream_t st);
