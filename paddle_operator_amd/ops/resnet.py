@@ -216,6 +216,17 @@ def bn_act(bn: torch.nn.BatchNorm2d, x, relu: bool = True, residual=None, rlink=
     return F.relu(y) if relu else y
 
 
+def _direct_cl_ok(p) -> bool:
+    """A convolution weight's fp32 arena gradient takes the kernel's direct
+    (accumulating) write: ``_direct_ok`` but for the channels_last [K, C, R, S]
+    view the arena keeps for a channels_last weight (``_direct_ok`` asks for the
+    NCHW-contiguous layout, which a 3×3 or the stem's 7×7 view is not — those
+    went through a temporary and an AccumulateGrad add)."""
+    g = p.grad
+    return (getattr(p, "_pdo_direct", False) and g is not None and not torch.is_grad_enabled()
+            and g.dtype == torch.float32 and g.is_contiguous(memory_format=torch.channels_last))
+
+
 def _gemm_fwd_1x1(m, T, C, K) -> bool:
     """1×1 stride-1 forward on the token-major GEMM (gemm_nt) rather than the
     implicit GEMM: measured faster for every ResNet-50 shape with K > 128 output
@@ -377,8 +388,7 @@ class _ConvFn(torch.autograd.Function):
                     g = None
             if g is not None:
                 dw = g.view(K, C, 1, 1).to(p.dtype)
-            elif (_direct_ok(p) and p.grad.dtype == torch.float32
-                    and p.grad.is_contiguous(memory_format=torch.channels_last)):
+            elif _direct_cl_ok(p):
                 m.conv_wgrad(dy, x, R, S, ctx.stride, ctx.pad, out=p.grad)
                 p._pdo_ready(p)
             else:
@@ -441,7 +451,7 @@ class _StemFn(torch.autograd.Function):
         dw = None
         if dy is not None and ctx.needs_input_grad[1]:
             dy = dy.contiguous(memory_format=torch.channels_last)
-            if _direct_ok(p) and p.grad.dtype == torch.float32 and p.grad.is_contiguous(memory_format=torch.channels_last):
+            if _direct_cl_ok(p):
                 m.stem_wgrad(dy, z, p.grad)
                 p._pdo_ready(p)
             else:

@@ -24,6 +24,11 @@ def main():
 
         from paddle_operator_amd import ops
         ops.global_avg_pool = lambda x: torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+    if os.environ.get("BENCH_CONV_DIRECT_NCHW") == "1":  # A/B: the round-5-earlier direct-write rule for conv weights
+        from paddle_operator_amd.ops import core as ops_core
+        from paddle_operator_amd.ops import resnet as ops_resnet
+        ops_resnet._direct_cl_ok = lambda p: (ops_core._direct_ok(p) and p.grad.dtype == torch.float32
+                                              and p.grad.is_contiguous(memory_format=torch.channels_last))
     t0 = time.time()
     tr = ResNetTrainer(a.batch, "cuda:0")
     for _ in range(a.warmup):
