@@ -309,11 +309,11 @@ _NT_GELU = [True]
 
 
 # fc2 input gradient with the fused GELU' epilogue (gemm_nt) where its shape
-# contract holds; PDO_NT_DGELU=0 restores hipBLASLt + the bias-GELU kernel.
+# contract holds; False (test hook) restores hipBLASLt + the bias-GELU kernel.
 _NT_DGELU = [True]
 
 # _NTMLPFn saves gelu' from the fc1 epilogue (EPI 7 / 8) instead of the
-# pre-activation; PDO_NT_GD=0 = the recomputing pair (EPI 2 / 3), the A/B alternative
+# pre-activation; the environment switch off = the recomputing pair (EPI 2 / 3), the A/B alternative
 _NT_GD = [os.environ.get("PDO_NT_GD", "1") != "0"]
 
 
@@ -427,7 +427,7 @@ _QKV_FUSED = [True]
 
 def qkv_attention(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, n_head: int) -> torch.Tensor:
     """attention(linear(h, w, b)) — fused QKV-bias gradient on the HIP path
-    (PDO_QKV_FUSED=0: separate linear + attention nodes)."""
+    (``_QKV_FUSED`` off: separate linear + attention nodes)."""
     S, C3 = h.shape[-2], w.shape[0]
     if _QKV_FUSED[0] and use_hip(h) and b is not None and (C3 // 3) // n_head == 64 and S % 128 == 0 and h.dim() == 3:
         return _QKVAttnFn.apply(h, w, b, n_head)
@@ -485,7 +485,7 @@ class _LMHeadXentFn(torch.autograd.Function):
     token chunks: per chunk the logits GEMM (gemm_nt4), the softmax statistics,
     dlogits written in place, the chunk's dX GEMM and its dW GEMM accumulated
     into one [Vp, C] gradient — so only a [chunk, Vp] logits buffer exists.
-    The chunk is ``PDO_LM_CHUNK`` tokens (``lm_head_xent``): 16384 caps the
+    The chunk is ``_LM_CHUNK`` tokens (``lm_head_xent``): 16384 caps the
     buffer at 1.6 GB; the default (-1) is one chunk of every token, i.e. the
     whole [tokens, Vp] logits tensor (6.6 GB at GPT-2-medium B = 64), which
     ran 0.5 ms/step faster (profiles/r3_xent_fused.md).  The gradients are
@@ -605,7 +605,7 @@ def _lm_head_loss_only(h, w, target, vocab: int, chunk: int):
     return loss_sum / cnt.clamp(min=1.0)
 
 
-# PDO_LM_CHUNK=tokens: the chunked LM head + cross-entropy (_LMHeadXentFn); -1
+# the LM-head token chunk: the chunked LM head + cross-entropy (_LMHeadXentFn); -1
 # (default) = one chunk of every token: the LM head, the one-kernel cross-entropy
 # (xent_fused) and the dX / dW GEMMs in the forward, dloss applied to dX / dW in the
 # backward — 143.55 vs 144.04 ms/step against the separate linear + cross_entropy

@@ -236,7 +236,7 @@ def _gemm_fwd_1x1(m, T, C, K) -> bool:
 
 
 # the 1×1 forward on gemm_nt takes the BatchNorm statistics in its epilogue
-# (gemm_nt4 EPI 9) where the 4-wave mainloop runs it; PDO_GEMM_BN_STATS=0 = a
+# (gemm_nt EPI 9); the environment switch off = a
 # separate statistics pass over the output (the A/B alternative)
 _GEMM_BN_STATS = [os.environ.get("PDO_GEMM_BN_STATS", "1") != "0"]
 
