@@ -514,9 +514,10 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   if (tiles > 0x7fffffffLL) return -2;
   const int nk = K / BK;
   if (nk < 4 || nk % 2) return -2;  // the mainloop runs k-tiles in pairs, at least two
-  // 8: group_m sweep (tools/nt4_probe.py; in the step: tools/gpu.sh stepab, 8 ahead of 4 and 16) on the GPT-2
-  // NT shapes (row-major = 1: wide K = 1024 GEMM 501 -> 451 us, fc2 dX ⊙ GELU' 642 -> 607, qkv 433 -> 419)
-  constexpr int group_m = 8;
+  // 4 since round 5 (with the saved-gelu' / BatchNorm-statistics epilogues): GPT-2-medium step 145.511 /
+  // 145.624 / 145.680 / 145.716 (8) vs 145.498 / 145.392 / 145.501 / 145.406 ms (4), 16 +3.2 ms
+  // (soab, profiles/r5gd_saved_gelu_grad.md); round 3 had 8 ahead of 4 and 16 on the older epilogues
+  constexpr int group_m = 4;
   const int g = persistent_grid(tiles);
   auto go = [&](auto kern) {
     kern<<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m);
