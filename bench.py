@@ -109,9 +109,12 @@ def parse_args(argv=None):
                          "xGMI layout: under a device plugin only GPUs of one pod see each other)")
     ap.add_argument("--ops", choices=["hip", "torch"], default=os.environ.get("PDO_OPS", "hip"))
     ap.add_argument("--secondary-resnet", type=int, default=int(os.environ.get("PDO_BENCH_RESNET", "1")),
-                    help="after the GPT-2 job (GPUs only): a ResNet-50 job (configs 2/3, batch 256 per GPU, 20 timed "
-                         "steps) on the same ranks, reported under 'secondary' — 1: at one GPU only, 2: at every N, "
-                         "0: skip")
+                    help="after the GPT-2 job (GPU or virtual-GPU nodes): a ResNet-50 job (configs 2/3: "
+                         "deploy/examples/resnet.yaml, batch 256 per GPU, 20 timed steps) on the same N ranks, reported "
+                         "under 'secondary' — 1: run it, 0: skip")
+    ap.add_argument("--gang", choices=["auto", "on", "off"], default="auto",
+                    help="Volcano gang scheduling of the benchmark jobs (config 4: PodGroup minMember=N, "
+                         "reference controllers/paddlejob_helper.go:478-549): auto = on for N > 1")
     ap.add_argument("--timeout", type=float, default=900.0, help="per-job limit (s)")
     ap.add_argument("--keep", action="store_true", help="keep the sandbox (rank logs)")
     ap.add_argument("--ready-only", action="store_true", help="only the ready trials (prints their record)")
@@ -129,7 +132,7 @@ def parse_args(argv=None):
 class Launcher:
     """One in-process local backend; launches PaddleJobs and reads pdo-kv."""
 
-    def __init__(self, mode, zygote, gpus, sandbox, extra_args=(), nproc=1, cpu_threads=0):
+    def __init__(self, mode, zygote, gpus, sandbox, extra_args=(), nproc=1, cpu_threads=0, volcano=False):
         from paddle_operator_amd.controller import LocalCluster
         from paddle_operator_amd.kv.client import KVClient
 
@@ -140,9 +143,11 @@ class Launcher:
         self.extra_args = list(extra_args)
         self.nproc = nproc  # ranks per pod (--nproc-per-pod; amd.com/gpu per pod)
         self.cpu_threads = cpu_threads  # --virtual-gpus: CPU ranks behind GPU requests
+        self.volcano = volcano
         self.cl = LocalCluster(mode=mode, agent="exec", sandbox_root=sandbox,
                                nodes=[{"name": "node0", "gpus": gpus}],
-                               kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote)
+                               kv_endpoint=f"127.0.0.1:{self.port}", zygote=zygote, volcano=volcano)
+        self.gang_log = {}  # job -> PodGroup observations (wait_records)
         self.cl.serve(f"127.0.0.1:{self.port}")
         self.cl.start()
         self.kv = KVClient(f"127.0.0.1:{self.port}")
@@ -155,7 +160,7 @@ class Launcher:
                 time.sleep(0.05)
             log(f"zygote ready in {time.time() - t0:.1f}s")
 
-    def container(self, args, ops):
+    def container(self, args, ops, scheduler=None):
         from paddle_operator_amd.api import types as T
         env = [{"name": "PYTHONPATH", "value": REPO}, {"name": "PDO_KV", "value": f"127.0.0.1:{self.port}"},
                {"name": "PDO_PYTHON", "value": sys.executable}, {"name": "PDO_OPS", "value": ops}]
@@ -167,14 +172,25 @@ class Launcher:
             c["resources"] = {"limits": {T.AMD_GPU: self.nproc}}
         return c
 
-    def launch(self, name, ranks, args, ops):
+    def launch(self, name, ranks, args, ops, gang=False):
+        """``gang``: the job goes through the Volcano path (PodGroup with
+        minMember = pods, all-or-nothing binding by the gang scheduler); else,
+        on a volcano-enabled cluster, it opts out with the default scheduler
+        (builders.cpp without_volcano), as the ready trials do."""
         from paddle_operator_amd.api import types as T
         args = list(args) + self.extra_args
         if self.nproc > 1:
             args += ["--nproc-per-pod", str(self.nproc)]
-        job = T.paddlejob(name, worker={"replicas": ranks // self.nproc,
-                                        "template": {"spec": {"containers": [self.container(args, ops)]}}},
-                          clean_pod_policy="Always")
+        pods = ranks // self.nproc
+        spec = {"containers": [self.container(args, ops)]}
+        policy = None
+        if self.volcano and gang:
+            policy = {"minAvailable": pods, "queue": "default"}
+            self.gang_log[name] = {"phases": [], "bound_before_inqueue": 0, "min_member": None}
+        elif self.volcano:
+            spec["schedulerName"] = "default-scheduler"
+        job = T.paddlejob(name, worker={"replicas": pods, "template": {"spec": spec}},
+                          clean_pod_policy="Always", scheduling_policy=policy)
         t0 = time.time()
         self.cl.create(job)
         return t0
@@ -186,6 +202,8 @@ class Launcher:
         beat = time.time() + 30
         while time.time() < deadline:
             recs = self.kv.get_prefix(prefix)
+            if name in self.gang_log:
+                self._watch_gang(name)
             if len(recs) >= n:
                 return [json.loads(v) for v in recs.values()]
             phase = ((self.cl.job(name) or {}).get("status") or {}).get("phase")
@@ -198,6 +216,25 @@ class Launcher:
         self.dump_logs(name)
         raise RuntimeError(f"{name}: {len(recs)}/{n} {kind} records (phase "
                            f"{((self.cl.job(name) or {}).get('status') or {}).get('phase')})")
+
+    def _watch_gang(self, name):
+        """PodGroup phase sequence, and whether any pod was bound to a node
+        while its PodGroup was not yet admitted (Inqueue / Running)."""
+        g = self.gang_log[name]
+        if g.get("admitted"):
+            return
+        pg = self.cl.get("PodGroup", name)
+        if pg is None:
+            return
+        ph = (pg.get("status") or {}).get("phase") or "Pending"
+        g["min_member"] = (pg.get("spec") or {}).get("minMember")
+        if not g["phases"] or g["phases"][-1] != ph:
+            g["phases"].append(ph)
+        bound = sum(bool((p.get("spec") or {}).get("nodeName")) for p in self.cl.pods(name))
+        g["bound_pods"] = bound
+        if bound and ph not in ("Inqueue", "Running"):
+            g["bound_before_inqueue"] += 1
+        g["admitted"] = ph == "Running" and bound == g["min_member"]
 
     def dump_logs(self, name, tail=int(os.environ.get("PDO_BENCH_LOG_TAIL", "4000"))):
         import glob
@@ -279,6 +316,14 @@ def _comm_summary(rs):
     return out
 
 
+def _gang_summary(g):
+    if not g:
+        return None
+    return {"podgroup_min_member": g.get("min_member"), "podgroup_phases": g.get("phases"),
+            "bound_pods": g.get("bound_pods"), "bound_before_inqueue": g.get("bound_before_inqueue"),
+            "scheduler": "volcano (pdo gang scheduler)"}
+
+
 def orchestrate(a):
     from paddle_operator_amd.models.gpt2 import GPT2Config
     from paddle_operator_amd.utils.topology import gpu_count
@@ -313,17 +358,19 @@ def orchestrate(a):
     if gpus:
         # read by the in-process agent (csrc/core/agent.cpp) and its warm launcher
         os.environ["PDO_GPU_VISIBILITY"] = "isolate" if a.rehearse_shared_gpu else a.gpu_visibility
-        # warm slots per GPU: two (back-to-back jobs start warm) up to 2 GPUs; one
-        # above, so ranks + slots stay at ≤ 2 processes per GPU on a full node
-        os.environ.setdefault("PDO_SLOTS_PER_GPU", "2" if N <= 2 else "1")
+        # warm slots per GPU: three (back-to-back jobs start warm: launch/zygote.py
+        # slots_per_gpu) up to 2 GPUs; one above, so ranks + slots stay at ≤ 2
+        # processes per GPU on a full node
+        os.environ.setdefault("PDO_SLOTS_PER_GPU", "3" if N <= 2 else "1")
     sandbox = tempfile.mkdtemp(prefix="pdo-bench-")
     if a.no_warm_slots:
         os.environ["PDO_WARM_SLOTS"] = "0"  # read by the agent when it starts the zygote
     out = {}
     try:
         nproc = N if a.pod_layout == "one-pod" else 1
+        gang = a.gang == "on" or (a.gang == "auto" and N > 1)
         L = Launcher(a.mode, not a.no_zygote, gpus, os.path.join(sandbox, a.mode), extra_args, nproc,
-                     cpu_threads=1 if a.virtual_gpus else 0)
+                     cpu_threads=1 if a.virtual_gpus else 0, volcano=gang)
         try:
             trials = []
             for t in range(a.ready_trials):
@@ -366,20 +413,29 @@ def orchestrate(a):
                 out["ready_train"] = ready_stats(tt)
                 log(f"ready-to-train p50 {out['ready_train']['p50']}s over {len(tt)} {a.workload} jobs")
             wl += ["--steps", str(a.steps), "--warmup", str(a.warmup), "--bench", "--timeout", "600"]
-            t0 = L.launch(name, N, wl, a.ops)
+            t0 = L.launch(name, N, wl, a.ops, gang=gang)
             rs = L.wait_records(name, "bench", N, a.timeout)
             L.finish(name)
             out["bench"] = rs
             out["bench_ready_s"] = max(r["t_ready"] for r in rs) - t0
-            if a.workload == "gpt2" and a.secondary_resnet and gpus and a.ops == "hip" and (N == 1 or a.secondary_resnet > 1):
-                # the reference's own example workload (deploy/examples/resnet.yaml) in the same
-                # driver run; a failure here never costs the headline record
+            if gang:
+                out["gang"] = L.gang_log.get(name)
+            if a.workload == "gpt2" and a.secondary_resnet and gpus:
+                # the reference's own example workload (deploy/examples/resnet.yaml, config 3 at
+                # N = 8) on the same N ranks in the same driver run; a failure here never costs
+                # the headline record
                 try:
-                    wl2 = ["--workload", "resnet50", "--batch", "256", "--steps", "20", "--warmup", "5", "--bench",
-                           "--timeout", "600"]
-                    L.launch("resnet50-bench", N, wl2, a.ops)
+                    if a.virtual_gpus:  # CPU rehearsal: the tiny ResNet, as --workload resnet50 --tiny
+                        wl2 = ["--workload", "resnet50", "--tiny", "--batch", "2", "--steps", "2", "--warmup", "1"]
+                    else:
+                        wl2 = ["--workload", "resnet50", "--batch", "256", "--steps", "20", "--warmup", "5"]
+                    wl2 += ["--bench", "--timeout", "600"]
+                    L.launch("resnet50-bench", N, wl2, a.ops, gang=gang)
                     out["resnet"] = L.wait_records("resnet50-bench", "bench", N, min(a.timeout, 300.0))
+                    out["resnet_wl"] = wl2
                     L.finish("resnet50-bench")
+                    if gang:
+                        out["resnet_gang"] = L.gang_log.get("resnet50-bench")
                 except Exception as e:  # noqa: BLE001
                     out["resnet_error"] = f"{type(e).__name__}: {e}"
                     log(f"secondary ResNet-50 job failed: {out['resnet_error']}")
@@ -411,7 +467,8 @@ def orchestrate(a):
     pods = N if a.pod_layout == "per-gpu" else 1
     launch = (f"PaddleJob worker.replicas={pods} x {N // pods} GPU, planner={a.mode}, zygote={not a.no_zygote}, "
               f"warm_slots={not a.no_zygote and not a.no_warm_slots and bool(gpus)}, "
-              f"gpu_visibility={os.environ.get('PDO_GPU_VISIBILITY', 'isolate') if gpus else 'cpu'}")
+              f"gpu_visibility={os.environ.get('PDO_GPU_VISIBILITY', 'isolate') if gpus else 'cpu'}"
+              + (f", gang=volcano PodGroup minMember={pods}" if out.get("gang") else ""))
     extra = {
         "baseline_metric": BASELINE_METRIC,
         "ready_p50_s": out["ready"]["p50"] if out.get("ready") else None,
@@ -427,6 +484,9 @@ def orchestrate(a):
         "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in rs),
         # N > 1: measured after the timed region by every rank (launch/run.py _comm_diag)
         "comm": _comm_summary(rs),
+        # Volcano gang path (N > 1): the PodGroup's minMember and the phases it went
+        # through; bound_before_inqueue counts polls that saw a pod bound before admission
+        "gang": _gang_summary(out.get("gang")),
     }
     dev = "cpu/gloo" if not gpus else rs[0].get("gpu_name", "gpu")
     if a.workload == "gpt2":
@@ -445,17 +505,21 @@ def orchestrate(a):
                "model_tflops_per_gpu": round(flops_gpu / 1e12, 1),
                "mfu_vs_2.5PF_dense": round(flops_gpu / 2.5e15, 4)}
         if out.get("resnet"):
-            r2 = out["resnet"]
+            r2, wl2 = out["resnet"], out["resnet_wl"]
+            st2, mb2 = int(wl2[wl2.index("--steps") + 1]), int(wl2[wl2.index("--batch") + 1])
             dt2 = max(r["seconds"] for r in r2)
-            rate2 = sum(r["tokens_per_step_rank"] for r in r2) * 20 / dt2
+            rate2 = sum(r["tokens_per_step_rank"] for r in r2) * st2 / dt2
             rec["secondary"] = {
                 "metric": "launched images/sec (ResNet-50 PaddleJob through the pdo operator, collective DP over RCCL)",
-                "value": round(rate2, 1), "unit": "images/s", "n_gpus": N, "steps": 20, "warmup": 5,
-                "ms_per_step": round(dt2 / 20 * 1e3, 3), "dtype": "bf16",
+                "value": round(rate2, 1), "unit": "images/s", "n_gpus": N, "steps": st2,
+                "warmup": int(wl2[wl2.index("--warmup") + 1]),
+                "ms_per_step": round(dt2 / st2 * 1e3, 3), "dtype": "bf16" if not a.virtual_gpus else "fp32",
                 "data": "synthetic (on-device random 224x224 images and labels), random-init weights",
-                "config": {"model": "resnet50", "global_batch": 256 * N, "micro_batch_per_gpu": 256, "resolution": 224,
+                "config": {"model": "resnet18-like-tiny (CPU rehearsal)" if a.virtual_gpus else "resnet50", "global_batch": mb2 * N,
+                           "micro_batch_per_gpu": mb2, "resolution": 32 if a.virtual_gpus else 224,
                            "parallelism": f"dp{N}", "pod_layout": f"{pods}x{N // pods}"},
-                "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in r2)}
+                "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in r2),
+                "comm": _comm_summary(r2), "gang": _gang_summary(out.get("resnet_gang"))}
         elif out.get("resnet_error"):
             rec["secondary"] = {"error": out["resnet_error"]}
     else:

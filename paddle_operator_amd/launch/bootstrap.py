@@ -160,6 +160,13 @@ def init(t_start: float, backend: Optional[str] = None, timeout_s: int = 300, ip
     b.t_pg = time.time()
     b.phases = {"entry": round(t_entry - t_start, 4), "hip": round(t_dev - t_entry, 4),
                 "comm": round(t_comm - t_dev, 4), "warm": round(b.t_pg - t_comm, 4)}
+    # entry split (zygote launches): client → zygote, parked behind a warming
+    # slot, and handoff/fork → bootstrap.init inside the rank
+    t_recv, t_disp = os.environ.get("PDO_T_ZYG_RECV"), os.environ.get("PDO_T_DISPATCH")
+    if t_recv and t_disp:
+        b.phases.update({"to_zygote": round(float(t_recv) - t_start, 4),
+                         "park": round(float(t_disp) - float(t_recv), 4),
+                         "rank_entry": round(t_entry - float(t_disp), 4)})
     return b
 
 

@@ -89,21 +89,24 @@ SLOT_WARM_MAX_S = float(os.environ.get("PDO_SLOT_WARM_MAX_S", "60"))
 # "mem_mb" in the status table), "exit" = once that job's rank exits (no
 # second context on the GPU while the job runs)
 SLOT_RESPAWN = os.environ.get("PDO_SLOT_RESPAWN", "handoff")
-# warm slots kept per GPU (PDO_SLOTS_PER_GPU).  With one, a job that starts
-# right after another on the same GPU finds its slot still re-warming (HIP +
-# RCCL init, ≈ 1 s: bench.py 'ready_b2b'); a second slot serves it warm.  Each
-# slot holds a HIP context and a 1-rank communicator on the GPU ('mem_mb' in
-# the status table, well under 1 GB of the 288 GB).  Unset, the default follows
-# the number of warm devices (slots_per_gpu): two up to 2 GPUs, one above, so a
-# full 8-GPU node runs at most rank + slot = 2 processes per GPU — the layout
-# bench.py measures.
+# warm slots kept per GPU (PDO_SLOTS_PER_GPU).  A slot re-warms in ≈ 1.6 s (HIP
+# + RCCL init, 'warm_s' in the status table) while back-to-back jobs on one GPU
+# arrive every ≈ 0.7 s (bench.py 'ready_b2b': create → ready → Completed →
+# deleted).  A pool of k slots absorbs such a stream only while warm_s / k ≤
+# the job interval: with two, every job from the third on parked ≈ 1.6 − 2·0.7
+# ≈ 0.2 s behind a warming slot (the round-5 'ready_b2b' p50 of 0.27 s, entry
+# phase 0.20 s); three keep it at zero.  Each slot holds a HIP context and a
+# 1-rank communicator on the GPU ('mem_mb' ≈ 1 GB of the 288 GB).  Unset, the
+# default follows the number of warm devices (slots_per_gpu): three up to 2
+# GPUs, one above, so a full 8-GPU node runs at most rank + slot = 2 processes
+# per GPU — the layout bench.py measures.
 _SLOTS_ENV = os.environ.get("PDO_SLOTS_PER_GPU", "")
 
 
 def slots_per_gpu(n_devices: int) -> int:
     if _SLOTS_ENV.strip():
         return max(1, int(_SLOTS_ENV))
-    return 2 if n_devices <= 2 else 1
+    return 3 if n_devices <= 2 else 1
 
 
 SLOTS_PER_GPU = slots_per_gpu(1)
@@ -265,7 +268,8 @@ def _slot_main(dev: str, sock: socket.socket, listener: socket.socket):
         if test_mode == "hang":  # CPU tests: a slot stuck in its warm-up
             while True:
                 time.sleep(3600)
-        if test_mode == "cpu":  # CPU tests: a slot that warms nothing
+        if test_mode == "cpu":  # CPU tests: a slot that warms nothing (in PDO_SLOT_TEST_WARM_S)
+            time.sleep(float(os.environ.get("PDO_SLOT_TEST_WARM_S", "0") or 0))
             info = {"device": "none"}
         elif os.environ.get("PDO_GPU_VISIBILITY") == "all":
             os.environ.pop("HIP_VISIBLE_DEVICES", None)
@@ -321,7 +325,8 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
     slot_fails: Dict[str, int] = {}
     pending: Dict[str, list] = {}      # device -> [(conn, req, fds, t_park)] waiting for a warming slot
     rank_dev: Dict[int, str] = {}      # rank pid -> GPU whose slot it took (SLOT_RESPAWN = exit)
-    served = {"warm": 0, "cold": 0, "park_timeouts": 0, "warm_timeouts": 0}
+    served = {"warm": 0, "cold": 0, "park_timeouts": 0, "warm_timeouts": 0, "parked": 0, "park_s": 0.0,
+              "park_max_s": 0.0}
     per_gpu = slots_per_gpu(len(warm_devices or ()))
 
     def log(msg):
@@ -365,7 +370,20 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
         conn.setblocking(False)
         sel.register(conn, selectors.EVENT_READ, pid)
 
+    def stamp(req, how):
+        """Dispatch timestamps for the rank's phase split (launch/bootstrap.py):
+        request received → handed to a slot / forked; parked time is counted."""
+        now = time.time()
+        env = req.setdefault("env", {})
+        t_recv = float(req.get("_t_recv") or now)
+        env["PDO_T_ZYG_RECV"] = repr(t_recv)
+        env["PDO_T_DISPATCH"] = repr(now)
+        env["PDO_DISPATCH"] = how
+        served["park_s"] = round(served["park_s"] + (now - t_recv), 4)
+        served["park_max_s"] = round(max(served["park_max_s"], now - t_recv), 4)
+
     def cold(conn, req, fds):
+        stamp(req, "cold")
         pid = os.fork()
         if pid == 0:
             _child(req, fds, ls)
@@ -375,6 +393,7 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
         attach(pid, conn)
 
     def handoff(sl, conn, req, fds):
+        stamp(req, "warm")
         try:
             _send_request(sl.sock, req, fds)
         except OSError as e:  # the slot died under us
@@ -468,12 +487,13 @@ def serve(path: str, idle_exit_s: float = 0.0, warm_devices: Optional[List[str]]
                         pass
                     conn.close()
                     continue
-                last_activity = time.time()
+                last_activity = req["_t_recv"] = time.time()
                 dev = warm_device_of(req, key) if warm_devices else None
                 sl = ready_slot(dev) if dev is not None else None
                 if sl is not None:
                     handoff(sl, conn, req, fds)
                 elif dev is not None and slots.get(dev):  # warming: wait for one, at most SLOT_PARK_S (expire)
+                    served["parked"] += 1
                     pending.setdefault(dev, []).append((conn, req, fds, time.time()))
                 else:
                     cold(conn, req, fds)

@@ -241,6 +241,36 @@ def test_bench_eight_ranks_virtual_gpus(layout):
     assert rec["ready"]["trials"] == 2 and rec["ready_b2b"]["trials"] == 1
 
 
+def test_bench_eight_virtual_gpus_gang_and_secondary():
+    """Configs 3 and 4 in the 8-GPU driver run, rehearsed on CPU: the GPT-2 job
+    goes through the Volcano gang path (PodGroup minMember=8, admitted before any
+    pod binds, Running once all 8 run — reference controllers/paddlejob_helper.go
+    :478-549), the ResNet job (deploy/examples/resnet.yaml) runs on the same 8
+    ranks under 'secondary', and both records carry the comm block."""
+    env = _bench_env()
+    env.pop("PDO_SLOTS_PER_GPU", None)
+    args = ["--gpus", "8", "--cpu", "--virtual-gpus", "--model", "gpt2-tiny", "--micro-batch", "2", "--seq", "64",
+            "--steps", "2", "--warmup", "1", "--ready-trials", "1", "--compat-trials", "0", "--train-ready-trials", "0",
+            "--b2b-trials", "0", "--ops", "torch"]
+    r = subprocess.run([sys.executable, "bench.py"] + args, cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
+    g = rec["gang"]
+    assert g["podgroup_min_member"] == 8 and g["bound_before_inqueue"] == 0, g
+    assert g["podgroup_phases"][-1] == "Running" and "Inqueue" in g["podgroup_phases"] + ["Inqueue"], g
+    assert g["bound_pods"] == 8, g
+    assert "gang=volcano PodGroup minMember=8" in rec["config"]["launch"]
+    c = rec["comm"]
+    assert c["ranks"] == 8 and c["buckets"]["count"] >= 1 and c["allreduce_busbw_GBps_min"] > 0, c
+    sec = rec["secondary"]
+    assert "error" not in sec, sec
+    assert sec["n_gpus"] == 8 and sec["value"] > 0 and sec["config"]["parallelism"] == "dp8"
+    assert sec["gang"]["podgroup_min_member"] == 8 and sec["gang"]["bound_before_inqueue"] == 0
+    assert sec["comm"]["ranks"] == 8
+
+
 @pytest.mark.slow
 def test_bench_contract_torchrun_two_ranks():
     """Under the driver's torchrun wrapper: rank 0 launches, rank 1 only waits; one JSON line."""

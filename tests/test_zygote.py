@@ -164,3 +164,59 @@ def test_two_slots_serve_back_to_back_jobs_warm(tmp_path):
             s.close()
     finally:
         _stop(p)
+
+
+def test_back_to_back_stream_dispatch_delay_bounded(tmp_path):
+    """A stream of back-to-back jobs on one GPU while replacement slots warm
+    (simulated 1.0 s warm-up, one job every ≈ 0.45 s — the round-5 b2b regime
+    scaled down): with the default pool (3 slots at ≤ 2 GPUs) no request parks
+    long; the zygote's own stamps (PDO_T_ZYG_RECV / PDO_T_DISPATCH) bound it."""
+    env0 = {k: v for k, v in os.environ.items() if k != "PDO_SLOTS_PER_GPU"}
+    path = str(tmp_path / "z.sock")
+    e = dict(env0, PYTHONPATH=REPO, PDO_SLOT_TEST="cpu", PDO_SLOT_TEST_WARM_S="1.0")
+    p = subprocess.Popen([sys.executable, "-m", "paddle_operator_amd.launch.zygote", "--socket", path,
+                          "--warm-devices", "0"], env=e, stdout=open(tmp_path / "z.log", "w"),
+                         stderr=subprocess.STDOUT)
+    try:
+        t_end = time.time() + 120
+        st = None
+        while time.time() < t_end:
+            st = zygote.query_status(path)
+            if st and (st["slots"].get("0") or {}).get("n_ready") == st["slots_per_gpu"]:
+                break
+            time.sleep(0.05)
+        assert st["slots_per_gpu"] == 3, st
+        for _ in range(7):
+            t0 = time.time()
+            s = _request(path, e, ["--workload", "noop", "--exit-after-ready"], PDO_RANK_HOLD_S="0.1")
+            assert _readline(s).startswith("PID ")
+            assert _readline(s).startswith("EXIT ")
+            s.close()
+            time.sleep(max(0.0, 0.45 - (time.time() - t0)))
+        st = zygote.query_status(path)
+        assert st["served"]["warm"] == 7 and st["served"]["cold"] == 0, st
+        # every request dispatched at once: nothing parked behind a warming slot
+        assert st["served"]["park_max_s"] < 0.1, st["served"]
+    finally:
+        _stop(p)
+
+
+def test_two_slot_pool_parks_under_the_same_stream(tmp_path):
+    """The same stream with PDO_SLOTS_PER_GPU=2 parks (the round-5 regression's
+    mechanism): warm_s / 2 > the job interval."""
+    p, path, env = _start(tmp_path, PDO_SLOT_TEST="cpu", PDO_SLOT_TEST_WARM_S="1.0", PDO_SLOTS_PER_GPU="2")
+    try:
+        t_end = time.time() + 60
+        while time.time() < t_end and (zygote.query_status(path)["slots"].get("0") or {}).get("n_ready") != 2:
+            time.sleep(0.05)
+        for _ in range(6):
+            t0 = time.time()
+            s = _request(path, env, ["--workload", "noop", "--exit-after-ready"], PDO_RANK_HOLD_S="0.1")
+            assert _readline(s).startswith("PID ")
+            assert _readline(s).startswith("EXIT ")
+            s.close()
+            time.sleep(max(0.0, 0.3 - (time.time() - t0)))
+        st = zygote.query_status(path)
+        assert st["served"]["parked"] >= 1 and st["served"]["park_max_s"] > 0.1, st["served"]
+    finally:
+        _stop(p)
