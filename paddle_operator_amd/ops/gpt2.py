@@ -510,9 +510,12 @@ class _LMHeadXentFn(torch.autograd.Function):
         # dW stays private to this node until its backward: a split tied weight
         # (parallel/flat.py) then adds it, scaled by dloss, into its head-gradient
         # slot (bucket 0) — two forwards before one backward each add their own
-        # part, and a forward whose graph is dropped leaves the slot untouched
+        # part (bucket 0 launches after the last of them: AuxGrad.node_done), and a
+        # forward whose graph is dropped leaves the slot untouched
         sp = getattr(w, "_pdo_split", None)
         ctx.split = sp
+        if sp is not None:
+            sp.node_begin()  # the slot is ready once every such node's backward has added (flat.AuxGrad)
         dw = torch.empty(Vp, C, device=h.device, dtype=h.dtype)
         loss_sum = torch.zeros((), device=h.device, dtype=torch.float32)
         for c0 in range(0, N, chunk):
@@ -550,7 +553,7 @@ class _LMHeadXentFn(torch.autograd.Function):
         sp = ctx.split
         if sp is not None:
             m.axpy_dev_(sp.grad.view(-1), dw.view(-1), d)  # slot += dloss · dW, one rounding
-            sp.ready(sp)
+            sp.node_done()
             return dh.view(ctx.shape), None, None, None, None
         m.scale_dev_(dw, d)
         return dh.view(ctx.shape), dw, None, None, None
@@ -566,6 +569,7 @@ class _SplitHeadLinearFn(torch.autograd.Function):
     def forward(ctx, h, w, sp):
         ctx.save_for_backward(h, w)
         ctx.sp = sp
+        sp.node_begin()
         return _fwd_gemm(h, w) if h.is_cuda else F.linear(h, w)
 
     @staticmethod
@@ -580,7 +584,7 @@ class _SplitHeadLinearFn(torch.autograd.Function):
         if not (dy.is_cuda and dy2.dtype == torch.bfloat16 and _HIP_DW[0] and dy2.is_contiguous()
                 and h2.is_contiguous() and _native.require_hip().gemm_dw(dy2, h2, g, True)):
             g.addmm_(dy2.t().to(g.dtype), h2.to(g.dtype))
-        sp.ready(sp)
+        sp.node_done()
         return dh, None, None
 
 

@@ -89,7 +89,9 @@ class FlatAdamW:
                          self._norm_buf, lr, self.b1, self.b2, self.eps, self.wd,
                          bc1, bc2, grad_scale, clip)
             return
-        # reference path (fp32 math, identical formula to the kernel)
+        # reference path: the kernel's formula in fp32 with IEEE sqrt and division
+        # (the default HIP kernel, adamw_fast_kernel, uses the hardware v_sqrt /
+        # v_rcp, ≈ 1 ulp: the two drift apart by rounding, step by step)
         g = f.param_grads.float() * grad_scale
         if clip > 0:
             norm = torch.sqrt(self._norm_buf[0])
@@ -106,11 +108,12 @@ class FlatAdamW:
         return {"master": self.master, "m": self.m, "v": self.v, "step": self.step_count}
 
     def load_state_dict(self, sd):
-        if sd["master"].numel() != self.master.numel():
-            raise ValueError(f"optimizer state has {sd['master'].numel()} elements, the arena {self.master.numel()}")
-        self.master.copy_(sd["master"])
-        self.m.copy_(sd["m"])
-        self.v.copy_(sd["v"])
+        # either arena layout (FlatParams.from_checkpoint: pre-round-5 states lead
+        # with the split head slot); another model's state raises
+        f = self.flat
+        self.master.copy_(f.from_checkpoint(sd["master"]))
+        self.m.copy_(f.from_checkpoint(sd["m"]))
+        self.v.copy_(f.from_checkpoint(sd["v"]))
         self.step_count = int(sd["step"])
         self.flat.params.copy_(self.master)
 

@@ -117,6 +117,8 @@ class BucketedDDP:
         self._next = 0
         self._seen = set()
         self._staged = False
+        for a in self.flat.aux_slots:  # LM-head nodes writing a split slot this step (flat.AuxGrad)
+            a.param.nodes = 0
 
     def finish(self, opt=None):
         """Call after backward: launch stragglers, make the compute stream wait,

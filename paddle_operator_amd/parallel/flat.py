@@ -72,12 +72,31 @@ class AuxGrad:
 
     ``grad`` is its arena view (same shape as the parameter); the op that
     produces this part of the gradient writes (or adds) into it and calls
-    ``ready(self)`` — BucketedDDP counts it like a parameter of bucket 0."""
+    ``node_done()`` — BucketedDDP counts it like a parameter of bucket 0.
+
+    Several graph nodes may write the slot in one step (two forwards through
+    the LM head before one backward): each forward registers its node
+    (``node_begin``) and the slot is reported ready only when the LAST of them
+    has added its part.  Reporting at the first would launch bucket 0's
+    all-reduce while the second node's add is still to come — RCCL reducing a
+    buffer the compute stream then writes.  A node whose graph is dropped never
+    ends; its bucket is then launched by ``BucketedDDP.finish`` (stragglers).
+    ``BucketedDDP.prepare`` resets the count: call it before the forward."""
 
     def __init__(self, name: str, grad: torch.Tensor):
         self.name = name
         self.grad = grad
         self.ready = _noop_ready
+        self.nodes = 0
+
+    def node_begin(self):
+        self.nodes += 1
+
+    def node_done(self):
+        self.nodes -= 1
+        if self.nodes <= 0:
+            self.nodes = 0
+            self.ready(self)
 
 
 def default_no_decay(name: str, p: torch.Tensor) -> bool:
@@ -306,11 +325,25 @@ class FlatParams:
     def state_dict(self):
         return {s.name: s.param.detach() for s in self.slots}
 
-    def load_params(self, flat_params: torch.Tensor):
-        """Copy a checkpointed flat parameter buffer into the arena, refusing a
-        buffer of another layout (a different model or an arena from before the
-        head slot moved out of the parameter range)."""
-        if flat_params.numel() != self.numel:
-            raise ValueError(f"checkpoint arena has {flat_params.numel()} elements, this model's has {self.numel}: "
+    def legacy_head_elems(self, n: int) -> int:
+        """Checkpoints written before the split head-gradient slots moved behind
+        the parameter range (round 5) lead with those slots in params / master /
+        m / v: a buffer of exactly ``numel + Σ round_up(slot, ALIGN)`` elements is
+        that layout, and the leading elements returned here are dropped on load."""
+        head = sum(_round_up(a.numel, ALIGN) for a in self.aux_slots)
+        return head if head and n == self.numel + head else 0
+
+    def from_checkpoint(self, buf: torch.Tensor) -> torch.Tensor:
+        """A checkpointed parameter-range buffer in this arena's layout; raises
+        on a buffer of another model."""
+        n = buf.numel()
+        skip = self.legacy_head_elems(n)
+        if n - skip != self.numel:
+            raise ValueError(f"checkpoint arena has {n} elements, this model's has {self.numel}: "
                              "saved by a different model or arena layout")
-        self.params.copy_(flat_params.to(self.params.device))
+        return buf.reshape(-1)[skip:]
+
+    def load_params(self, flat_params: torch.Tensor):
+        """Copy a checkpointed flat parameter buffer into the arena (either
+        layout, ``from_checkpoint``); a buffer of another model raises."""
+        self.params.copy_(self.from_checkpoint(flat_params).to(self.params.device))

@@ -418,3 +418,94 @@ def test_flat_shadow_scope_cpu():
         w.add_(1.0)  # a change outside the scope: the next scope refreshes
     with flat.shadow_scope():
         assert torch.equal(view, w.detach().to(torch.bfloat16))
+
+
+def _two_forward_worker(rank, world, port, outdir):
+    """Two graphs through the split LM head before one backward, DDP on: bucket
+    0 (the head slot) must launch only after BOTH nodes added their part."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PDO_OPS="torch")
+    torch.set_num_threads(1)
+    from paddle_operator_amd.models.gpt2 import GPT2, GPT2Config
+    from paddle_operator_amd.parallel.ddp import BucketedDDP
+    from paddle_operator_amd.parallel.flat import FlatParams
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    cfg = GPT2Config.named("gpt2-tiny")
+    model = GPT2(cfg)
+    flat = FlatParams(model, dtype=torch.float32, device="cpu", bucket_bytes=64 << 10, late=("wte",),
+                      split=("wte",))
+    ddp = BucketedDDP(flat)
+    sp = flat.aux_slots[0].param
+    seen = []
+    if ddp.enabled:
+        orig = ddp._launch
+
+        def launch(i):  # the head slot's node count when its bucket goes on the wire
+            if i == 0:
+                seen.append((sp.nodes, done[0]))
+            orig(i)
+        ddp._launch = launch
+    done = [0]
+    orig_done = sp.node_done
+
+    def node_done():
+        done[0] += 1
+        orig_done()
+    sp.node_done = node_done
+    x, y = _batch(cfg, B=8)
+    per = x.shape[0] // world
+    sl = slice(rank * per, (rank + 1) * per)
+    flat.zero_grad()
+    ddp.prepare()
+    loss = model(x[sl], y[sl]) + 0.5 * model(x[sl].flip(1), y[sl].flip(1))
+    loss.backward()
+    ddp.finish()
+    if rank == 0:
+        torch.save({"grads": {n: (p.grad.float() * ddp.grad_scale).clone() for n, p in model.named_parameters()},
+                    "seen": seen, "done": done[0]}, os.path.join(outdir, f"w{world}.pt"))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def test_split_head_two_forwards_ddp_two_ranks(tmp_path):
+    """ADVICE r5 (ops/gpt2.py:552): with two LM-head graphs before one backward,
+    bucket 0 (the split head slot) is launched once, after the second node's
+    add — and the 2-rank averaged gradients equal one process's full batch."""
+    port = _free_port()
+    mp.start_processes(_two_forward_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    _two_forward_worker(0, 1, port, str(tmp_path))
+    d2 = torch.load(tmp_path / "w2.pt", weights_only=True)
+    d1 = torch.load(tmp_path / "w1.pt", weights_only=True)
+    assert d2["done"] == 2 and d2["seen"] == [(0, 2)], d2["seen"]
+    for n, r in d1["grads"].items():
+        err = float((d2["grads"][n] - r).norm() / (r.norm() + 1e-12))
+        assert err < 1e-4, (n, err)
+
+
+def test_legacy_checkpoint_layout_loads():
+    """ADVICE r5 (flat.py:309): an arena checkpoint from before the split head
+    slot moved behind the parameter range (params / master / m / v led by the
+    aligned wte-sized slot) still loads; another model's buffer still raises."""
+    os.environ["PDO_OPS"] = "torch"
+    from paddle_operator_amd.models.gpt2 import GPT2, GPT2Config
+    from paddle_operator_amd.ops.optim import FlatAdamW
+    from paddle_operator_amd.parallel.flat import ALIGN, FlatParams
+
+    model = GPT2(GPT2Config.named("gpt2-tiny"))
+    flat = FlatParams(model, dtype=torch.float32, device="cpu", late=("wte",), split=("wte",))
+    opt = FlatAdamW(flat)
+    wte = dict(model.named_parameters())["wte.weight"] if "wte.weight" in dict(model.named_parameters()) else None
+    head = flat.legacy_head_elems(flat.numel + sum((a.numel + ALIGN - 1) // ALIGN * ALIGN for a in flat.aux_slots))
+    assert head > 0 and (wte is None or head >= wte.numel())
+    new = torch.randn(flat.numel)
+    legacy = torch.cat([torch.full((head,), 7.0), new])
+    flat.load_params(legacy)
+    assert torch.equal(flat.params, new)
+    opt.load_state_dict({"master": legacy, "m": legacy * 2, "v": legacy.abs(), "step": 3})
+    assert torch.equal(opt.master, new) and torch.equal(opt.m, new * 2) and opt.step_count == 3
+    flat.load_params(new * 3)  # the current layout
+    assert torch.equal(flat.params, new * 3)
+    with pytest.raises(ValueError):
+        flat.load_params(torch.zeros(flat.numel + 1))

@@ -117,6 +117,22 @@ def _resnet_fwd(m, x):
     return m.fc(torch.flatten(torch.nn.functional.adaptive_avg_pool2d(y, 1), 1)), h
 
 
+# HIP error vs fp32 ≤ ANCHOR_RATIO × the framework-bf16 error + ANCHOR_FLOOR (a
+# relative-error floor for tensors the bf16 framework reproduces almost exactly)
+ANCHOR_RATIO, ANCHOR_FLOOR = 1.5, 0.005
+
+
+def _dump(name, table):
+    """PDO_TEST_DUMP_DIR: write an anchor's per-tensor (hip, framework-bf16)
+    error table (evidence for profiles/)."""
+    d = os.environ.get("PDO_TEST_DUMP_DIR")
+    if d:
+        import json
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name), "w") as f:
+            json.dump({k: [round(a, 6), round(b, 6)] for k, (a, b) in table.items()}, f, indent=0)
+
+
 @pytest.mark.gpu
 def test_resnet50_width_hip_vs_fp32(cuda):
     """Full-width ResNet-50 (64 … 2048 channels, every stage and block type) on
@@ -130,7 +146,7 @@ def test_resnet50_width_hip_vs_fp32(cuda):
 
     The bound is bf16's own: the framework ops in bf16 (``PDO_OPS=torch`` +
     autocast, MIOpen convolutions) run on the same batch, and every HIP error
-    against fp32 must stay within 1.5× the framework-bf16 error (+ 0.03).  BN
+    against fp32 must stay within 1.5× the framework-bf16 error (+ 0.005).  BN
     γ / β gradients carry ≈ 40 % bf16 noise either way at this batch
     (tools/resnet_anchor_probe.py); a dropped, doubled or mis-masked gradient
     is O(1) above it.  Batch 16 at 128 × 128: every stage's token count is a
@@ -181,9 +197,12 @@ def test_resnet50_width_hip_vs_fp32(cuda):
         a, b = a.detach().float().cpu(), b.detach().float().cpu()
         return float((a - b).norm() / (b.norm() + 1e-12))
 
+    table = {}
+
     def within(name, hip_t, fw_t, ref_t, bad):
         eh, ef = rel(hip_t, ref_t), rel(fw_t, ref_t)
-        if not eh <= 1.5 * ef + 0.03:
+        table[name] = (eh, ef)
+        if not eh <= ANCHOR_RATIO * ef + ANCHOR_FLOOR:
             bad[name] = (round(eh, 4), round(ef, 4))
 
     assert abs(loss_h.item() - loss_r.item()) < 1e-2 * abs(loss_r.item()), (loss_h.item(), loss_r.item())
@@ -197,4 +216,5 @@ def test_resnet50_width_hip_vs_fp32(cuda):
     for n, b in hip.named_buffers():
         if "running" in n:
             within(n, b, fb[n], rb[n], bad)
+    _dump("resnet50_anchor.json", table)
     assert not bad, bad
