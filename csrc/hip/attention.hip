@@ -138,25 +138,15 @@ __device__ __forceinline__ void retire(const bf16x8 (&v)[N]) {
 }
 __device__ __forceinline__ void retire(float x) { asm volatile("" ::"v"(x)); }
 
-// Work order of the (b, h) × block grid.  order 0: heaviest blocks first across
-// every (b, h) — one pair's blocks run far apart in time, so each re-fetches the
-// pair's K/V (or Q/dO) tiles from beyond L2.  order 1: XCD-grouped — blocks
-// b and b + 8 share an XCD (round-robin dispatch), each XCD walks a contiguous
-// range of pairs and a pair's nb blocks consecutively (heaviest first), so its
-// tiles are fetched once into that XCD's L2 and read by all of them.  Speed
-// only, never correctness (any mapping is a bijection of the grid).
-// r = 0 is the heaviest block of the pair.
+// Work order of the (b, h) × block grid: heaviest blocks first across every
+// (b, h) (r = 0 is the heaviest block of the pair).  ``order`` is reserved
+// (0); the XCD-grouped alternative was measured and removed (attn_order).
 __device__ __forceinline__ void attn_block(int order, int nb, int BH, int& bh, int& r) {
+  (void)order;
+  (void)nb;
   const int id = blockIdx.x;
-  if (order == 0) {
-    bh = id % BH;
-    r = id / BH;
-    return;
-  }
-  const int nwg = BH * nb, xcd = id & 7, slot = id >> 3, q = nwg >> 3, rem = nwg & 7;
-  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + slot;
-  bh = L / nb;
-  r = L - bh * nb;
+  bh = id % BH;
+  r = id / BH;
 }
 
 // ----- global → register → LDS staging of a [64 rows][64] tile (256 threads) -----
@@ -777,12 +767,8 @@ __device__ __forceinline__ void dkdv_body(const bf16* __restrict__ qkv, const bf
   const bf16 *__restrict__ qkv, const bf16 *__restrict__ dout, const float *__restrict__ lse,                        \
       const float *__restrict__ delta, bf16 *__restrict__ dqkv, int B, int S, int H, float c2, float scale,          \
       float *__restrict__ dbias_part, int order
-template <int V>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_d64(PDO_DKDV_ARGS) {
-  dkdv_body<V>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
-}
-// the same body capped at 168 VGPRs: 3 waves per SIMD instead of 2 (the LDS
-// ring, 49.5 KiB per workgroup, allows 3 workgroups per CU)
+// capped at 168 VGPRs: 3 waves per SIMD (the LDS ring, 49.5 KiB per
+// workgroup, allows 3 workgroups per CU)
 template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_bwd_dkdv3_d64(PDO_DKDV_ARGS) {
   dkdv_body<V>(qkv, dout, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
@@ -985,34 +971,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   dq_body<V>(qkv, dout, o, lse, delta, dqkv, B, S, H, c2, scale, dbias_part, order);
 }
 
-static int env_int(const char* k, int def) {
-  const char* e = getenv(k);
-  return e && *e ? atoi(e) : def;
-}
-// Heaviest-first order by default.  The XCD-grouped order cuts the kernels'
-// L2 misses 2-3× (forward TCC_EA0_RDREQ 3.1e6 vs 1.05e7 per call) and wins
-// the isolated microbenchmark (backward 761 / 754 vs 775 / 777 µs), but loses
-// in the GPT-2-medium step: 144.20 / 144.02 / 144.19 vs 143.88 / 143.78 /
-// 143.81 ms (stepab, round 5) — its last workgroups end unevenly.  4-wave-
-// per-SIMD builds of the forward and dQ spilled and ran 401 / 1068 µs (removed).
-static int attn_order() {
-  static const int o = env_int("PDO_ATTN_ORDER", 0);
-  return o;
-}
+// Heaviest-first order (attn_block).  The XCD-grouped order cut the kernels'
+// L2 misses 2-3× (forward TCC_EA0_RDREQ 3.1e6 vs 1.05e7 per call) and won the
+// isolated microbenchmark (backward 761 / 754 vs 775 / 777 µs), but lost in
+// the GPT-2-medium step: 144.20 / 144.02 / 144.19 vs 143.88 / 143.78 / 143.81
+// ms (stepab, round 5) — its last workgroups end unevenly; removed in round 6.
+// 4-wave-per-SIMD builds of the forward and dQ spilled and ran 401 / 1068 µs
+// (removed).
+static int attn_order() { return 0; }
 
 int attn_fwd(const bf16* qkv, bf16* o, float* lse, int B, int S, int H, int D, float scale, hipStream_t st) {
   if (D != HD || S % 128 != 0) return -2;
   // variant 3 (lane-mask diagonal, v_max3 chains, buffer-load staging, v_dot2
-  // row sums, packed epilogue) by default: 285.1 / 289.0 vs 302.6 / 303.1 µs
-  // for variant 0 (tools/attn_ab.sh, B64 H16 S1024, 2 interleaved rounds;
-  // variant 1 alone 290.2 / 290.3, variant 2 alone 298.2 / 300.1);
-  // PDO_ATTN_FWDV=0 is the A/B alternative
-  static const int v = env_int("PDO_ATTN_FWDV", 3);
+  // row sums, packed epilogue): 285.1 / 289.0 vs 302.6 / 303.1 µs for variant 0
+  // (tools/attn_ab.sh, B64 H16 S1024, 2 interleaved rounds; variant 1 alone
+  // 290.2 / 290.3, variant 2 alone 298.2 / 300.1).  Variant 0 (pointer
+  // staging) remains for a (b, h) slice past 31-bit buffer offsets
   const int grid = B * H * (S / 128);
   const float c2 = scale * LOG2E;
   // buffer-load variants address the (b, h) slice with 31-bit byte offsets
   const bool fits = (size_t)S * 3 * H * HD * 2 < (1ull << 31);
-  if (fits && v == 3)
+  if (fits)
     attn_fwd3_d64<3><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order());
   else
     attn_fwd3_d64<0><<<grid, 256, 0, st>>>(qkv, o, lse, B, S, H, c2, attn_order());
@@ -1024,35 +1003,22 @@ int attn_bwd(const bf16* dout, const bf16* qkv, const bf16* o, const float* lse,
   if (D != HD || S % 128 != 0) return -2;
   const int grid = B * H * (S / 128);
   // dQ first: it also produces delta = rowsum(dO ∘ O), which dK/dV reads
-  // variant 1 by default: forward + backward 772.7 / 769.1 vs 786.9 / 784.3 µs
-  // with variant 0 (PDO_ATTN_DQV=0, the A/B alternative; tools/attn_ab.sh)
-  static const int dqv = env_int("PDO_ATTN_DQV", 1);
+  // variant 1: forward + backward 772.7 / 769.1 vs 786.9 / 784.3 µs with
+  // variant 0 (tools/attn_ab.sh), which remains for slices past 31-bit buffer offsets
   const bool fits = (size_t)S * 3 * H * HD * 2 < (1ull << 31);
-  if (dqv == 1 && fits)
+  if (fits)
     attn_bwd_dq_d64<1><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                              dbias_part, attn_order());
   else
     attn_bwd_dq_d64<0><<<grid, 256, 0, st>>>(qkv, dout, o, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
                                              dbias_part, attn_order());
-  // 3 waves per SIMD (168 VGPRs) by default: bwd 799 -> 768 us isolated, -0.55 ms/step;
-  // PDO_ATTN_DKDV3=0 = the 2-waves-per-SIMD build of the same body (A/B alternative)
-  static const int dkdv3 = env_int("PDO_ATTN_DKDV3", 1);
-  // variant 1 (fragments prefetched two k-steps / four transposed reads deep,
-  // lane-mask triangle) by default: forward + backward 759.4 / 763.0 vs 766.8 /
-  // 764.8 µs (tools/attn_ab.sh); PDO_ATTN_DKDVV=0 is the A/B alternative
-  static const int dkdvv = env_int("PDO_ATTN_DKDVV", 1);
-  if (dkdv3 && dkdvv == 1)
-    attn_bwd_dkdv3_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                                dbias_part, attn_order());
-  else if (dkdv3)
-    attn_bwd_dkdv3_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                                dbias_part, attn_order());
-  else if (dkdvv == 1)
-    attn_bwd_dkdv_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                               dbias_part, attn_order());
-  else
-    attn_bwd_dkdv_d64<0><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
-                                               dbias_part, attn_order());
+  // 3 waves per SIMD (168 VGPRs): bwd 799 -> 768 us isolated, -0.55 ms/step
+  // against the 2-wave build; variant 1 (fragments prefetched two k-steps / four
+  // transposed reads deep, lane-mask triangle): forward + backward 759.4 / 763.0
+  // vs 766.8 / 764.8 µs (tools/attn_ab.sh).  The 2-wave build and variant 0
+  // were removed in round 6 (settled A/Bs).
+  attn_bwd_dkdv3_d64<1><<<grid, 256, 0, st>>>(qkv, dout, lse, delta, dqkv, B, S, H, scale * LOG2E, scale,
+                                              dbias_part, attn_order());
   return 0;
 }
 

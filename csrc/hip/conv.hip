@@ -959,11 +959,9 @@ static void wgrad_fold(const float* part, int splits, int rows, int cols, int ld
 }
 
 // the weight gradient on gemm_dw4's 256 × 256 mainloop (B gathered per tap) where
-// its contract holds: ≥ 128 output channels, R·S·C % 256 = 0 (PDO_WGRAD_DW4=0: off)
-static int g_wgrad_dw4 = [] {
-  const char* e = getenv("PDO_WGRAD_DW4");
-  return e && *e ? atoi(e) : 1;
-}();
+// its contract holds: ≥ 128 output channels, R·S·C % 256 = 0 (conv_wgrad_mode(0):
+// off, for the probes and tests)
+static int g_wgrad_dw4 = 1;
 static int wgrad_dw4_splits(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
   // (R·S·C) % 128: at most half of the last 256-column tile is padding.  A 1×1
   // stride-1 product with half-height or half-padded tiles stays on the 128 × 128
@@ -983,11 +981,10 @@ int conv_wgrad_mode(int mode) {
   return prev;
 }
 
-// the tap-group 3×3 kernels for 64 / 128 channels (PDO_WGRAD_C64=0: the per-tap / dw4 kernels)
-static int g_wgrad_c64 = [] {
-  const char* e = getenv("PDO_WGRAD_C64");
-  return e && *e ? atoi(e) : 1;
-}();
+// the tap-group 3×3 kernels for 64 / 128 channels (ahead of the per-tap / dw4
+// kernels on every such shape: profiles/r4i_conv_probe.jsonl); conv_wgrad_c64_mode(0)
+// selects those for the probes and tests
+static int g_wgrad_c64 = 1;
 // splits of the tap-group kernel (grid = splits × tap groups ≈ one workgroup per CU); 0: not taken
 static int wgrad_c64_splits(int N, int H, int W, int C, int Kout, int R, int S, int stride, int pad) {
   if (!g_wgrad_c64 || C != Kout || (C != 64 && C != 128) || R != 3 || S != 3 || pad != 1) return 0;
@@ -1169,12 +1166,8 @@ __global__ __launch_bounds__(256) void stem_dw_kernel(const float* __restrict__ 
 
 // split count of the stem weight gradient: two workgroups per CU, ≥ 8 k-steps each
 int stem_splits(long long M) {
-  static const int env = [] {
-    const char* e = getenv("PDO_STEM_SPLITS");
-    return e && *e ? atoi(e) : 0;
-  }();
   const long long ks = (M + 63) / 64;
-  long long sp = env > 0 ? env : 512;
+  long long sp = 512;
   if (sp > ks / 8) sp = ks / 8;
   return sp < 1 ? 1 : (int)sp;
 }

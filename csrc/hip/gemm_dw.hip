@@ -222,11 +222,8 @@ __global__ __launch_bounds__(NTHR) void gemm_dw_kernel(const bf16* __restrict__ 
 // 32x32x16 (isolated: qkv 333 -> 325 us, proj 125 -> 118, fc1 404 -> 400, fc2
 // 409 -> 403 for impl 1; step 144.7 -> 143.4 ms, profiles/r3_dw4_m16.md);
 // impl 0 = the 8-wave loop below.
-// PDO_DW_IMPL overrides (A/B in the step: tools/gpu.sh 'stepab:PDO_DW_IMPL=1 PDO_DW_IMPL=2')
-static int g_dw_impl = [] {
-  const char* e = getenv("PDO_DW_IMPL");
-  return e && *e ? atoi(e) : 1;
-}();
+// gemm_dw_impl() in the module selects one (probes and tests)
+static int g_dw_impl = 1;
 void gemm_dw_set_impl(int impl) { g_dw_impl = impl; }
 int gemm_dw_get_impl() { return g_dw_impl; }
 

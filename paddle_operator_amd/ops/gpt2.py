@@ -313,8 +313,9 @@ _NT_GELU = [True]
 _NT_DGELU = [True]
 
 # _NTMLPFn saves gelu' from the fc1 epilogue (EPI 7 / 8) instead of the
-# pre-activation; the environment switch off = the recomputing pair (EPI 2 / 3), the A/B alternative
-_NT_GD = [os.environ.get("PDO_NT_GD", "1") != "0"]
+# pre-activation (−0.8 ms/step, profiles/r5gd_saved_gelu_grad.md); False (test hook) =
+# the recomputing pair (EPI 2 / 3), kept under tests/test_ops_gpu.py
+_NT_GD = [True]
 
 
 def _nt_dgelu_ok(hp, w2) -> bool:

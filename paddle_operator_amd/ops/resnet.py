@@ -236,9 +236,9 @@ def _gemm_fwd_1x1(m, T, C, K) -> bool:
 
 
 # the 1×1 forward on gemm_nt takes the BatchNorm statistics in its epilogue
-# (gemm_nt EPI 9); the environment switch off = a
-# separate statistics pass over the output (the A/B alternative)
-_GEMM_BN_STATS = [os.environ.get("PDO_GEMM_BN_STATS", "1") != "0"]
+# (gemm_nt EPI 9, profiles/r5bs_gemm_bn_stats_epilogue.md); False (test hook) = a
+# separate statistics pass over the output
+_GEMM_BN_STATS = [True]
 
 
 def _fwd_stats_rows(m, conv: torch.nn.Conv2d, x) -> int:
@@ -576,7 +576,7 @@ class _BNActBNResFn(torch.autograd.Function):
 
 # ResNet's downsample block: bn3 and the downsample BatchNorm in one apply pass
 # (_BNActBNResFn); False = the downsample BatchNorm's own apply pass (A/B, tests)
-_DS_FUSED = [os.environ.get("PDO_DS_BN_FUSED", "1") != "0"]
+_DS_FUSED = [True]
 
 
 def conv_bn_ds_act(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x, dconv: torch.nn.Conv2d,

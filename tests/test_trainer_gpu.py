@@ -13,7 +13,7 @@ vocab 50304, S = 1024, B = 8, 2 layers) for 3 steps, against:
 * ``fw``: the same in bf16 (bf16 module, fp32 master copies, torch AdamW) — the
   framework's own bf16 error, the yardstick.
 
-Per parameter, the 3-step update (p₃ − p₀) of the production trainer must be
+Per parameter, the 3-step update (p₃ − p₀, fp32 master weights) of the production trainer must be
 within 1.5× the framework-bf16 update error against fp32 (+ 0.02 for tensors
 whose updates are sign-dominated at step 1-3, where both are O(0.1)); the loss
 trajectory within 2e-2 of fp32.  Also: the global-norm partials computed
@@ -66,7 +66,10 @@ def _worker(port, out):
         fresh = tr.opt.grad_norm_sq(tr.ddp.grad_scale).clone()
         res["norm_bits_equal"].append(bool(torch.equal(drained, fresh)))
     torch.cuda.synchronize()
-    ph = {n: p.detach().float().clone() for n, p in tr.model.named_parameters()}
+    # the trainer's fp32 master weights (a 3-step update, ≈ 3·lr, is below the bf16
+    # compute copy's ulp for O(1) weights such as the LayerNorm gains)
+    ph = {s.name: tr.opt.master[s.offset:s.offset + s.numel].view(s.shape).clone() for s in tr.flat.slots}
+    assert set(ph) == set(p0)
     dist.destroy_process_group()
 
     # fp32 truth and the framework's bf16 on plain torch ops, from the same p0

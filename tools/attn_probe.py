@@ -45,8 +45,6 @@ def main():
     o, lse = m.attn_fwd(qkv.view(B, S, 3 * H * D), H)
     res["pdo_fwd_us"] = bench(lambda: m.attn_fwd(qkv.view(B, S, 3 * H * D), H))
     res["pdo_bwd_us"] = bench(lambda: m.attn_bwd(dout.view(B, S, H * D), qkv.view(B, S, 3 * H * D), o, lse, H))
-    if os.environ.get("PDO_ATTN_PIPE") is not None:
-        res["pipe"] = os.environ["PDO_ATTN_PIPE"]
     # correctness vs SDPA (fp32 math on bf16 inputs)
     q, k, v = [qkv[:, :, i].transpose(1, 2) for i in range(3)]
     ref = F.scaled_dot_product_attention(q.float(), k.float(), v.float(), is_causal=True)

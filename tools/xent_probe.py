@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Fused LM-head cross-entropy pass (csrc/hip/xent.hip xent_fused) at the GPT-2-medium
 shape: µs per call and achieved TB/s (the logits read, dlogits written in place).
-PDO_XENT_REG=0 selects the two-read kernel (A/B, one process per setting).
 
     python tools/xent_probe.py [--tokens 65536] [--vocab 50257] [--vp 50304]
 """
@@ -39,7 +38,7 @@ def main():
     err = float((lg[:R, :a.vocab].float() - p / a.tokens).abs().max() * a.tokens)
     ref_loss = float(torch.nn.functional.cross_entropy(base[:, :a.vocab].float()[:4096], tgt[:4096]))
     t = sorted(bench(lambda: m.xent_fused(lg, tgt, inv, a.vocab), iters=5, warm=1) for _ in range(3))[1]
-    print(json.dumps({"reg": os.environ.get("PDO_XENT_REG", "1"), "us": round(t, 1),
+    print(json.dumps({"us": round(t, 1),
                       "TBps": round(2 * a.tokens * a.vp * 2 / t / 1e6, 2), "dlogit_err_x_count": err,
                       "loss": float(loss), "ref_loss_first4096": ref_loss}))
 
