@@ -58,13 +58,24 @@ def _worker(port, out):
     p0 = {n: p.detach().float().clone() for n, p in tr.model.named_parameters()}
     batches = [tr.batch() for _ in range(STEPS)]
 
-    res = {"loss_h": [], "loss_r": [], "loss_f": [], "norm_bits_equal": []}
+    res = {"loss_h": [], "loss_r": [], "loss_f": [], "norm_bits_equal": [], "gnorm_h": [], "gnorm_r": [],
+           "gnorm_f": []}
+    g1 = None
+    hist_h = []
     for x, y in batches:
         res["loss_h"].append(float(tr.step(x, y).item()))
         # the drain's per-bucket partials (already summed into _norm_buf) vs a fresh one-pass sum
         drained = tr.opt._norm_buf[0].clone()
         fresh = tr.opt.grad_norm_sq(tr.ddp.grad_scale).clone()
         res["norm_bits_equal"].append(bool(torch.equal(drained, fresh)))
+        res["gnorm_h"].append(float(drained.sqrt()))
+        # this step's arena gradients (after the split fold) and master weights, per parameter
+        gk = {s.name: tr.flat.param_grads[s.offset:s.offset + s.numel].view(s.shape).float().clone()
+              for s in tr.flat.slots}
+        hist_h.append((gk, {s.name: tr.opt.master[s.offset:s.offset + s.numel].view(s.shape).clone()
+                            for s in tr.flat.slots}))
+        if g1 is None:
+            g1 = gk
     torch.cuda.synchronize()
     # the trainer's fp32 master weights (a 3-step update, ≈ 3·lr, is below the bf16
     # compute copy's ulp for O(1) weights such as the LayerNorm gains)
@@ -86,7 +97,7 @@ def _worker(port, out):
         groups = [{"params": [q for q, p in zip(master, m.parameters()) if p.dim() >= 2], "weight_decay": 0.1},
                   {"params": [q for q, p in zip(master, m.parameters()) if p.dim() < 2], "weight_decay": 0.0}]
         opt = torch.optim.AdamW(groups, lr=tr.opt.lr, betas=(tr.opt.b1, tr.opt.b2), eps=tr.opt.eps)
-        losses = []
+        losses, norms, grads1, hist = [], [], None, []
         for x, y in batches:
             m.zero_grad(set_to_none=True)
             loss = m(x, y)
@@ -94,15 +105,30 @@ def _worker(port, out):
             losses.append(float(loss.item()))
             for q, p in zip(master, m.parameters()):
                 q.grad = p.grad.float()
-            torch.nn.utils.clip_grad_norm_(master, tr.opt.max_grad_norm)
+            if grads1 is None:
+                grads1 = {n: q.grad.clone() for (n, _), q in zip(m.named_parameters(), master)}
+            norms.append(float(torch.nn.utils.clip_grad_norm_(master, tr.opt.max_grad_norm)))
+            hist.append(({n: q.grad.clone() for (n, _), q in zip(m.named_parameters(), master)},))
             opt.step()
             with torch.no_grad():
                 for q, p in zip(master, m.parameters()):
                     p.copy_(q)
-        return losses, {n: q.detach().clone() for (n, _), q in zip(m.named_parameters(), master)}
+            hist[-1] += ({n: q.detach().clone() for (n, _), q in zip(m.named_parameters(), master)},)
+        return losses, norms, grads1, {n: q.detach().clone() for (n, _), q in zip(m.named_parameters(), master)}, hist
 
-    res["loss_r"], pr = run(torch.float32)
-    res["loss_f"], pf = run(torch.bfloat16)
+    res["loss_r"], res["gnorm_r"], gr1, pr, hist_r = run(torch.float32)
+    res["loss_f"], res["gnorm_f"], gf1, pf, hist_f = run(torch.bfloat16)
+
+    def rel(a, b):
+        return float((a - b).norm() / (b.norm() + 1e-20))
+    # per step k: (hip, framework bf16) errors of the step-k gradient and of the update p_k − p0
+    res["steps"] = {n: [(rel(hist_h[k][0][n], hist_r[k][0][n]), rel(hist_f[k][0][n], hist_r[k][0][n]),
+                         rel(hist_h[k][1][n] - p0[n], hist_r[k][1][n] - p0[n]),
+                         rel(hist_f[k][1][n] - p0[n], hist_r[k][1][n] - p0[n])) for k in range(STEPS)]
+                    for n in ("lnf_w", "lnf_b", "blocks.1.fc_proj.bias", "blocks.1.ln1_b", "blocks.0.ln1_w", "wte")}
+    # step-1 gradients: (hip, framework bf16) relative errors against fp32
+    res["errs_g"] = {n: (float((g1[n] - gr1[n]).norm() / (gr1[n].norm() + 1e-20)),
+                         float((gf1[n] - gr1[n]).norm() / (gr1[n].norm() + 1e-20))) for n in g1}
     errs = {}
     for n in ph:
         dr = pr[n] - p0[n]
@@ -129,6 +155,8 @@ def test_gpt2_trainer_steps_vs_fp32(tmp_path, cuda):
     assert all(res["norm_bits_equal"]), res["norm_bits_equal"]
     for i, (lh, lr_, lf) in enumerate(zip(res["loss_h"], res["loss_r"], res["loss_f"])):
         assert abs(lh - lr_) < 2e-2, (i, lh, lr_, lf)
+    bad = {n: (round(eh, 4), round(ef, 4)) for n, (eh, ef) in res["errs_g"].items() if not eh <= 1.5 * ef + 0.005}
+    assert not bad, ("step-1 gradients", bad)
     bad = {n: (round(eh, 4), round(ef, 4)) for n, (eh, ef) in res["errs"].items() if not eh <= 1.5 * ef + 0.02}
     worst = max(res["errs"].items(), key=lambda kv: kv[1][0] / (kv[1][1] + 1e-3))
     print("worst update error (hip, framework bf16):", worst)
