@@ -6,19 +6,21 @@ sums, ``BucketedDDP.finish(opt)`` with per-bucket global-norm partials (DDP on:
 a 1-rank RCCL communicator with ``PDO_DDP_ALWAYS=1``, so the hooks, bucket
 launches and partials all run), clipped fused ``FlatAdamW`` over the bf16
 arena with fp32 master weights — at GPT-2-medium width (C = 1024, 16 heads,
-vocab 50304, S = 1024, B = 8, 2 layers) for 3 steps, against:
+vocab 50304, S = 1024, B = 8, 2 layers) for 3 steps.
 
-* ``ref``: the SAME initial weights in fp32, plain torch ops (``PDO_OPS=torch``),
-  ``torch.optim.AdamW`` + ``clip_grad_norm_`` — the truth;
-* ``fw``: the same in bf16 (bf16 module, fp32 master copies, torch AdamW) — the
-  framework's own bf16 error, the yardstick.
+Teacher-forced per step (the trajectories of a sign-like Adam update diverge
+chaotically after one step: a single near-zero gradient whose bf16 sign differs
+moves one element by 2·lr, 6 % of a 1024-element update — measured, round 6):
 
-Per parameter, the 3-step update (p₃ − p₀, fp32 master weights) of the production trainer must be
-within 1.5× the framework-bf16 update error against fp32 (+ 0.02 for tensors
-whose updates are sign-dominated at step 1-3, where both are O(0.1)); the loss
-trajectory within 2e-2 of fp32.  Also: the global-norm partials computed
-per bucket during the drain equal a one-pass recomputation bit for bit
-(ddp.py:139).
+* gradients: at the trainer's own weights of that step, the production
+  gradient (arena, after the split fold) against the SAME weights in fp32 with
+  plain torch ops (``PDO_OPS=torch``) — every parameter within 1.5× the
+  framework's own bf16 error at those weights (+ 0.005) — and the loss;
+* optimizer: the fused clipped AdamW's master-weight update against
+  ``torch.optim.AdamW``'s formula + ``clip_grad_norm_`` in fp32 (fp64 norm)
+  applied to the same gradients and the trainer's own moments;
+* the global-norm partials computed per bucket during the drain equal a
+  one-pass recomputation bit for bit (ddp.py:139).
 """
 import os
 import socket
@@ -41,6 +43,10 @@ def _port():
     return p
 
 
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-30))
+
+
 def _worker(port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PDO_OPS="hip", PDO_DDP_ALWAYS="1")
     import torch.distributed as dist
@@ -55,86 +61,58 @@ def _worker(port, out):
     tr = GPT2Trainer(cfg, B, S, dev, bucket_mb=16)  # ≈ 10 buckets: partials and launches per bucket
     tr.sync_initial_weights()
     assert tr.ddp.enabled and len(tr.flat.buckets) >= 2 and tr.flat.aux_slots, "production composition not active"
-    p0 = {n: p.detach().float().clone() for n, p in tr.model.named_parameters()}
-    batches = [tr.batch() for _ in range(STEPS)]
+    opt, flat = tr.opt, tr.flat
+    slots = flat.slots
+    view = lambda buf, s: buf[s.offset:s.offset + s.numel].view(s.shape)  # noqa: E731
+    with torch.device(dev):
+        ref = GPT2(cfg)  # fp32
+        fw = GPT2(cfg).bfloat16()  # the framework in bf16
 
-    res = {"loss_h": [], "loss_r": [], "loss_f": [], "norm_bits_equal": [], "gnorm_h": [], "gnorm_r": [],
-           "gnorm_f": []}
-    g1 = None
-    hist_h = []
-    for x, y in batches:
-        res["loss_h"].append(float(tr.step(x, y).item()))
-        # the drain's per-bucket partials (already summed into _norm_buf) vs a fresh one-pass sum
-        drained = tr.opt._norm_buf[0].clone()
-        fresh = tr.opt.grad_norm_sq(tr.ddp.grad_scale).clone()
-        res["norm_bits_equal"].append(bool(torch.equal(drained, fresh)))
-        res["gnorm_h"].append(float(drained.sqrt()))
-        # this step's arena gradients (after the split fold) and master weights, per parameter
-        gk = {s.name: tr.flat.param_grads[s.offset:s.offset + s.numel].view(s.shape).float().clone()
-              for s in tr.flat.slots}
-        hist_h.append((gk, {s.name: tr.opt.master[s.offset:s.offset + s.numel].view(s.shape).clone()
-                            for s in tr.flat.slots}))
-        if g1 is None:
-            g1 = gk
-    torch.cuda.synchronize()
-    # the trainer's fp32 master weights (a 3-step update, ≈ 3·lr, is below the bf16
-    # compute copy's ulp for O(1) weights such as the LayerNorm gains)
-    ph = {s.name: tr.opt.master[s.offset:s.offset + s.numel].view(s.shape).clone() for s in tr.flat.slots}
-    assert set(ph) == set(p0)
-    dist.destroy_process_group()
-
-    # fp32 truth and the framework's bf16 on plain torch ops, from the same p0
-    os.environ["PDO_OPS"] = "torch"
-
-    def run(dtype):
-        with torch.device(dev):
-            m = GPT2(cfg)
+    def ref_grads(model, master, x, y):
+        """Loss and gradients of ``model`` (torch ops) at the trainer's master weights."""
+        params = dict(model.named_parameters())
         with torch.no_grad():
-            for n, p in m.named_parameters():
-                p.copy_(p0[n])
-        m.to(dtype)
-        master = [p.detach().float().clone().requires_grad_() for p in m.parameters()]
-        groups = [{"params": [q for q, p in zip(master, m.parameters()) if p.dim() >= 2], "weight_decay": 0.1},
-                  {"params": [q for q, p in zip(master, m.parameters()) if p.dim() < 2], "weight_decay": 0.0}]
-        opt = torch.optim.AdamW(groups, lr=tr.opt.lr, betas=(tr.opt.b1, tr.opt.b2), eps=tr.opt.eps)
-        losses, norms, grads1, hist = [], [], None, []
-        for x, y in batches:
-            m.zero_grad(set_to_none=True)
-            loss = m(x, y)
+            for s in slots:
+                params[s.name].copy_(view(master, s))
+        model.zero_grad(set_to_none=True)
+        os.environ["PDO_OPS"] = "torch"
+        try:
+            loss = model(x, y)
             loss.backward()
-            losses.append(float(loss.item()))
-            for q, p in zip(master, m.parameters()):
-                q.grad = p.grad.float()
-            if grads1 is None:
-                grads1 = {n: q.grad.clone() for (n, _), q in zip(m.named_parameters(), master)}
-            norms.append(float(torch.nn.utils.clip_grad_norm_(master, tr.opt.max_grad_norm)))
-            hist.append(({n: q.grad.clone() for (n, _), q in zip(m.named_parameters(), master)},))
-            opt.step()
-            with torch.no_grad():
-                for q, p in zip(master, m.parameters()):
-                    p.copy_(q)
-            hist[-1] += ({n: q.detach().clone() for (n, _), q in zip(m.named_parameters(), master)},)
-        return losses, norms, grads1, {n: q.detach().clone() for (n, _), q in zip(m.named_parameters(), master)}, hist
+        finally:
+            os.environ["PDO_OPS"] = "hip"
+        return float(loss.item()), {n: p.grad.float() for n, p in params.items()}
 
-    res["loss_r"], res["gnorm_r"], gr1, pr, hist_r = run(torch.float32)
-    res["loss_f"], res["gnorm_f"], gf1, pf, hist_f = run(torch.bfloat16)
-
-    def rel(a, b):
-        return float((a - b).norm() / (b.norm() + 1e-20))
-    # per step k: (hip, framework bf16) errors of the step-k gradient and of the update p_k − p0
-    res["steps"] = {n: [(rel(hist_h[k][0][n], hist_r[k][0][n]), rel(hist_f[k][0][n], hist_r[k][0][n]),
-                         rel(hist_h[k][1][n] - p0[n], hist_r[k][1][n] - p0[n]),
-                         rel(hist_f[k][1][n] - p0[n], hist_r[k][1][n] - p0[n])) for k in range(STEPS)]
-                    for n in ("lnf_w", "lnf_b", "blocks.1.fc_proj.bias", "blocks.1.ln1_b", "blocks.0.ln1_w", "wte")}
-    # step-1 gradients: (hip, framework bf16) relative errors against fp32
-    res["errs_g"] = {n: (float((g1[n] - gr1[n]).norm() / (gr1[n].norm() + 1e-20)),
-                         float((gf1[n] - gr1[n]).norm() / (gr1[n].norm() + 1e-20))) for n in g1}
-    errs = {}
-    for n in ph:
-        dr = pr[n] - p0[n]
-        den = float(dr.norm()) + 1e-12
-        errs[n] = (float((ph[n] - p0[n] - dr).norm()) / den, float((pf[n] - p0[n] - dr).norm()) / den)
-    res["errs"] = errs
+    res = {"loss": [], "norm_bits_equal": [], "grad_errs": [], "opt_err": [], "clip": []}
+    for k in range(STEPS):
+        x, y = tr.batch()
+        master0, m0, v0 = opt.master.clone(), opt.m.clone(), opt.v.clone()
+        loss_h = float(tr.step(x, y).item())
+        # the drain's per-bucket partials (already summed into _norm_buf) vs a fresh one-pass sum
+        drained = opt._norm_buf[0].clone()
+        fresh = opt.grad_norm_sq(tr.ddp.grad_scale).clone()
+        res["norm_bits_equal"].append(bool(torch.equal(drained, fresh)))
+        g_h = {s.name: view(flat.param_grads, s).float() * tr.ddp.grad_scale for s in slots}
+        loss_r, g_r = ref_grads(ref, master0, x, y)
+        loss_f, g_f = ref_grads(fw, master0, x, y)
+        res["loss"].append((loss_h, loss_r, loss_f))
+        res["grad_errs"].append({n: (_rel(g_h[n], g_r[n]), _rel(g_f[n], g_r[n])) for n in g_h})
+        # optimizer: torch's AdamW formula + clip on the trainer's own gradients and moments
+        gflat = flat.param_grads.float() * tr.ddp.grad_scale
+        norm = float(gflat.double().norm())
+        c = min(1.0, opt.max_grad_norm / (norm + 1e-6))
+        res["clip"].append((norm, float(drained.sqrt()), c))
+        g = gflat * c
+        t = opt.step_count
+        bc1, bc2 = 1 - opt.b1 ** t, 1 - opt.b2 ** t
+        m1 = opt.b1 * m0 + (1 - opt.b1) * g
+        v1 = opt.b2 * v0 + (1 - opt.b2) * g * g
+        dec = flat.decay_chunks.repeat_interleave(flat.numel // flat.decay_chunks.numel())
+        want = master0 * (1 - opt.lr * opt.wd * dec) - opt.lr * (m1 / bc1) / ((v1 / bc2).sqrt() + opt.eps)
+        res["opt_err"].append({s.name: _rel(view(opt.master, s) - view(master0, s), view(want, s) - view(master0, s))
+                               for s in slots})
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
     torch.save(res, out)
 
 
@@ -147,17 +125,19 @@ def test_gpt2_trainer_steps_vs_fp32(tmp_path, cuda):
     assert p.exitcode == 0, p.exitcode
     res = torch.load(out, weights_only=True)
     d = os.environ.get("PDO_TEST_DUMP_DIR")
-    if d:  # evidence for profiles/: losses, norm check, per-parameter (hip, framework bf16) update errors
+    if d:  # evidence for profiles/: per step losses, norm check, per-parameter (hip, framework bf16) errors
         import json
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "gpt2_trainer_anchor.json"), "w") as f:
             json.dump({k: v for k, v in res.items()}, f, indent=0)
     assert all(res["norm_bits_equal"]), res["norm_bits_equal"]
-    for i, (lh, lr_, lf) in enumerate(zip(res["loss_h"], res["loss_r"], res["loss_f"])):
-        assert abs(lh - lr_) < 2e-2, (i, lh, lr_, lf)
-    bad = {n: (round(eh, 4), round(ef, 4)) for n, (eh, ef) in res["errs_g"].items() if not eh <= 1.5 * ef + 0.005}
-    assert not bad, ("step-1 gradients", bad)
-    bad = {n: (round(eh, 4), round(ef, 4)) for n, (eh, ef) in res["errs"].items() if not eh <= 1.5 * ef + 0.02}
-    worst = max(res["errs"].items(), key=lambda kv: kv[1][0] / (kv[1][1] + 1e-3))
-    print("worst update error (hip, framework bf16):", worst)
-    assert not bad, bad
+    for k in range(STEPS):
+        lh, lr_, lf = res["loss"][k]
+        assert abs(lh - lr_) < 1e-2, (k, lh, lr_, lf)
+        norm, drained, _ = res["clip"][k]
+        assert abs(norm - drained) < 1e-4 * norm, (k, norm, drained)  # the drained partials' norm is the norm
+        bad = {n: (round(eh, 4), round(ef, 4)) for n, (eh, ef) in res["grad_errs"][k].items()
+               if not eh <= 1.5 * ef + 0.005}
+        assert not bad, ("gradients", k, bad)
+        bad = {n: e for n, e in res["opt_err"][k].items() if not e < 1e-4}
+        assert not bad, ("optimizer update", k, bad)

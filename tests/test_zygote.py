@@ -101,8 +101,16 @@ def test_slot_stuck_warming_is_killed_and_counted(tmp_path):
         # every retry got stuck too: killed SLOT_RETRIES times, then no more slots
         assert st["failed"]["0"] >= zygote.SLOT_RETRIES, st
         assert st["served"]["warm_timeouts"] >= zygote.SLOT_RETRIES
-        time.sleep(0.3)
+        # slots spawned before the retry budget ran out (the pool holds up to
+        # slots_per_gpu) hit their own deadline; none is respawned after that
+        t_end = time.time() + 30
+        while time.time() < t_end and "0" in zygote.query_status(path)["slots"]:
+            time.sleep(0.1)
         assert "0" not in zygote.query_status(path)["slots"]
+        n_failed = zygote.query_status(path)["failed"]["0"]
+        time.sleep(1.5)  # > PDO_SLOT_WARM_MAX_S: a respawned slot would have failed again by now
+        st = zygote.query_status(path)
+        assert "0" not in st["slots"] and st["failed"]["0"] == n_failed, st
     finally:
         _stop(p)
 

@@ -17,8 +17,8 @@
 #   'stepab:C1 C2 ..'   in-process GPT-2-medium step under each env config Ci (K=V[;K=V..]),
 #                       ROUNDS (default 3) interleaved rounds of STEPS (default 20) steps
 #   'resab:C1 C2 ..'    the same for the ResNet-50 step (tools/bench_resnet.py)
-#   'soab:SCRIPT ARGS'  A/B built extensions: every ab/*.so in turn over the tree's
-#                       _pdo_hip.so, python tools/SCRIPT ARGS with each, 2 rounds; restored after
+#   'soab:SCRIPT ARGS'  A/B built extensions: every ab/*.so (env:AB_GLOB=ab/x_*.so to pick) in turn
+#                       over the tree's _pdo_hip.so, python tools/SCRIPT ARGS with each, 2 rounds; restored after
 #   env:K=V             export K=V for the following steps
 set -o pipefail
 NAME=${1:?name}; shift
@@ -97,7 +97,7 @@ run_step() {
       local so=paddle_operator_amd/_pdo_hip.so round v out rc=0
       cp "$so" "$O/.tree_hip.so"
       for round in 1 2; do
-        for v in ab/*.so; do
+        for v in ${AB_GLOB:-ab/*.so}; do
           cp "$v" "$so"
           out=$(timeout -k 10 300 python "tools/${A[0]}" "${A[@]:1}" 2> "$O/soab.err") || { rc=1; tail -20 "$O/soab.err"; break 2; }
           echo "$round $(basename "$v" .so) $out"
