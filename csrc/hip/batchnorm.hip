@@ -183,10 +183,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
       ra.sh = *reinterpret_cast<const f32x8*>(rss + C + c);
     }
   };
-  auto one = [&](long long i, bf16x8 xb, bf16x8 rb) {
-    f32x8 v = preact(to_f32(xb), a);
+  if (HOIST) load_aff((int)(i0 % C8) * 8);
+  for (long long i = i0; i < n8; i += stride) {
+    if (!HOIST) load_aff((int)(i % C8) * 8);
+    f32x8 v = preact(to_f32(reinterpret_cast<const bf16x8*>(x)[i]), a);
     if (res) {
-      const f32x8 r = to_f32(rb);
+      const f32x8 r = to_f32(reinterpret_cast<const bf16x8*>(res)[i]);
       v += rss ? preact(r, ra) : r;
     }
     if (relu) {
@@ -201,30 +203,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) bits |= ((float)yb[j] > 0.f ? 1u : 0u) << j;
       mask[i] = (unsigned char)bits;
     }
-  };
-  const bf16x8* xv8 = reinterpret_cast<const bf16x8*>(x);
-  const bf16x8* rv8 = reinterpret_cast<const bf16x8*>(res);
-  if (HOIST) {
-    // two grid-stride vectors per lane per iteration (same channel chunk), every
-    // load issued before any math: twice the bytes in flight per wave
-    load_aff((int)(i0 % C8) * 8);
-    long long i = i0;
-    for (; i + stride < n8; i += 2 * stride) {
-      const bf16x8 x0 = xv8[i], x1 = xv8[i + stride];
-      bf16x8 r0 = x0, r1 = x1;
-      if (res) {
-        r0 = rv8[i];
-        r1 = rv8[i + stride];
-      }
-      one(i, x0, r0);
-      one(i + stride, x1, r1);
-    }
-    if (i < n8) one(i, xv8[i], res ? rv8[i] : xv8[i]);
-    return;
-  }
-  for (long long i = i0; i < n8; i += stride) {
-    load_aff((int)(i % C8) * 8);
-    one(i, xv8[i], res ? rv8[i] : xv8[i]);
   }
 }
 
@@ -403,31 +381,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     k1 = *reinterpret_cast<const f32x8*>(coef + C + c);
     k2 = *reinterpret_cast<const f32x8*>(coef + 2 * C + c);
   };
-  auto one = [&](long long i, const f32x8& xv, const f32x8& g) {
+  if (HOIST) load((int)(i0 % C8) * 8);
+  for (long long i = i0; i < n8; i += stride) {
+    if (!HOIST) load((int)(i % C8) * 8);
+    const f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(x)[i]);
+    const f32x8 g = relu_grad(dy, y, xv, a, i, relu);
     if (dres) reinterpret_cast<bf16x8*>(dres)[i] = to_bf16(g);
     reinterpret_cast<bf16x8*>(dx)[i] = to_bf16(k * g - k1 - k2 * (xv - mu));
-  };
-  const bf16x8* xv8 = reinterpret_cast<const bf16x8*>(x);
-  if (HOIST) {
-    // two grid-stride vectors per lane per iteration, loads first (bn_apply_kernel)
-    load((int)(i0 % C8) * 8);
-    long long i = i0;
-    for (; i + stride < n8; i += 2 * stride) {
-      const f32x8 x0 = to_f32(xv8[i]), x1 = to_f32(xv8[i + stride]);
-      const f32x8 g0 = relu_grad(dy, y, x0, a, i, relu), g1 = relu_grad(dy, y, x1, a, i + stride, relu);
-      one(i, x0, g0);
-      one(i + stride, x1, g1);
-    }
-    if (i < n8) {
-      const f32x8 x0 = to_f32(xv8[i]);
-      one(i, x0, relu_grad(dy, y, x0, a, i, relu));
-    }
-    return;
-  }
-  for (long long i = i0; i < n8; i += stride) {
-    load((int)(i % C8) * 8);
-    const f32x8 xv = to_f32(xv8[i]);
-    one(i, xv, relu_grad(dy, y, xv, a, i, relu));
   }
 }
 
@@ -452,33 +412,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_pair_kernel(
     rk1 = *reinterpret_cast<const f32x8*>(rcoef + C + c);
     rk2 = *reinterpret_cast<const f32x8*>(rcoef + 2 * C + c);
   };
+  if (HOIST) load((int)(i0 % C8) * 8);
   const Affine unused{};
-  const bf16x8* xv8 = reinterpret_cast<const bf16x8*>(x);
-  const bf16x8* rv8 = reinterpret_cast<const bf16x8*>(r);
-  auto one = [&](long long i, const f32x8& xv, const f32x8& rv, const f32x8& g) {
+  for (long long i = i0; i < n8; i += stride) {
+    if (!HOIST) load((int)(i % C8) * 8);
+    const f32x8 xv = to_f32(reinterpret_cast<const bf16x8*>(x)[i]);
+    const f32x8 rv = to_f32(reinterpret_cast<const bf16x8*>(r)[i]);
+    const f32x8 g = relu_grad(dy, reinterpret_cast<const bf16*>(mask), xv, unused, i, 2);
     reinterpret_cast<bf16x8*>(dx)[i] = to_bf16(k * g - k1 - k2 * (xv - mu));
     reinterpret_cast<bf16x8*>(dr)[i] = to_bf16(rk * g - rk1 - rk2 * (rv - rmu));
-  };
-  if (HOIST) {
-    // two grid-stride vectors per lane per iteration, loads first (bn_apply_kernel)
-    load((int)(i0 % C8) * 8);
-    long long i = i0;
-    for (; i + stride < n8; i += 2 * stride) {
-      const f32x8 x0 = to_f32(xv8[i]), x1 = to_f32(xv8[i + stride]);
-      const f32x8 r0 = to_f32(rv8[i]), r1 = to_f32(rv8[i + stride]);
-      const f32x8 g0 = relu_grad(dy, reinterpret_cast<const bf16*>(mask), x0, unused, i, 2);
-      const f32x8 g1 = relu_grad(dy, reinterpret_cast<const bf16*>(mask), x1, unused, i + stride, 2);
-      one(i, x0, r0, g0);
-      one(i + stride, x1, r1, g1);
-    }
-    if (i < n8) one(i, to_f32(xv8[i]), to_f32(rv8[i]), relu_grad(dy, reinterpret_cast<const bf16*>(mask),
-                                                                   to_f32(xv8[i]), unused, i, 2));
-    return;
-  }
-  for (long long i = i0; i < n8; i += stride) {
-    load((int)(i % C8) * 8);
-    const f32x8 xv = to_f32(xv8[i]);
-    one(i, xv, to_f32(rv8[i]), relu_grad(dy, reinterpret_cast<const bf16*>(mask), xv, unused, i, 2));
   }
 }
 
