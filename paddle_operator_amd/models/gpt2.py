@@ -163,7 +163,7 @@ class GPT2(nn.Module):
         cfg = self.cfg
         x = ops.embedding(idx, self.wte, self.wpe)
         blk0 = self.blocks[0]
-        h = ops.layer_norm(x, blk0.ln1_w, blk0.ln1_b, cfg.ln_eps)
+        x, h = ops.layer_norm_res(x, blk0.ln1_w, blk0.ln1_b, cfg.ln_eps)
         for i, blk in enumerate(self.blocks):
             if i + 1 < len(self.blocks):
                 nb = self.blocks[i + 1]

@@ -15,7 +15,7 @@ from .core import (  # noqa: F401
     ref_cross_entropy, ref_layer_norm, transpose, use_hip)
 from .gpt2 import (  # noqa: F401
     _LMHeadXentFn, _LM_CHUNK, _QKV_FUSED, _RES_EPI, _XENT_FUSED, _NT_GELU, _NT_DGELU, _NT_GD, add_layer_norm,
-    attention, bias_gelu, cross_entropy, embedding, layer_norm, linear_add_layer_norm, lm_head_xent, mlp, mlp_add_layer_norm,
+    attention, bias_gelu, cross_entropy, embedding, layer_norm, layer_norm_res, linear_add_layer_norm, lm_head_xent, mlp, mlp_add_layer_norm,
     qkv_attention)
 from .resnet import (  # noqa: F401
     _BNActBNResFn, _BNLink, _BNReluPoolFn, _CompactGradLink, _ResMaskLink, _StemFn, _BN_FUSED, _DS_FUSED,
@@ -25,7 +25,7 @@ from .resnet import (  # noqa: F401
     max_pool_3x3s2)
 
 __all__ = [
-    "layer_norm", "add_layer_norm", "bias_gelu", "attention", "cross_entropy",
+    "layer_norm", "layer_norm_res", "add_layer_norm", "bias_gelu", "attention", "cross_entropy",
     "embedding", "ref_layer_norm", "ref_bias_gelu", "ref_attention",
     "ref_cross_entropy", "use_hip", "linear", "mlp", "qkv_attention", "lm_head_xent",
     "conv_bn_act", "conv_bn_ds_act", "bn_act", "deferred_reductions",

@@ -128,6 +128,16 @@ class _LNResFn(torch.autograd.Function):
         return dx, outs[1], outs[2], (outs[3] if ctx.has_rbias else None), None
 
 
+def layer_norm_res(x, w, b, eps=1e-5):
+    """(x, LN(x)) for a residual-stream tensor that also continues past the
+    LayerNorm (GPT-2's embedding output feeding block 0): x is returned as an
+    alias (_LNResFn), so its downstream gradient joins the LayerNorm backward in
+    one kernel instead of a separate [tokens, C] add."""
+    if use_hip(x) and x.is_contiguous():
+        return _LNResFn.apply(x, w, b, None, eps)
+    return x, layer_norm(x, w, b, eps)
+
+
 class _LinearResFn(torch.autograd.Function):
     """h = a·Wᵀ + b + x on gemm_nt4's EPI 5 (bias and the residual stream x
     summed in the register epilogue, one rounding).  ``b`` is taken as a
