@@ -26,6 +26,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$NAME; mkdir -p "$O"
 export TMPDIR=/tmp
 cd "$R" || exit 1
 PMC_PASS=0
+BENCH_PASS=0
 PROF_PASS=0
 say() { echo "[gpu.sh $(date +%H:%M:%S)] $*"; }
 
@@ -45,10 +46,13 @@ run_step() {
         || { tail -40 "$O/smoke.log"; return 1; }
       tail -2 "$O/smoke.log" ;;
     bench)
+      BENCH_PASS=$((BENCH_PASS + 1))
       local b=(--gpus 1 --steps 20 --warmup 5); [[ -n $arg ]] && b=("${A[@]}")
-      timeout -k 10 600 python bench.py "${b[@]}" > "$O/bench.json" 2> "$O/bench.err" \
-        || { tail -60 "$O/bench.err"; return 1; }
-      cat "$O/bench.json" ;;
+      local bj=$O/bench.json be=$O/bench.err
+      (( BENCH_PASS > 1 )) && { bj=$O/bench$BENCH_PASS.json; be=$O/bench$BENCH_PASS.err; }
+      timeout -k 10 600 python bench.py "${b[@]}" > "$bj" 2> "$be" \
+        || { tail -60 "$be"; return 1; }
+      cat "$bj" ;;
     probe)
       local s=${A[0]}
       timeout -k 10 600 python -u "tools/$s" "${A[@]:1}" > "$O/probe_${s%.py}.log" 2>&1 \
