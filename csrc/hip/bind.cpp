@@ -515,7 +515,7 @@ std::vector<at::Tensor> gemm_nt_dgelu(at::Tensor a, at::Tensor b, at::Tensor pre
   const int M = a.size(0), N = b.size(0), K = a.size(1);
   TORCH_CHECK(pre.dim() == 2 && pre.size(0) == M && pre.size(1) == N && bias.numel() == N);
   auto dx = at::empty({M, N}, a.options());
-  const int G = pdo::gemm_nt_dbias_rows(M);
+  const int G = pdo::gemm_nt_dbias_rows(M, K);
   auto part = at::empty({(int64_t)G * N + pdo::colsum_scratch_floats(G, N)}, a.options().dtype(at::kFloat));
   CHECK_RC(pdo::gemm_nt(bp(a), bp(b), M, N, K, K, K, bp(dx), N, saved_grad ? 8 : 3, bp(bias), bp(pre), N, fp(part),
                         cur_stream()),

@@ -306,7 +306,9 @@ int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc) {
          ldc % 4 == 0 && lda >= K && ldb >= K && ldc >= N;
 }
 
-int gemm_nt_dbias_rows(int M) { return 8 * (M / BM); }
+// partial rows of the EPI 3 / 8 bias gradient: 8 per 256-row tile on the 8-wave
+// ring, 2 on the 4-wave mainloop (its lane groups merge in-register)
+int gemm_nt_dbias_rows(int M, int K) { return (nt4_path(K) ? 2 : 8) * (M / BM); }
 int gemm_nt_epi_ok(int M, int N, int K) { return gemm_nt_ok(M, N, K, K, K, N) && nt4_path(K); }
 // rows per BatchNorm partial of EPI 9: a (tile, wm) half on the 4-wave mainloop, the tile on the ring
 int gemm_nt_stats_rows(int K) { return nt4_path(K) ? BM / 2 : BM; }

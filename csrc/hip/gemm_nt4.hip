@@ -347,10 +347,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
       }
     }
     if constexpr (EPI == 3 || EPI == 8) {
-      // partial row 4·wm + (l >> 4) of this M-tile's 8: the rows 16i + 4(l >> 4) + e
-      float* prow = dbias_part + (size_t)(8 * tm + 4 * wm + g4) * N + nb;
-      *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
-      *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
+      // the four lane groups (same 8 columns, rows 4·g4 + …) merged by xor-16 /
+      // xor-32 exchanges: partial row 2·tm + wm (gemm_nt4_dbias_rows) holds this
+      // wave's 128 rows — a quarter of the partial bytes of one row per lane group
+#pragma unroll
+      for (int x = 16; x <= 32; x *= 2)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) colp[k] += __shfl_xor(colp[k], x, 64);
+      if (g4 == 0) {
+        float* prow = dbias_part + (size_t)(2 * tm + wm) * N + nb;
+        *reinterpret_cast<f32x4*>(prow) = f32x4{colp[0], colp[1], colp[2], colp[3]};
+        *reinterpret_cast<f32x4*>(prow + 4) = f32x4{colp[4], colp[5], colp[6], colp[7]};
+      }
     }
   };
 

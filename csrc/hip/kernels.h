@@ -166,13 +166,13 @@ int gemm_dw_get_impl();
 // transpose.hip: out[C][R] = in[R][C], R and C multiples of 64
 // gemm_nt.hip: C[M][N] = A[M][K]·B[N][K]ᵀ with a fused epilogue
 // (0 plain, 1 +bias, 2 C = pre-activation & Y = gelu(C + bias),
-//  3 C = (A·Bᵀ)⊙gelu'(Y + bias) & fp32 column partials [gemm_nt_dbias_rows(M)][N])
+//  3 C = (A·Bᵀ)⊙gelu'(Y + bias) & fp32 column partials [gemm_nt_dbias_rows(M, K)][N])
 int gemm_nt_ok(int M, int N, int K, int lda, int ldb, int ldc);
 // EPI 7 / 8 / 9 (the 4-wave mainloop's epilogues) apply to this product
 int gemm_nt_epi_ok(int M, int N, int K);
 // rows per BatchNorm partial row of EPI 9 (gemm_nt with the statistics epilogue)
 int gemm_nt_stats_rows(int K);
-int gemm_nt_dbias_rows(int M);
+int gemm_nt_dbias_rows(int M, int K);
 int gemm_nt(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb, bf16* C, int ldc, int epi,
             const bf16* bias, bf16* Y, int ldy, float* dbias_part, hipStream_t st);
 // gemm_nt4.hip: the same contract on the 4-wave / 128 × 128-per-wave mainloop
