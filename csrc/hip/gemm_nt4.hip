@@ -26,9 +26,10 @@
 // A / B panels stay in L2).
 //
 // Persistent workgroups (grid = one per CU, virtual tile ids blockIdx.x +
-// k·gridDim.x): the next tile's first two k-tiles are issued before this
-// tile's register epilogue, so their HBM latency hides behind the epilogue's
-// conversions and stores.  Runs of 8 MFMAs share the B fragment (K ≤ 1024) or,
+// k·gridDim.x): the next tile's first two k-tiles are issued inside this
+// tile's last k-tile, right after its last LDS reads (round 6; before: at the
+// tile boundary), so their HBM latency hides behind the last MFMAs and the
+// register epilogue's conversions and stores.  Runs of 8 MFMAs share the B fragment (K ≤ 1024) or,
 // mirrored, the A fragment (K > 1024) — tools/nt4_probe.py,
 // profiles/r3_gemm_nt4_rows.md.
 //
@@ -190,6 +191,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 
   f32x4 acc[8][8];  // first written by mma0 in tile 0's block 0
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  // the last k-tile of a tile issues the NEXT tile's first two k-tiles (after its
+  // own last LDS reads, s ≥ 49) instead of the tile boundary doing it: ≈ 80 MFMAs
+  // more lead for those pieces.  EPI 8 also loads the first 16 of the epilogue's
+  // 32 gelu' rows there (into fa0 / fb0's registers, dead after slot 63)
+  constexpr bool EARLY8 = EPI == 8;
+  bool has_next = false;
+  int ntm = 0, ntn = 0;
+  Src nx0{}, nx1{};
+  bf16x8 pre_early[EARLY8 ? 16 : 1];
 
   // ---- epilogue ----
   // The accumulators leave the accumulator file through explicit
@@ -223,7 +233,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     unsigned char mk[EPI == 6 ? 32 : 1];  // EPI 6: the addend's keep bits (8 columns per byte)
     if constexpr (PRE) {
 #pragma unroll
-      for (int u = 0; u < 32; ++u) pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
+      for (int u = 0; u < 32; ++u) {
+        if constexpr (EARLY8) {
+          if (u < 16) {
+            pre[u] = pre_early[u];
+            continue;
+          }
+        }
+        pre[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
+      }
     }
     if constexpr (EPI == 6) {
       const unsigned char* mask = reinterpret_cast<const unsigned char*>(bias);
@@ -402,11 +420,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   //   s 51            lgkmcnt(0), barrier 2
   //   s 52-87 (÷5)    B pieces of t+2      s 93        vmcnt(t+2 pieces), barrier 3
   //   s 94-124 (even) F0 reads of t+1 (other buffer)
-  auto tile3 = [&](int t, auto buf_tag, auto first_tag, auto more_tag, auto load_tag) {
+  auto tile3 = [&](int t, auto buf_tag, auto first_tag, auto more_tag, auto load_tag,
+                   auto lastk_tag) {
     constexpr int BUF = decltype(buf_tag)::value;
     constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
     constexpr bool LOAD = decltype(load_tag)::value;
+    constexpr bool LASTK = decltype(lastk_tag)::value;
     using NB = std::integral_constant<int, BUF ^ 1>;
     using SB = std::integral_constant<int, BUF>;
     Src sn2{};
@@ -453,6 +473,35 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         __builtin_amdgcn_s_barrier();
       }
       if constexpr (MORE && s >= 94 && s < 126 && (s & 1) == 0) rdF0(NB{}, (s - 94) >> 1);
+      if constexpr (LASTK) {
+        if constexpr (s == 49) {
+          if (has_next) {
+            // every wave's last LDS reads of this tile precede any wave's refill
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            baseA = A + ((size_t)ntm * BM + 8 * w) * lda;
+            baseB = B + ((size_t)ntn * BN + 64 * (w & 1) + (w >> 1)) * ldb;
+            dhalfn = ntn * BN + BN > N;
+            nx0 = srcs(0);
+            nx1 = srcs(1);
+          }
+        }
+        if constexpr (s >= 50 && s < 66) {
+          if (has_next) dma(nx0, B0{}, s - 50);
+        }
+        if constexpr (s >= 66 && s < 82) {
+          if (has_next) dma(nx1, B1{}, s - 66);
+        }
+        if constexpr (EARLY8 && s >= 83 && s < 115 && (s & 1)) {
+          constexpr int u = (s - 83) >> 1;
+          const int g4 = lane >> 4;
+          const size_t mr = (size_t)(m0 + wm * 128 + 4 * g4);
+          // a half-width tile's wn = 1 waves store nothing: their (unused) rows stay in bounds
+          const int nb = n0 + ((halfn && wn == 1) ? 0 : wn * 128) + 8 * (lane & 15);
+          pre_early[u] = *reinterpret_cast<const bf16x8*>(Y + (mr + 16 * (u >> 2) + (u & 3)) * ldy + nb);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
   };
@@ -468,27 +517,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 #pragma unroll
     for (int q = 0; q < 16; ++q) rdF0(B0{}, q);
     // nk is even and ≥ 4 (host contract): pairs of tiles keep the buffer index static
-    tile3(0, B0{}, T_{}, T_{}, T_{});
-    tile3(1, B1{}, F_{}, T_{}, T_{});
+    tile3(0, B0{}, T_{}, T_{}, T_{}, F_{});
+    tile3(1, B1{}, F_{}, T_{}, T_{}, F_{});
     for (int t = 2; t < nk - 2; t += 2) {
-      tile3(t, B0{}, F_{}, T_{}, T_{});
-      tile3(t + 1, B1{}, F_{}, T_{}, T_{});
+      tile3(t, B0{}, F_{}, T_{}, T_{}, F_{});
+      tile3(t + 1, B1{}, F_{}, T_{}, T_{}, F_{});
     }
-    tile3(nk - 2, B0{}, F_{}, T_{}, F_{});
-    tile3(nk - 1, B1{}, F_{}, F_{}, F_{});
+    tile3(nk - 2, B0{}, F_{}, T_{}, F_{}, F_{});
     const int vn = vcur + (int)gridDim.x;
-    if (vn >= nwg) break;
-    int ntm, ntn;
-    coords(vn, ntm, ntn);
-    // every wave's last LDS reads of this tile precede any wave's refill
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    baseA = A + ((size_t)ntm * BM + 8 * w) * lda;
-    baseB = B + ((size_t)ntn * BN + 64 * (w & 1) + (w >> 1)) * ldb;
-    dhalfn = ntn * BN + BN > N;
-    issue01();
+    has_next = vn < nwg;
+    if (has_next) coords(vn, ntm, ntn);
+    tile3(nk - 1, B1{}, F_{}, F_{}, F_{}, T_{});  // issues the next tile's k-tiles 0 and 1 (has_next)
+    if (!has_next) break;
     row_epilogue();  // of this tile (m0, n0, tm, halfn)
     vcur = vn;
     tm = ntm;
