@@ -517,7 +517,8 @@ def orchestrate(a):
                 "data": "synthetic (on-device random 224x224 images and labels), random-init weights",
                 "config": {"model": "resnet18-like-tiny (CPU rehearsal)" if a.virtual_gpus else "resnet50", "global_batch": mb2 * N,
                            "micro_batch_per_gpu": mb2, "resolution": 32 if a.virtual_gpus else 224,
-                           "parallelism": f"dp{N}", "pod_layout": f"{pods}x{N // pods}"},
+                           "parallelism": f"dp{N}", "pod_layout": f"{pods}x{N // pods}",
+                           "step": "hip-graph replay" if all(r.get("hip_graph") for r in r2) else "eager"},
                 "max_mem_gb": max((r.get("max_mem_gb") or 0) for r in r2),
                 "comm": _comm_summary(r2), "gang": _gang_summary(out.get("resnet_gang"))}
         elif out.get("resnet_error"):

@@ -34,6 +34,9 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=0, help="per-rank micro batch (0 = workload default)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--tiny", action="store_true", help="tiny model variant (CPU tests)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="resnet50: keep the step eager (default on one GPU rank: captured once into a HIP graph "
+                         "and replayed, workloads/resnet.py; multi-rank steps stay eager)")
     ap.add_argument("--backend", default=None, help="nccl (RCCL) | gloo; default by device")
     ap.add_argument("--nproc-per-pod", type=int, default=int(os.environ.get("PDO_NPROC_PER_POD", "1") or 1),
                     help="ranks this pod runs, one per GPU it was given (amd.com/gpu: N): RANK = "
@@ -89,7 +92,7 @@ def run_collective(args, jenv) -> int:
         tokens_per_step = trainer.tokens_per_step()
     elif args.workload == "resnet50":
         from ..workloads.resnet import ResNetTrainer
-        trainer = ResNetTrainer(args.batch or (4 if args.tiny else 256), dev, tiny=args.tiny)
+        trainer = ResNetTrainer(args.batch or (4 if args.tiny else 256), dev, tiny=args.tiny, graph=args.graph)
         trainer.sync_initial_weights()
         tokens_per_step = trainer.B  # images
     start_step = 0
@@ -199,7 +202,8 @@ def _bench(args, b, jenv, trainer, tokens_per_step, ready_rec) -> int:
            "ready_s": ready_rec["t_ready"] - T_START, "t_ready": ready_rec["t_ready"],
            "backend": b.backend, "device": str(dev),
            "grad_reduce": getattr(getattr(trainer, "ddp", None), "grad_reduce", None),
-           "buckets": len(trainer.flat.buckets) if hasattr(trainer, "flat") else None}
+           "buckets": len(trainer.flat.buckets) if hasattr(trainer, "flat") else None,
+           "hip_graph": getattr(trainer, "_graph", None) is not None}
     if dev.type == "cuda":
         res["gpu_name"] = torch.cuda.get_device_name(dev)
         res["max_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 2)

@@ -56,7 +56,16 @@ class FlatSGD:
 
 
 class ResNetTrainer:
-    def __init__(self, batch: int, device, tiny: bool = False, bucket_mb: int = 25, channels_last: bool = True):
+    """``graph=True``: after two eager warm-up steps the whole training step
+    (weight cast, forward, loss, backward, SGD update) is captured once into a
+    HIP graph (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and every later
+    ``step()`` is one graph launch behind a fresh draw of the synthetic batch
+    into the captured input buffers.  Single-rank only: with the bucketed
+    all-reduce enabled the step stays eager (RCCL collectives on the overlap
+    stream are not captured)."""
+
+    def __init__(self, batch: int, device, tiny: bool = False, bucket_mb: int = 25, channels_last: bool = True,
+                 graph: bool = False):
         from .. import _native
         if _native.ops_mode() == "torch":  # the framework reference path: MIOpen convolutions
             from ..utils.tuning import use_shipped_miopen_db
@@ -77,6 +86,9 @@ class ResNetTrainer:
         self.res = 32 if tiny else 224
         self.classes = 10 if tiny else 1000
         self.gen = torch.Generator(device=self.device).manual_seed(dist.get_rank() if dist.is_initialized() else 0)
+        self.graph = bool(graph) and self.device.type == "cuda" and not self.ddp.enabled
+        self._graph = None  # (CUDAGraph, x buffer (NHWC), x view, labels, loss) once captured
+        self._eager_steps = 0
 
     def sync_initial_weights(self):
         self.ddp.broadcast_params(0)
@@ -102,7 +114,37 @@ class ResNetTrainer:
         return x, y
 
     def step(self):
+        """One training step; returns the loss tensor (in graph mode the captured
+        loss buffer, overwritten by the next step)."""
+        if self._graph is not None:
+            g, xb, _, yb, loss = self._graph
+            self._draw(xb, yb)
+            g.replay()
+            self.opt.step_count += 1
+            return loss
+        if self.graph and self._eager_steps >= 2:
+            return self._capture()
+        self._eager_steps += 1
         x, y = self.batch()
+        return self._step(x, y)
+
+    def _capture(self):
+        """Capture one training step on a side stream (the allocator's graph pool
+        holds every tensor the step allocates), then run it: the first graph step."""
+        xb, x, yb = self._batch_buffers()
+        cur = torch.cuda.current_stream(self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(cur)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                loss = self._step(x, yb)
+        cur.wait_stream(side)
+        self.opt.step_count -= 1  # recorded, not run
+        self._graph = (g, xb, x, yb, loss)
+        return self.step()
+
+    def _step(self, x, y):
         self.flat.zero_grad()
         self.ddp.prepare()
         # bf16 copies of the fp32 master weights: one cast of the arena per step

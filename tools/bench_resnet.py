@@ -1,6 +1,9 @@
 """ResNet-50 training throughput (img/s) on one GPU — BASELINE configs 2/3/5 workload.
 
-    python tools/bench_resnet.py [--batch 256] [--steps 20] [--warmup 10]
+    python tools/bench_resnet.py [--batch 256] [--steps 20] [--warmup 10] [--graph]
+
+--graph: the step captured once into a HIP graph (ResNetTrainer(graph=True)),
+replayed behind a fresh batch draw.
 """
 import argparse
 import json
@@ -16,6 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--graph", action="store_true")
     a = ap.parse_args()
     import torch
     from paddle_operator_amd.workloads.resnet import ResNetTrainer
@@ -30,7 +34,7 @@ def main():
         ops_resnet._direct_cl_ok = lambda p: (ops_core._direct_ok(p) and p.grad.dtype == torch.float32
                                               and p.grad.is_contiguous(memory_format=torch.channels_last))
     t0 = time.time()
-    tr = ResNetTrainer(a.batch, "cuda:0")
+    tr = ResNetTrainer(a.batch, "cuda:0", graph=a.graph)
     for _ in range(a.warmup):
         tr.step()
     torch.cuda.synchronize()
@@ -43,7 +47,7 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.steps
     print(json.dumps({"metric": "ResNet-50 train img/s (bf16 autocast, channels_last)", "value": round(a.batch / ms * 1e3, 1),
-                      "ms_per_step": round(ms, 2), "batch": a.batch, "warmup_s": round(t_warm, 1),
+                      "ms_per_step": round(ms, 2), "batch": a.batch, "graph": tr._graph is not None, "warmup_s": round(t_warm, 1),
                       "loss": float(loss.detach()), "miopen_find_mode": os.environ.get("MIOPEN_FIND_MODE", "default")}))
 
 
