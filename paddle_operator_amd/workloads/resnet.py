@@ -137,7 +137,9 @@ class ResNetTrainer:
         side.wait_stream(cur)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
-            with torch.cuda.graph(g, stream=side):
+            # thread_local: a process group's watchdog thread queries its events
+            # while this thread captures (global mode would fail those calls)
+            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                 loss = self._step(x, yb)
         cur.wait_stream(side)
         self.opt.step_count -= 1  # recorded, not run
@@ -155,7 +157,10 @@ class ResNetTrainer:
         loss.backward()
         self.ddp.finish()
         self.opt.step(self.ddp.grad_scale)
-        return loss
+        # detached: a caller holding the loss must not keep this step's autograd
+        # graph (and its AccumulateGrad nodes, bound to this step's stream) alive
+        # into the next step — that breaks the graph capture of the third step
+        return loss.detach()
 
     def state_dict(self):
         return {"params": self.flat.params, "opt_buf": self.opt.buf, "buffers": {k: v for k, v in

@@ -71,6 +71,20 @@ def test_resnet50_graph_replay_matches_eager(cuda):
 
 
 @pytest.mark.gpu
+def test_launcher_resnet50_graph_bench(cuda):
+    """The launched ResNet-50 rank (RCCL process group up, as bench.py's
+    secondary job) captures its step into a HIP graph and replays it."""
+    env = dict(os.environ, PYTHONPATH=REPO, POD_IP="127.0.0.1", PADDLE_PORT="36510")
+    out = subprocess.run([sys.executable, "-m", "paddle_operator_amd.launch", "--workload", "resnet50", "--batch", "16",
+                          "--bench", "--steps", "3", "--warmup", "3"],
+                         env=env, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    rec = [json.loads(l[10:]) for l in out.stdout.splitlines() if l.startswith("PDO_BENCH ")]
+    assert rec and rec[0]["hip_graph"] is True and rec[0]["backend"] == "nccl", rec
+    assert rec[0]["loss"] == rec[0]["loss"]  # finite, not NaN
+
+
+@pytest.mark.gpu
 def test_launcher_gpt2_single_gpu(cuda, tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, POD_IP="127.0.0.1", PADDLE_PORT="36500")
     out = subprocess.run([sys.executable, "-m", "paddle_operator_amd.launch", "--workload", "gpt2", "--tiny",
