@@ -1307,6 +1307,12 @@ PYBIND11_MODULE(_pdo_hip, m) {
     if (impl >= 0) pdo::gemm_nt_set_impl(impl);
     return prev;
   }, py::arg("impl") = -1, "select gemm_nt's mainloop (0 = 8-wave ring, 1 = 4-wave); returns the previous");
+  m.def("gemm_nt4_dynamic", [](int on) {
+    static int cur = 0;
+    const int prev = cur;
+    if (on >= 0) pdo::gemm_nt4_set_dynamic(cur = on);
+    return prev;
+  }, py::arg("on") = -1, "gemm_nt4 tile order: 1 = dynamic per-XCD counters, 0 = static (default); returns the previous");
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("out") = py::none());
   m.def("gemm_nt_gelu", &gemm_nt_gelu, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("saved_grad") = false);
   m.def("gemm_nt_dgelu", &gemm_nt_dgelu, py::arg("a"), py::arg("b"), py::arg("pre"), py::arg("bias"),

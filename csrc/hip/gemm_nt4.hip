@@ -46,6 +46,7 @@
 // deferred activation epilogue that ran the GELU / GELU′ pass one element
 // stage per MFMA slot under the next tile's k-loop: fc1 + GELU 565 vs 496 µs,
 // fc2 dX ⊙ GELU′ 730 vs 552 µs (r5_deferred_activation_epilogue.md).
+#include <atomic>
 #include <type_traits>
 #include <utility>
 
@@ -80,8 +81,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
                                                            int lda, int ldb, int M, int N, int nk,
                                                            bf16* __restrict__ C, int ldc,
                                                            const bf16* __restrict__ bias, bf16* __restrict__ Y,
-                                                           int ldy, float* __restrict__ dbias_part, int group_m) {
+                                                           int ldy, float* __restrict__ dbias_part, int group_m,
+                                                           unsigned* __restrict__ sched) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * 2 * 256 * BK];  // [buf][A|B][256][64]
+  __shared__ int s_next;  // dynamic order: the next virtual tile id, wave 0 → all
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -102,6 +105,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     tm_ = first_m + r % gsz;
     tn_ = r / gsz;
   };
+  // Tile order.  First tile: virtual id blockIdx.x.  Static (sched = nullptr):
+  // then + k·gridDim.x.  Dynamic: the next id of this workgroup's XCD comes
+  // from that XCD's counter sched[xcd] (ids xcd + 8j past the first round), so
+  // a workgroup that starts late — its CU held by another kernel, e.g. an RCCL
+  // all-reduce on the overlap stream at N > 1 — leaves its tiles to the running
+  // ones instead of extending the kernel by the hold (tools/overlap_probe.py:
+  // one CU held for 267 µs took the static fc1 dX GEMM from 397 to 592 µs).
+  // The ticket is taken with the last DMA pieces of the tile (k-tile nk − 3)
+  // and waited for with them; the last workgroup out resets the counters.
+  const bool dyn = sched != nullptr;
+  const int xq = blockIdx.x & 7, j0 = ((int)gridDim.x - xq + 7) >> 3;
+  unsigned ticket = 0;
+  int vnext = 0;
   int vcur = blockIdx.x;
   int tn, tm;
   coords(vcur, tm, tn);
@@ -421,7 +437,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
   //   s 52-87 (÷5)    B pieces of t+2      s 93        vmcnt(t+2 pieces), barrier 3
   //   s 94-124 (even) F0 reads of t+1 (other buffer)
   auto tile3 = [&](int t, auto buf_tag, auto first_tag, auto more_tag, auto load_tag,
-                   auto lastk_tag) {
+                   auto lastk_tag, bool tk = false) {
     constexpr int BUF = decltype(buf_tag)::value;
     constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
@@ -462,10 +478,17 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         __builtin_amdgcn_s_barrier();
       }
       if constexpr (LOAD && s >= 52 && s < 92 && (s - 52) % 5 == 0) dma(sn2, SB{}, (MIR ? 0 : 8) + (s - 52) / 5);
+      if constexpr (LOAD && s == 92) {
+        if (dyn && tk && w == 0 && lane == 0) ticket = atomicAdd(sched + xq, 1u);
+      }
       if constexpr (MORE && s == 93) {
-        // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in flight)
+        // this wave's tile t+1 pieces retired (its 16 tile t+2 pieces may stay in
+        // flight; wave 0 of a ticket tile: those and the ticket's atomic)
         if constexpr (LOAD) {
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          if (dyn && tk && w == 0)
+            asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -473,13 +496,25 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
         __builtin_amdgcn_s_barrier();
       }
       if constexpr (MORE && s >= 94 && s < 126 && (s & 1) == 0) rdF0(NB{}, (s - 94) >> 1);
+      if constexpr (MORE && !LOAD && s == 95) {  // k-tile nk − 2: the ticket has returned (vmcnt(0) at 93)
+        if (dyn && w == 0) s_next = xq + 8 * (j0 + (int)__builtin_amdgcn_readfirstlane(ticket));
+      }
       if constexpr (LASTK) {
         if constexpr (s == 49) {
-          if (has_next) {
-            // every wave's last LDS reads of this tile precede any wave's refill
+          // every wave's last LDS reads of this tile precede any wave's refill
+          if (dyn) {  // (the barrier also publishes s_next)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
+            vnext = __builtin_amdgcn_readfirstlane(s_next);
+            has_next = vnext < nwg;
+            if (has_next) coords(vnext, ntm, ntn);
+          } else if (has_next) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+          }
+          if (has_next) {
             baseA = A + ((size_t)ntm * BM + 8 * w) * lda;
             baseB = B + ((size_t)ntn * BN + 64 * (w & 1) + (w >> 1)) * ldb;
             dhalfn = ntn * BN + BN > N;
@@ -518,19 +553,21 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     for (int q = 0; q < 16; ++q) rdF0(B0{}, q);
     // nk is even and ≥ 4 (host contract): pairs of tiles keep the buffer index static
     tile3(0, B0{}, T_{}, T_{}, T_{}, F_{});
-    tile3(1, B1{}, F_{}, T_{}, T_{}, F_{});
+    tile3(1, B1{}, F_{}, T_{}, T_{}, F_{}, nk == 4);
     for (int t = 2; t < nk - 2; t += 2) {
       tile3(t, B0{}, F_{}, T_{}, T_{}, F_{});
-      tile3(t + 1, B1{}, F_{}, T_{}, T_{}, F_{});
+      tile3(t + 1, B1{}, F_{}, T_{}, T_{}, F_{}, t + 1 == nk - 3);
     }
     tile3(nk - 2, B0{}, F_{}, T_{}, F_{}, F_{});
-    const int vn = vcur + (int)gridDim.x;
-    has_next = vn < nwg;
-    if (has_next) coords(vn, ntm, ntn);
+    if (!dyn) {
+      vnext = vcur + (int)gridDim.x;
+      has_next = vnext < nwg;
+      if (has_next) coords(vnext, ntm, ntn);
+    }
     tile3(nk - 1, B1{}, F_{}, F_{}, F_{}, T_{});  // issues the next tile's k-tiles 0 and 1 (has_next)
     if (!has_next) break;
     row_epilogue();  // of this tile (m0, n0, tm, halfn)
-    vcur = vn;
+    vcur = vnext;
     tm = ntm;
     tn = ntn;
     m0 = tm * BM;
@@ -538,9 +575,46 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
     halfn = dhalfn;
   }
   row_epilogue();
+  if (dyn && w == 0) {
+    // the last workgroup out resets this launch slot's counters (vector stores)
+    unsigned done = 0;
+    if (lane == 0) done = atomicAdd(sched + 8, 1u);
+    done = __builtin_amdgcn_readfirstlane(done);
+    if (done == gridDim.x - 1 && lane < 9) sched[lane] = 0u;
+  }
 }
 
 }  // namespace
+
+// dynamic tile order: launch slots of 9 counters (8 XCDs + the exit count) in
+// a ring, zero between launches (the kernel's last workgroup resets its slot);
+// a launch inside a graph capture keeps its slot, which every replay leaves
+// zeroed again.  No slot (allocation failed, or a first launch inside a
+// capture): the static order.  Off by default — on one GPU the static order is
+// 0.5 ms/step faster (GPT-2-medium 141.35 vs 141.87 ms, two interleaved
+// rounds); the bucketed DDP turns it on for multi-rank jobs, where RCCL kernels
+// hold CUs during the backward (parallel/ddp.py)
+static int g_nt4_dynamic = 0;
+void gemm_nt4_set_dynamic(int on) { g_nt4_dynamic = on; }
+static unsigned* sched_slot(hipStream_t st) {
+  constexpr int SLOTS = 256, SLOT_U32 = 16;  // one 64-B line per launch
+  static unsigned* ring = nullptr;
+  static std::atomic<unsigned> next{0};
+  if (!g_nt4_dynamic) return nullptr;
+  if (!ring) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    static unsigned* const r = [] {
+      void* p = nullptr;
+      if (hipMalloc(&p, SLOTS * SLOT_U32 * sizeof(unsigned)) != hipSuccess) return (unsigned*)nullptr;
+      if (hipMemset(p, 0, SLOTS * SLOT_U32 * sizeof(unsigned)) != hipSuccess) return (unsigned*)nullptr;
+      return (unsigned*)p;
+    }();
+    ring = r;
+    if (!ring) return nullptr;
+  }
+  return ring + SLOT_U32 * (next.fetch_add(1, std::memory_order_relaxed) % SLOTS);
+}
 
 // one workgroup per CU (a multiple of 8: the XCD mapping)
 static int persistent_grid(long long tiles) {
@@ -567,8 +641,9 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
   // (soab, profiles/r5gd_saved_gelu_grad.md); round 3 had 8 ahead of 4 and 16 on the older epilogues
   constexpr int group_m = 4;
   const int g = persistent_grid(tiles);
+  unsigned* sched = sched_slot(st);
   auto go = [&](auto kern) {
-    kern<<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m);
+    kern<<<g, NTHR, 0, st>>>(A, B, lda, ldb, M, N, nk, C, ldc, bias, Y, ldy, dbias_part, group_m, sched);
     return 0;
   };
   auto launch = [&](auto mir_tag) -> int {

@@ -83,6 +83,14 @@ class BucketedDDP:
         # overlapped pipeline: its collectives are stream-ordered kernels.
         self._serial = (self.enabled and flat.device.type == "cuda" and dist.is_initialized()
                         and dist.get_backend(group) == "gloo")
+        if self.enabled and self.world > 1 and flat.device.type == "cuda" and not self._serial:
+            # RCCL kernels on the overlap stream hold CUs during the backward; a
+            # persistent GEMM with a static tile order would wait for them with
+            # the tiles it was dealt (tools/overlap_probe.py): dynamic order
+            from .. import _native
+            m = _native.hip_ext()
+            if m is not None and hasattr(m, "gemm_nt4_dynamic"):
+                m.gemm_nt4_dynamic(1)
         if self.enabled:
             for s in flat.slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._hook))

@@ -264,3 +264,49 @@ def test_nt_bn_stats_epilogue_vs_fp32(hip, M, N, K):
     var = (part[:, 1].sum(0) + (rows * (part[:, 0] / rows - mean) ** 2).sum(0)) / M
     torch.testing.assert_close(mean, ref.mean(0), rtol=1e-2, atol=2e-3)
     torch.testing.assert_close(var, ref.var(0, unbiased=False), rtol=2e-2, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(65536, 1024, 1024), (65536, 1024, 256), (3328, 50304, 512),
+                                   (2048, 768, 4096)])
+def test_nt4_dynamic_tile_order_matches_static(hip, M, N, K):
+    """The dynamic per-XCD tile order (gemm_nt4_dynamic(1), multi-rank jobs) writes
+    exactly what the static order does — every tile once, the same tile math —
+    across more launches than the counter ring holds (each launch's last
+    workgroup must leave its slot zeroed: a stale counter would skip tiles), with
+    the fused epilogues, on a half-width last tile column and at nk = 4."""
+    x, w, b = _mk(M, N, K, seed=7)
+    y = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    prev = hip.gemm_nt4_dynamic(0)
+    try:
+        ref = (hip.gemm_nt(x, w), hip.gemm_nt(x, w, b), hip.gemm_nt_add(x, w, y))
+        hip.gemm_nt4_dynamic(1)
+        for it in range(300):  # > 256 slots: every slot reused
+            got = hip.gemm_nt(x, w)
+            if it % 50 == 0 or it == 299:
+                assert torch.equal(got, ref[0]), it
+        assert torch.equal(hip.gemm_nt(x, w, b), ref[1])
+        assert torch.equal(hip.gemm_nt_add(x, w, y), ref[2])
+    finally:
+        hip.gemm_nt4_dynamic(prev)
+
+
+def test_nt4_dynamic_tile_order_in_graph_replays(hip):
+    """A dynamic-order launch captured in a HIP graph keeps its counter slot;
+    every replay must find it zeroed again and cover all tiles."""
+    x, w, _ = _mk(65536, 1024, 1024, seed=3)
+    ref = hip.gemm_nt(x, w)
+    prev = hip.gemm_nt4_dynamic(1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        out = hip.gemm_nt(x, w)
+    torch.cuda.current_stream().wait_stream(s)
+    try:
+        for _ in range(5):
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref)
+    finally:
+        hip.gemm_nt4_dynamic(prev)
