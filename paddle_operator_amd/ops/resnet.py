@@ -261,6 +261,15 @@ def _gemm_wgrad_1x1(C, K) -> bool:
     return ((K + 255) // 256) * (C // 256) >= 8
 
 
+def _wt_1x1(ctx, wb, K, C):
+    """Wᵀ [C, K] of a 1×1 weight for its input-gradient GEMM: the view of the
+    step's batched transpose (FlatParams.shadow_t, built with the bf16 shadow in
+    one launch) when the forward read the shadow, else one transpose."""
+    if ctx.wt is not None and ctx.wt.numel() == C * K:
+        return ctx.wt.view(C, K)
+    return transpose(wb.view(K, C))
+
+
 class _ConvFn(torch.autograd.Function):
     """y = conv2d(x, w) for a channels_last bf16 activation on hand-written
     kernels: the NHWC implicit GEMM (csrc/hip/conv.hip) for 3×3 stride 1 / 2 and
@@ -346,7 +355,7 @@ class _ConvFn(torch.autograd.Function):
             No, _, Ho, Wo = dy.shape
             T4 = No * Ho * Wo
             if m.gemm_nt_supported(T4, C, K):
-                g = m.gemm_nt(dy.permute(0, 2, 3, 1).reshape(T4, K), transpose(wb.view(K, C)))
+                g = m.gemm_nt(dy.permute(0, 2, 3, 1).reshape(T4, K), _wt_1x1(ctx, wb, K, C))
                 clink.give(g.view(No, Ho, Wo, C).permute(0, 3, 1, 2))
                 clink = "given"
         if ctx.needs_input_grad[0] and clink != "given":
@@ -354,7 +363,7 @@ class _ConvFn(torch.autograd.Function):
             # BatchNorm then takes its own statistics pass)
             if ctx.one and _gemm_dgrad_1x1(m, T, C, K):
                 dy2 = dy.permute(0, 2, 3, 1).reshape(T, K)
-                wt2 = transpose(wb.view(K, C))
+                wt2 = _wt_1x1(ctx, wb, K, C)
                 dx = (m.gemm_nt_add(dy2, wt2, dalias.permute(0, 2, 3, 1).reshape(T, C), mask=amask)
                       if dalias is not None else m.gemm_nt(dy2, wt2))
                 amask = None

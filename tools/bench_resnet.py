@@ -33,6 +33,10 @@ def main():
         from paddle_operator_amd.ops import resnet as ops_resnet
         ops_resnet._direct_cl_ok = lambda p: (ops_core._direct_ok(p) and p.grad.dtype == torch.float32
                                               and p.grad.is_contiguous(memory_format=torch.channels_last))
+    if os.environ.get("BENCH_WT1X1_PERCALL") == "1":  # A/B: a transpose per 1×1 input gradient (pre round 6)
+        from paddle_operator_amd.ops import resnet as ops_resnet
+        from paddle_operator_amd.ops.core import transpose
+        ops_resnet._wt_1x1 = lambda ctx, wb, K, C: transpose(wb.view(K, C))
     t0 = time.time()
     tr = ResNetTrainer(a.batch, "cuda:0", graph=a.graph)
     for _ in range(a.warmup):
