@@ -590,10 +590,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt4_kernel(const bf16* __restric
 // a ring, zero between launches (the kernel's last workgroup resets its slot);
 // a launch inside a graph capture keeps its slot, which every replay leaves
 // zeroed again.  No slot (allocation failed, or a first launch inside a
-// capture): the static order.  Off by default — on one GPU the static order is
-// 0.5 ms/step faster (GPT-2-medium 141.35 vs 141.87 ms, two interleaved
-// rounds); the bucketed DDP turns it on for multi-rank jobs, where RCCL kernels
-// hold CUs during the backward (parallel/ddp.py)
+// capture): the static order.  Off (gemm_nt4_set_dynamic, for experiments):
+// on one GPU the static order is 0.5 ms/step faster (GPT-2-medium 141.35 vs
+// 141.87 ms), and in a step with CU-holding side kernels launched where the
+// bucketed DDP launches its all-reduces the dynamic order did not recover any
+// of the delay (tools/overlap_step_probe.py: +3.7 ms static vs +4.1 ms dynamic)
+// — a side kernel gets its CU at a kernel boundary and delays whichever kernel
+// comes next, most often not a gemm_nt4 (profiles/r6r_overlap_probe.md)
 static int g_nt4_dynamic = 0;
 void gemm_nt4_set_dynamic(int on) { g_nt4_dynamic = on; }
 static unsigned* sched_slot(hipStream_t st) {

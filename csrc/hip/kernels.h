@@ -182,7 +182,7 @@ int gemm_nt4(const bf16* A, const bf16* B, int M, int N, int K, int lda, int ldb
 // which mainloop gemm_nt() runs: 0 = 8-wave ring (gemm_nt.hip), 1 = 4-wave
 // (gemm_nt4.hip, default)
 void gemm_nt_set_impl(int impl);
-// gemm_nt4 tile order: 1 = dynamic per-XCD counters, 0 = static (default)
+// gemm_nt4 tile order: 1 = dynamic per-XCD counters, 0 = static (default; experiments only)
 void gemm_nt4_set_dynamic(int on);
 int gemm_nt_get_impl();
 int transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);

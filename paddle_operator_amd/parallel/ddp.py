@@ -44,15 +44,6 @@ import torch.distributed as dist
 from .flat import FlatParams
 
 
-def gemm_tile_order(enabled: bool, world: int, device_type: str, serial: bool) -> int:
-    """gemm_nt4's tile order for this job: 1 (dynamic) when RCCL all-reduces
-    run on the overlap stream during the backward — their kernels hold CUs, and a
-    persistent GEMM with the static order waits for a held CU with the tiles it
-    was dealt (tools/overlap_probe.py, profiles/r6r_overlap_probe.md) — else 0
-    (static: 0.5 ms/step faster on one GPU)."""
-    return int(enabled and world > 1 and device_type == "cuda" and not serial)
-
-
 class BucketedDDP:
     def __init__(self, flat: FlatParams, group=None, enabled: bool | None = None, grad_reduce: str | None = None):
         self.flat = flat
@@ -92,11 +83,6 @@ class BucketedDDP:
         # overlapped pipeline: its collectives are stream-ordered kernels.
         self._serial = (self.enabled and flat.device.type == "cuda" and dist.is_initialized()
                         and dist.get_backend(group) == "gloo")
-        if gemm_tile_order(self.enabled, self.world, flat.device.type, self._serial):
-            from .. import _native
-            m = _native.hip_ext()
-            if m is not None and hasattr(m, "gemm_nt4_dynamic"):
-                m.gemm_nt4_dynamic(1)
         if self.enabled:
             for s in flat.slots:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._hook))

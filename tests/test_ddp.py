@@ -510,15 +510,3 @@ def test_legacy_checkpoint_layout_loads():
     with pytest.raises(ValueError):
         flat.load_params(torch.zeros(flat.numel + 1))
 
-
-def test_gemm_tile_order_policy():
-    """gemm_nt4 runs its dynamic tile order exactly for multi-rank GPU jobs whose
-    all-reduces overlap the backward (RCCL); one GPU, CPU ranks and the serial
-    gloo-on-GPU rehearsal keep the static order."""
-    from paddle_operator_amd.parallel.ddp import gemm_tile_order
-    assert gemm_tile_order(True, 8, "cuda", False) == 1
-    assert gemm_tile_order(True, 2, "cuda", False) == 1
-    assert gemm_tile_order(False, 1, "cuda", False) == 0
-    assert gemm_tile_order(True, 1, "cuda", False) == 0  # PDO_DDP_ALWAYS at world 1
-    assert gemm_tile_order(True, 2, "cpu", False) == 0
-    assert gemm_tile_order(True, 2, "cuda", True) == 0  # gloo on GPU tensors
