@@ -269,7 +269,7 @@ def test_nt_bn_stats_epilogue_vs_fp32(hip, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(65536, 1024, 1024), (65536, 1024, 256), (3328, 50304, 512),
                                    (2048, 768, 4096)])
 def test_nt4_dynamic_tile_order_matches_static(hip, M, N, K):
-    """The dynamic per-XCD tile order (gemm_nt4_dynamic(1), multi-rank jobs) writes
+    """The dynamic per-XCD tile order (gemm_nt4_dynamic(1), an experiment switch) writes
     exactly what the static order does — every tile once, the same tile math —
     across more launches than the counter ring holds (each launch's last
     workgroup must leave its slot zeroed: a stale counter would skip tiles), with

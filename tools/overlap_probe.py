@@ -16,7 +16,8 @@ loses ≈ H / 256 of its throughput.
     python tools/overlap_probe.py [--holds 1,3] [--hold-us 300] [--iters 10]
 
 gemm_nt4 runs in both tile orders (static: one GPU; dynamic per-XCD counters:
-what the bucketed DDP selects for multi-rank jobs).
+the experiment switch gemm_nt4_dynamic(1); tools/overlap_step_probe.py
+measures both inside the training step).
 """
 import argparse
 import json
@@ -49,7 +50,7 @@ def main():
     lw, lb = torch.ones(C, **bf), torch.zeros(C, **bf)
     qkv = torch.randn(64, 1024, 3 * C, **bf)
     _, mean, rstd = m.layernorm_fwd(x, lw, lb, 1e-5)[:3]
-    def nt4(order, fn):  # gemm_nt4 with its tile order: 0 static (one GPU), 1 dynamic (multi-rank jobs)
+    def nt4(order, fn):  # gemm_nt4 with its tile order: 0 static (the default), 1 dynamic
         def run_():
             prev = m.gemm_nt4_dynamic(order)
             try:
