@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--every", type=int, default=2)
     ap.add_argument("--hold-us", type=float, default=300.0)
+    ap.add_argument("--side-priority", type=int, default=0,
+                    help="side stream priority (0 default, -1 high: ProcessGroupNCCL's is_high_priority_stream)")
     a = ap.parse_args()
     import torch
     from paddle_operator_amd import _native
@@ -50,7 +52,7 @@ def main():
 
     t4 = once(hog_of(4096))
     hog = hog_of(max(256, int(4096 * a.hold_us / t4) // 128 * 128))
-    side = torch.cuda.Stream(dev)
+    side = torch.cuda.Stream(dev, priority=a.side_priority)
     active = [False]
     launched = [0]
 
@@ -99,7 +101,7 @@ def main():
             res[c].append(round(ms, 3))
             per[c] = n
     m.gemm_nt4_dynamic(0)
-    print(json.dumps({"hooked_params": len(params), "side_kernels_per_step": per, "hold_us": a.hold_us,
+    print(json.dumps({"side_priority": a.side_priority, "hooked_params": len(params), "side_kernels_per_step": per, "hold_us": a.hold_us,
                       "ms_per_step": res, "median": {c: statistics.median(v) for c, v in res.items()}}))
 
 
